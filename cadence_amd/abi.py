@@ -1,0 +1,273 @@
+"""ctypes mirrors of include/cdr/schema.h, include/cdr/cdr.h and include/cdr/synth.h.
+
+The C headers are the source of truth; ``check_layouts()`` compares every mirror's
+size with ``cdr_struct_size`` exported by libcdr so a drift fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+u8, u32, i32, u64, i64, f64 = C.c_uint8, C.c_uint32, C.c_int32, C.c_uint64, C.c_int64, C.c_double
+
+# ------------------------------------------------------------------ constants
+FIRST_EVENT_ID = 1
+EMPTY_EVENT_ID = -23
+EMPTY_VERSION = -24
+
+(STATE_CREATED, STATE_RUNNING, STATE_COMPLETED, STATE_ZOMBIE, STATE_VOID) = range(5)
+(CLOSE_NONE, CLOSE_COMPLETED, CLOSE_FAILED, CLOSE_CANCELED, CLOSE_TERMINATED,
+ CLOSE_CONTINUED_AS_NEW, CLOSE_TIMED_OUT) = range(7)
+TIMEOUT_START_TO_CLOSE, TIMEOUT_SCHEDULE_TO_START, TIMEOUT_SCHEDULE_TO_CLOSE, TIMEOUT_HEARTBEAT = range(4)
+TTS_START_TO_CLOSE, TTS_SCHEDULE_TO_START, TTS_SCHEDULE_TO_CLOSE, TTS_HEARTBEAT = 1, 2, 4, 8
+BUILDER_LOCAL, BUILDER_2DC, BUILDER_NDC = 0, 1, 2
+
+EVENT_TYPES = [
+    "WorkflowExecutionStarted", "WorkflowExecutionCompleted", "WorkflowExecutionFailed",
+    "WorkflowExecutionTimedOut", "DecisionTaskScheduled", "DecisionTaskStarted",
+    "DecisionTaskCompleted", "DecisionTaskTimedOut", "DecisionTaskFailed", "ActivityTaskScheduled",
+    "ActivityTaskStarted", "ActivityTaskCompleted", "ActivityTaskFailed", "ActivityTaskTimedOut",
+    "ActivityTaskCancelRequested", "RequestCancelActivityTaskFailed", "ActivityTaskCanceled",
+    "TimerStarted", "TimerFired", "CancelTimerFailed", "TimerCanceled",
+    "WorkflowExecutionCancelRequested", "WorkflowExecutionCanceled",
+    "RequestCancelExternalWorkflowExecutionInitiated", "RequestCancelExternalWorkflowExecutionFailed",
+    "ExternalWorkflowExecutionCancelRequested", "MarkerRecorded", "WorkflowExecutionSignaled",
+    "WorkflowExecutionTerminated", "WorkflowExecutionContinuedAsNew",
+    "StartChildWorkflowExecutionInitiated", "StartChildWorkflowExecutionFailed",
+    "ChildWorkflowExecutionStarted", "ChildWorkflowExecutionCompleted", "ChildWorkflowExecutionFailed",
+    "ChildWorkflowExecutionCanceled", "ChildWorkflowExecutionTimedOut",
+    "ChildWorkflowExecutionTerminated", "SignalExternalWorkflowExecutionInitiated",
+    "SignalExternalWorkflowExecutionFailed", "ExternalWorkflowExecutionSignaled",
+    "UpsertWorkflowSearchAttributes",
+]
+EV = {name: i for i, name in enumerate(EVENT_TYPES)}
+EVF_BATCH_FIRST = 0x1
+
+STATUS = {
+    0: "OK", 1: "E_HISTORY_EMPTY", 2: "E_NEWRUN_HISTORY_EMPTY", 3: "E_UNKNOWN_EVENT_TYPE",
+    4: "E_INVALID_STATE_TRANSITION", 5: "E_VH_LOWER_VERSION", 6: "E_VH_LOWER_EVENT_ID",
+    7: "E_DECISION_NOT_FOUND", 8: "E_ACTIVITY_NOT_FOUND", 9: "E_ACTIVITY_ID_NOT_FOUND",
+    10: "E_MISSING_ACTIVITY_INFO", 11: "E_DOMAIN_NOT_FOUND", 12: "E_REBUILD_NEXT_EVENT_ID",
+    13: "E_BAD_INPUT", 32: "P_ACTIVITY_STARTED_NIL", 33: "P_CHILD_STARTED_NIL",
+    34: "P_VH_ITEM_INVALID", 35: "P_UNKNOWN_CLUSTER", 64: "NOT_APPLIED",
+}
+OK = 0
+RF_IN_NEWRUN, RF_IS_NEWRUN, RF_NEWRUN_APPLIED = 1, 2, 4
+
+SF_HAS_PARENT_DOMAIN, SF_PARENT_DOMAIN_MISSING, SF_HAS_PARENT_EXEC = 0x1, 0x2, 0x4
+SF_HAS_PARENT_INITIATED, SF_HAS_RETRY, SF_HAS_MEMO, SF_HAS_SEARCH_ATTR = 0x8, 0x10, 0x20, 0x40
+SF_HAS_RESET_POINTS, SF_CRON_INITIATOR = 0x80, 0x100
+AF_HAS_RETRY = 0x1
+XF_DOMAIN_MISSING, XF_CHILD_ONLY = 0x1, 0x2
+RP_HAS_CHECKSUM, RP_HAS_RUN_ID, RP_HAS_FIRST_DC_ID, RP_HAS_CREATED = 0x1, 0x2, 0x4, 0x8
+RP_HAS_EXPIRING, RP_HAS_RESETTABLE, RP_RESETTABLE = 0x10, 0x20, 0x40
+XI_CANCEL_REQUESTED, XI_HAS_RETRY, XI_HAS_EXPIRATION, XI_HAS_BRANCH = 0x1, 0x2, 0x4, 0x8
+XI_HAS_MEMO, XI_HAS_SEARCH_ATTR, XI_HAS_RESET_POINTS, XI_STARTED, XI_VH_BRANCH = 0x10, 0x20, 0x40, 0x80, 0x100
+AI_CANCEL_REQUESTED, AI_HAS_RETRY, AI_STARTED_TIME_SET = 0x1, 0x2, 0x4
+MAX_CLUSTERS = 8
+SLICE_WIDTH = 64
+
+
+def _S(name, fields):
+    return type(name, (C.Structure,), {"_fields_": fields})
+
+
+# ------------------------------------------------------------------ input
+CdrKV = _S("cdr_kv", [("key", u32), ("value", u32)])
+CdrResetPoint = _S("cdr_reset_point", [
+    ("binary_checksum", u32), ("run_id", u32), ("first_decision_completed_id", i64),
+    ("created_time_nano", i64), ("expiring_time_nano", i64), ("flags", u32), ("_pad", u32)])
+AttrStarted = _S("cdr_attr_wf_started", [
+    ("workflow_type", u32), ("task_list", u32), ("cron_schedule", u32), ("flags", u32),
+    ("parent_domain_id", u32), ("parent_workflow_id", u32), ("parent_run_id", u32), ("continued_run_id", u32),
+    ("parent_initiated_id", i64), ("expiration_ts", i64),
+    ("exec_timeout_s", i32), ("task_timeout_s", i32), ("attempt", i32), ("first_decision_backoff_s", i32),
+    ("backoff_coefficient", f64),
+    ("retry_initial_s", i32), ("retry_max_interval_s", i32), ("retry_max_attempts", i32),
+    ("retry_expiration_s", i32), ("nonretriable", u32), ("memo", u32),
+    ("search_attr_off", u32), ("search_attr_len", u32), ("reset_points_off", u32), ("reset_points_len", u32)])
+AttrDTSched = _S("cdr_attr_dt_scheduled", [("attempt", i64), ("start_to_close_s", i32), ("task_list", u32)])
+AttrDT = _S("cdr_attr_dt", [("scheduled_event_id", i64), ("started_event_id", i64), ("request_id", u32),
+                            ("binary_checksum", u32), ("timeout_type", i32), ("_pad", i32)])
+AttrATSched = _S("cdr_attr_at_scheduled", [
+    ("activity_id", u32), ("task_list", u32), ("s2s_s", i32), ("s2c_s", i32), ("stc_s", i32), ("hb_s", i32),
+    ("flags", u32), ("nonretriable", u32), ("retry_initial_s", i32), ("retry_max_interval_s", i32),
+    ("retry_max_attempts", i32), ("retry_expiration_s", i32), ("backoff_coefficient", f64)])
+AttrAT = _S("cdr_attr_at", [("scheduled_event_id", i64), ("started_event_id", i64), ("request_id", u32),
+                            ("activity_id", u32), ("timeout_type", i32), ("attempt", i32)])
+AttrTimer = _S("cdr_attr_timer", [("timer_id", u32), ("_pad", u32), ("start_to_fire_s", i64),
+                                  ("started_event_id", i64)])
+AttrExternal = _S("cdr_attr_external", [
+    ("domain", u32), ("workflow_id", u32), ("run_id", u32), ("workflow_type", u32), ("signal_name", u32),
+    ("input", u32), ("control", u32), ("flags", u32), ("parent_close_policy", i32), ("_pad", i32)])
+AttrRef = _S("cdr_attr_initiated_ref", [("initiated_event_id", i64), ("run_id", u32), ("_pad", u32)])
+AttrCAN = _S("cdr_attr_can", [("new_execution_run_id", u32), ("_pad", u32)])
+AttrUpsert = _S("cdr_attr_upsert", [("search_attr_off", u32), ("search_attr_len", u32)])
+
+
+class AttrUnion(C.Union):
+    _fields_ = [("started", AttrStarted), ("dt_sched", AttrDTSched), ("dt", AttrDT), ("at_sched", AttrATSched),
+                ("at", AttrAT), ("timer", AttrTimer), ("ext", AttrExternal), ("ref", AttrRef), ("can", AttrCAN),
+                ("upsert", AttrUpsert), ("raw", u8 * 112)]
+
+
+CdrEvent = _S("cdr_event", [("event_id", i64), ("version", i64), ("timestamp", i64), ("task_id", i64),
+                            ("type", u32), ("flags", u32), ("a", AttrUnion)])
+CdrWfDesc = _S("cdr_wf_desc", [
+    ("wf_key", u64), ("ev_off", u64), ("ev_len", u64), ("domain_id", u32), ("workflow_id", u32), ("run_id", u32),
+    ("request_id", u32), ("builder", u32), ("retention_days", i32), ("failover_version", i64),
+    ("expected_next_event_id", i64), ("parent", i32), ("newrun", i32), ("newrun_call", u32), ("newrun_ndc", u32)])
+CdrClusterMeta = _S("cdr_cluster_meta", [("failover_version_increment", i64), ("current_cluster", i32),
+                                         ("n_clusters", i32), ("initial_version", i64 * MAX_CLUSTERS)])
+CdrBatch = _S("cdr_batch", [
+    ("events", C.POINTER(CdrEvent)), ("n_events", u64), ("wfs", C.POINTER(CdrWfDesc)), ("n_wfs", u32),
+    ("empty_uuid", u32), ("kvs", C.POINTER(CdrKV)), ("n_kvs", u64), ("rps", C.POINTER(CdrResetPoint)),
+    ("n_rps", u64), ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64)])
+
+# ------------------------------------------------------------------ output
+CdrExecInfo = _S("cdr_exec_info", [
+    ("domain_id", u32), ("workflow_id", u32), ("run_id", u32), ("create_request_id", u32),
+    ("parent_domain_id", u32), ("parent_workflow_id", u32), ("parent_run_id", u32), ("task_list", u32),
+    ("workflow_type", u32), ("decision_request_id", u32), ("cron_schedule", u32), ("memo", u32),
+    ("nonretriable", u32), ("branch_tree_id", u32), ("flags", u32), ("_pad0", u32),
+    ("initiated_id", i64), ("completion_event_batch_id", i64), ("workflow_timeout", i32),
+    ("decision_timeout_value", i32), ("state", i32), ("close_status", i32), ("last_first_event_id", i64),
+    ("last_event_task_id", i64), ("next_event_id", i64), ("last_processed_event", i64), ("signal_count", i32),
+    ("decision_timeout", i32), ("decision_version", i64), ("decision_schedule_id", i64),
+    ("decision_started_id", i64), ("decision_attempt", i64), ("decision_started_ts", i64),
+    ("decision_scheduled_ts", i64), ("decision_original_scheduled_ts", i64), ("attempt", i32),
+    ("initial_interval", i32), ("backoff_coefficient", f64), ("maximum_interval", i32), ("maximum_attempts", i32),
+    ("expiration_time", i64), ("expiration_seconds", i32), ("_pad1", i32), ("branch_id_lo", u64),
+    ("branch_id_hi", u64), ("reset_points_len", u32), ("search_attr_len", u32)])
+CdrReplState = _S("cdr_repl_state", [
+    ("current_version", i64), ("start_version", i64), ("last_write_version", i64), ("last_write_event_id", i64),
+    ("lri_version", i64 * MAX_CLUSTERS), ("lri_last_event_id", i64 * MAX_CLUSTERS), ("lri_mask", u32),
+    ("present", u32)])
+CdrVHItem = _S("cdr_vh_item", [("event_id", i64), ("version", i64)])
+CdrActivityInfo = _S("cdr_activity_info", [
+    ("version", i64), ("schedule_id", i64), ("scheduled_event_batch_id", i64), ("scheduled_time", i64),
+    ("started_id", i64), ("started_time", i64), ("last_heartbeat_time", i64), ("expiration_time", i64),
+    ("cancel_request_id", i64), ("activity_id", u32), ("request_id", u32), ("task_list", u32), ("nonretriable", u32),
+    ("s2s", i32), ("s2c", i32), ("stc", i32), ("hb", i32), ("timer_task_status", i32), ("attempt", i32),
+    ("initial_interval", i32), ("maximum_interval", i32), ("maximum_attempts", i32), ("flags", u32),
+    ("backoff_coefficient", f64)])
+CdrTimerInfo = _S("cdr_timer_info", [("version", i64), ("started_id", i64), ("expiry_time", i64), ("task_id", i64),
+                                     ("timer_id", u32), ("_pad", u32)])
+CdrChildInfo = _S("cdr_child_info", [
+    ("version", i64), ("initiated_id", i64), ("initiated_event_batch_id", i64), ("started_id", i64),
+    ("create_request_lo", u64), ("create_request_hi", u64), ("started_workflow_id", u32), ("started_run_id", u32),
+    ("domain_name", u32), ("workflow_type", u32), ("parent_close_policy", i32), ("_pad", i32)])
+CdrCancelInfo = _S("cdr_cancel_info", [("version", i64), ("initiated_event_batch_id", i64), ("initiated_id", i64),
+                                       ("cancel_request_lo", u64), ("cancel_request_hi", u64)])
+CdrSignalInfo = _S("cdr_signal_info", [
+    ("version", i64), ("initiated_event_batch_id", i64), ("initiated_id", i64), ("signal_request_lo", u64),
+    ("signal_request_hi", u64), ("signal_name", u32), ("input", u32), ("control", u32), ("_pad", u32)])
+CdrWfResult = _S("cdr_wf_result", [
+    ("code", i32), ("flags", u32), ("fail_event_id", i64), ("fail_index", i64), ("n_activity", u32),
+    ("n_timer", u32), ("n_child", u32), ("n_cancel", u32), ("n_signal", u32), ("n_vh", u32),
+    ("n_reset_points", u32), ("n_search_attr", u32)])
+CdrWfCaps = _S("cdr_wf_caps", [
+    ("act_off", u64), ("timer_off", u64), ("child_off", u64), ("cancel_off", u64), ("signal_off", u64),
+    ("vh_off", u64), ("rp_off", u64), ("sa_off", u64), ("act_cap", u32), ("timer_cap", u32), ("child_cap", u32),
+    ("cancel_cap", u32), ("signal_cap", u32), ("vh_cap", u32), ("rp_cap", u32), ("sa_cap", u32)])
+CdrTotals = _S("cdr_totals", [(n, u64) for n in ("act", "timer", "child", "cancel", "signal", "vh", "rp", "sa")])
+CdrOut = _S("cdr_out", [(n, C.c_void_p) for n in (
+    "result", "exec", "repl", "vh", "act", "timer", "child", "cancel", "signal", "rp", "sa")])
+CdrSlices = _S("cdr_slices", [
+    ("n_slices", u32), ("_pad", u32), ("n_rows", u64), ("arena_words", u64)] + [(n, C.c_void_p) for n in (
+        "slice_row0", "slice_len", "lane_wf", "type_flags", "event_id", "version", "timestamp", "task_id", "key",
+        "aux", "h", "n", "arena")])
+CdrDevBatch = _S("cdr_dev_batch", [
+    ("ev", CdrSlices), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
+    ("n_wfs", u32), ("empty_uuid", u32), ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64)])
+
+# ------------------------------------------------------------------ synth
+CdrSynthParams = _S("cdr_synth_params", [
+    ("config", i32), ("n_wfs", u32), ("seed", u64), ("target_len", u32), ("max_len", u32), ("error_rate", f64),
+    ("builder", i32), ("rebuild", i32)])
+CdrSynthSizes = _S("cdr_synth_sizes", [("n_events", u64), ("n_entries", u32), ("_pad", u32), ("n_kvs", u64),
+                                       ("n_rps", u64), ("arena_words", u64)])
+CdrSynthPlanInfo = _S("cdr_synth_plan_info", [
+    ("n_events", u64), ("n_entries", u32), ("n_slices", u32), ("n_rows", u64), ("arena_words", u64),
+    ("n_kvs", u64), ("n_rps", u64), ("totals", CdrTotals)])
+
+MIRRORS = {
+    "cdr_event": CdrEvent, "cdr_wf_desc": CdrWfDesc, "cdr_cluster_meta": CdrClusterMeta, "cdr_batch": CdrBatch,
+    "cdr_kv": CdrKV, "cdr_reset_point": CdrResetPoint, "cdr_attr_wf_started": AttrStarted,
+    "cdr_attr_at_scheduled": AttrATSched, "cdr_exec_info": CdrExecInfo, "cdr_repl_state": CdrReplState,
+    "cdr_vh_item": CdrVHItem, "cdr_activity_info": CdrActivityInfo, "cdr_timer_info": CdrTimerInfo,
+    "cdr_child_info": CdrChildInfo, "cdr_cancel_info": CdrCancelInfo, "cdr_signal_info": CdrSignalInfo,
+    "cdr_wf_result": CdrWfResult, "cdr_wf_caps": CdrWfCaps, "cdr_totals": CdrTotals, "cdr_out": CdrOut,
+    "cdr_slices": CdrSlices, "cdr_dev_batch": CdrDevBatch,
+}
+
+# C ABI entry points declared in include/cdr/cdr.h and include/cdr/synth.h
+EXPORTS = {
+    "cdr_plan_caps": (i32, [C.POINTER(CdrBatch), C.POINTER(CdrWfCaps), C.POINTER(CdrTotals)]),
+    "cdr_plan_slices": (i32, [C.POINTER(CdrWfDesc), u32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(u32),
+                              C.POINTER(u64)]),
+    "cdr_plan_arena_words": (u64, [C.POINTER(CdrBatch)]),
+    "cdr_pack_slices": (i32, [C.POINTER(CdrBatch), C.POINTER(CdrSlices), i32]),
+    "cdr_create": (C.c_void_p, [i32]),
+    "cdr_destroy": (None, [C.c_void_p]),
+    "cdr_replay_sliced_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p]),
+    "cdr_replay_batch": (i32, [C.c_void_p, C.POINTER(CdrBatch), C.POINTER(CdrWfCaps), C.POINTER(CdrTotals),
+                               C.POINTER(CdrOut)]),
+    "cdr_compact_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
+                                C.c_void_p, C.c_void_p]),
+    "cdr_checksum_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p, C.c_void_p]),
+    "cdr_fingerprint32": (u32, [C.c_char_p, C.c_size_t]),
+    "cdr_workflow_id_to_shard": (i32, [C.c_char_p, C.c_size_t, i32]),
+    "cdr_last_kernel_ms": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "cdr_version": (C.c_char_p, []),
+    "cdr_struct_size": (u64, [C.c_char_p]),
+    "cdr_synth_size": (i32, [C.POINTER(CdrSynthParams), C.POINTER(CdrSynthSizes)]),
+    "cdr_synth_fill": (i32, [C.POINTER(CdrSynthParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                             C.POINTER(CdrBatch)]),
+    "cdr_synth_sliced_plan": (i32, [C.POINTER(CdrSynthParams), C.POINTER(CdrSynthPlanInfo)]),
+    "cdr_synth_sliced_fill": (i32, [C.POINTER(CdrSynthParams), C.POINTER(CdrSlices), C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.POINTER(CdrBatch), i32]),
+}
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libcdr.so")
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the in-tree libcdr.so (fails loudly: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check_layouts():
+    """Raise if any ctypes mirror disagrees with the C struct size."""
+    L = lib()
+    bad = []
+    for name, ty in MIRRORS.items():
+        n = L.cdr_struct_size(name.encode())
+        if n != C.sizeof(ty):
+            bad.append((name, n, C.sizeof(ty)))
+    if bad:
+        raise RuntimeError(f"ABI mirror mismatch (name, C, ctypes): {bad}")
+
+
+def np_view(arr, ty):
+    """numpy structured view (no copy) of a ctypes array of `ty`."""
+    return np.frombuffer(arr, dtype=np.dtype((np.void, C.sizeof(ty))))

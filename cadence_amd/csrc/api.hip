@@ -1,0 +1,295 @@
+// api.hip — host pipeline, stream compaction and checksum kernels of libcdr.
+//
+// cdr_replay_batch is the synchronous "hand me decoded histories, give me mutable
+// states" entry point (the batch analogue of stateBuilder.applyEvents); the
+// device-resident path used by the benchmark is cdr_replay_sliced_async.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "cdr/cdr.h"
+
+#define HIPCHK(x)                                                                                     \
+  do {                                                                                                \
+    hipError_t _e = (x);                                                                              \
+    if (_e != hipSuccess) {                                                                           \
+      fprintf(stderr, "cdr: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(_e), __FILE__, __LINE__); \
+      return CDR_API_EDEVICE;                                                                         \
+    }                                                                                                 \
+  } while (0)
+
+struct cdr_ctx;  // defined in replay.hip
+
+namespace {
+
+// dense copy of one pending table: one thread per (workflow, row)
+template <class Row>
+__global__ void k_compact_rows(const cdr_wf_caps* caps, const cdr_wf_result* res, const uint64_t* row_base,
+                               uint32_t n_wfs, int table, const Row* src, Row* dst) {
+  const uint32_t w = blockIdx.x;
+  if (w >= n_wfs) return;
+  const cdr_wf_caps c = caps[w];
+  const cdr_wf_result r = res[w];
+  uint64_t off;
+  uint32_t n;
+  switch (table) {
+    case 0: off = c.act_off; n = r.n_activity; break;
+    case 1: off = c.timer_off; n = r.n_timer; break;
+    case 2: off = c.child_off; n = r.n_child; break;
+    case 3: off = c.cancel_off; n = r.n_cancel; break;
+    default: off = c.signal_off; n = r.n_signal; break;
+  }
+  if (r.code != CDR_OK) n = 0;
+  for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) dst[row_base[w] + j] = src[off + j];
+}
+
+// exclusive scan of per-workflow counts (single block, chunked; counts are small)
+__global__ void k_scan_counts(const cdr_wf_result* res, uint32_t n_wfs, int table, uint64_t* row_base) {
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (n_wfs + blockDim.x - 1) / blockDim.x;
+  const uint32_t b0 = t * per, b1 = min(n_wfs, b0 + per);
+  uint64_t sum = 0;
+  for (uint32_t w = b0; w < b1; w++) {
+    const cdr_wf_result& r = res[w];
+    uint32_t n = table == 0 ? r.n_activity : table == 1 ? r.n_timer : table == 2 ? r.n_child
+               : table == 3 ? r.n_cancel : r.n_signal;
+    sum += r.code == CDR_OK ? n : 0;
+  }
+  part[t] = sum;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t run = 0;
+    for (uint32_t i = 0; i < blockDim.x; i++) {
+      uint64_t v = part[i];
+      part[i] = run;
+      run += v;
+    }
+    row_base[n_wfs] = run;
+  }
+  __syncthreads();
+  uint64_t run = part[t];
+  for (uint32_t w = b0; w < b1; w++) {
+    row_base[w] = run;
+    const cdr_wf_result& r = res[w];
+    uint32_t n = table == 0 ? r.n_activity : table == 1 ? r.n_timer : table == 2 ? r.n_child
+               : table == 3 ? r.n_cancel : r.n_signal;
+    run += r.code == CDR_OK ? n : 0;
+  }
+}
+
+__device__ __forceinline__ uint64_t fold(uint64_t h, uint64_t v) { return cdr_mix64(h ^ v) + 0x9E3779B97F4A7C15ull; }
+__device__ uint64_t hash_bytes(uint64_t h, const void* p, uint32_t bytes) {
+  const uint64_t* q = (const uint64_t*)p;
+  for (uint32_t i = 0; i < bytes / 8; i++) h = fold(h, q[i]);
+  return h;
+}
+
+// per-workflow hash of the whole output record set, summed (order-independent)
+__global__ void k_checksum(cdr_dev_batch B, cdr_out O, unsigned long long* sum) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t h = 0;
+  if (w < B.n_wfs) {
+    const cdr_wf_result r = O.result[w];
+    h = fold(0x5EED, (uint64_t)(uint32_t)r.code | ((uint64_t)r.flags << 32));
+    h = fold(h, (uint64_t)r.fail_event_id);
+    if (r.code == CDR_OK) {
+      const cdr_wf_caps c = B.caps[w];
+      h = hash_bytes(h, &O.exec[w], sizeof(cdr_exec_info));
+      h = hash_bytes(h, &O.repl[w], sizeof(cdr_repl_state));
+      h = hash_bytes(h, O.vh + c.vh_off, r.n_vh * sizeof(cdr_vh_item));
+      h = hash_bytes(h, O.act + c.act_off, r.n_activity * sizeof(cdr_activity_info));
+      h = hash_bytes(h, O.timer + c.timer_off, r.n_timer * sizeof(cdr_timer_info));
+      h = hash_bytes(h, O.child + c.child_off, r.n_child * sizeof(cdr_child_info));
+      h = hash_bytes(h, O.cancel + c.cancel_off, r.n_cancel * sizeof(cdr_cancel_info));
+      h = hash_bytes(h, O.signal + c.signal_off, r.n_signal * sizeof(cdr_signal_info));
+      h = hash_bytes(h, O.rp + c.rp_off, r.n_reset_points * sizeof(cdr_reset_point));
+      h = hash_bytes(h, O.sa + c.sa_off, r.n_search_attr * sizeof(cdr_kv));
+    }
+  }
+  // wave reduction then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_down(h, o, 64);
+  if ((threadIdx.x & 63) == 0 && h) atomicAdd(sum, (unsigned long long)h);
+}
+
+template <class T>
+int dmalloc(T** p, uint64_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  HIPCHK(hipMalloc((void**)p, n * sizeof(T)));
+  return CDR_API_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cdr_compact_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out, void* dense,
+                      uint64_t* row_base, void* stream) {
+  if (!ctx || !in || !out || table < 0 || table > 4) return CDR_API_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, st, out->result, in->n_wfs, table, row_base);
+  HIPCHK(hipGetLastError());
+  const dim3 g(in->n_wfs), b(64);
+  if (in->n_wfs == 0) return CDR_API_OK;
+  switch (table) {
+    case 0:
+      hipLaunchKernelGGL(k_compact_rows<cdr_activity_info>, g, b, 0, st, in->caps, out->result, row_base, in->n_wfs,
+                         table, out->act, (cdr_activity_info*)dense);
+      break;
+    case 1:
+      hipLaunchKernelGGL(k_compact_rows<cdr_timer_info>, g, b, 0, st, in->caps, out->result, row_base, in->n_wfs,
+                         table, out->timer, (cdr_timer_info*)dense);
+      break;
+    case 2:
+      hipLaunchKernelGGL(k_compact_rows<cdr_child_info>, g, b, 0, st, in->caps, out->result, row_base, in->n_wfs,
+                         table, out->child, (cdr_child_info*)dense);
+      break;
+    case 3:
+      hipLaunchKernelGGL(k_compact_rows<cdr_cancel_info>, g, b, 0, st, in->caps, out->result, row_base, in->n_wfs,
+                         table, out->cancel, (cdr_cancel_info*)dense);
+      break;
+    default:
+      hipLaunchKernelGGL(k_compact_rows<cdr_signal_info>, g, b, 0, st, in->caps, out->result, row_base, in->n_wfs,
+                         table, out->signal, (cdr_signal_info*)dense);
+      break;
+  }
+  HIPCHK(hipGetLastError());
+  return CDR_API_OK;
+}
+
+int cdr_checksum_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, uint64_t* dev_sum, void* stream) {
+  if (!ctx || !in || !out || !dev_sum) return CDR_API_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipMemsetAsync(dev_sum, 0, sizeof(uint64_t), st));
+  const uint32_t blocks = (in->n_wfs + 255) / 256;
+  if (blocks)
+    hipLaunchKernelGGL(k_checksum, dim3(blocks), dim3(256), 0, st, *in, *out, (unsigned long long*)dev_sum);
+  HIPCHK(hipGetLastError());
+  return CDR_API_OK;
+}
+
+int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot, cdr_out* out) {
+  if (!ctx || !b || !caps || !tot || !out) return CDR_API_EINVAL;
+  // ---- plan + pack on the host
+  uint32_t ns = 0;
+  uint64_t rows = 0;
+  int rc = cdr_plan_slices(b->wfs, b->n_wfs, nullptr, nullptr, nullptr, &ns, &rows);
+  if (rc) return rc;
+  std::vector<int32_t> lane(ns * (size_t)CDR_SLICE_WIDTH);
+  std::vector<uint32_t> slen(ns);
+  std::vector<uint64_t> row0(ns);
+  rc = cdr_plan_slices(b->wfs, b->n_wfs, lane.data(), slen.data(), row0.data(), &ns, &rows);
+  if (rc) return rc;
+  const uint64_t ne = rows * CDR_SLICE_WIDTH;
+  const uint64_t aw = cdr_plan_arena_words(b);
+  std::vector<uint32_t> tf(ne), hh(ne);
+  std::vector<int64_t> eid(ne), ver(ne), ts(ne), task(ne), key(ne), aux(ne);
+  std::vector<int32_t> nn(ne);
+  std::vector<uint64_t> arena(aw ? aw : 1);
+  cdr_slices hs{};
+  hs.n_slices = ns;
+  hs.n_rows = rows;
+  hs.arena_words = aw;
+  hs.slice_row0 = row0.data();
+  hs.slice_len = slen.data();
+  hs.lane_wf = lane.data();
+  hs.type_flags = tf.data();
+  hs.event_id = eid.data();
+  hs.version = ver.data();
+  hs.timestamp = ts.data();
+  hs.task_id = task.data();
+  hs.key = key.data();
+  hs.aux = aux.data();
+  hs.h = hh.data();
+  hs.n = nn.data();
+  hs.arena = arena.data();
+  rc = cdr_pack_slices(b, &hs, 0);
+  if (rc) return rc;
+
+  // ---- device buffers
+  std::vector<void*> allocs;
+  auto up = [&](const void* src, uint64_t bytes) -> void* {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess) return nullptr;
+    allocs.push_back(p);
+    if (bytes && hipMemcpy(p, src, bytes, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return p;
+  };
+  auto dz = [&](uint64_t bytes) -> void* {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess) return nullptr;
+    allocs.push_back(p);
+    (void)hipMemset(p, 0, bytes ? bytes : 8);
+    return p;
+  };
+  auto free_all = [&]() {
+    for (void* p : allocs) (void)hipFree(p);
+  };
+  cdr_dev_batch db{};
+  db.ev.n_slices = ns;
+  db.ev.n_rows = rows;
+  db.ev.arena_words = aw;
+  db.ev.slice_row0 = (const uint64_t*)up(row0.data(), ns * 8ull);
+  db.ev.slice_len = (const uint32_t*)up(slen.data(), ns * 4ull);
+  db.ev.lane_wf = (const int32_t*)up(lane.data(), lane.size() * 4ull);
+  db.ev.type_flags = (const uint32_t*)up(tf.data(), ne * 4);
+  db.ev.event_id = (const int64_t*)up(eid.data(), ne * 8);
+  db.ev.version = (const int64_t*)up(ver.data(), ne * 8);
+  db.ev.timestamp = (const int64_t*)up(ts.data(), ne * 8);
+  db.ev.task_id = (const int64_t*)up(task.data(), ne * 8);
+  db.ev.key = (const int64_t*)up(key.data(), ne * 8);
+  db.ev.aux = (const int64_t*)up(aux.data(), ne * 8);
+  db.ev.h = (const uint32_t*)up(hh.data(), ne * 4);
+  db.ev.n = (const int32_t*)up(nn.data(), ne * 4);
+  db.ev.arena = (const uint64_t*)up(arena.data(), arena.size() * 8);
+  db.wfs = (const cdr_wf_desc*)up(b->wfs, (uint64_t)b->n_wfs * sizeof(cdr_wf_desc));
+  db.caps = (const cdr_wf_caps*)up(caps, (uint64_t)b->n_wfs * sizeof(cdr_wf_caps));
+  db.kvs = (const cdr_kv*)up(b->kvs, b->n_kvs * sizeof(cdr_kv));
+  db.rps = (const cdr_reset_point*)up(b->rps, b->n_rps * sizeof(cdr_reset_point));
+  db.n_wfs = b->n_wfs;
+  db.empty_uuid = b->empty_uuid;
+  db.cluster = b->cluster;
+  db.now_ns = b->now_ns;
+  db.uuid_seed = b->uuid_seed;
+  cdr_out dout{};
+  dout.result = (cdr_wf_result*)dz((uint64_t)b->n_wfs * sizeof(cdr_wf_result));
+  dout.exec = (cdr_exec_info*)dz((uint64_t)b->n_wfs * sizeof(cdr_exec_info));
+  dout.repl = (cdr_repl_state*)dz((uint64_t)b->n_wfs * sizeof(cdr_repl_state));
+  dout.vh = (cdr_vh_item*)dz(tot->vh * sizeof(cdr_vh_item));
+  dout.act = (cdr_activity_info*)dz(tot->act * sizeof(cdr_activity_info));
+  dout.timer = (cdr_timer_info*)dz(tot->timer * sizeof(cdr_timer_info));
+  dout.child = (cdr_child_info*)dz(tot->child * sizeof(cdr_child_info));
+  dout.cancel = (cdr_cancel_info*)dz(tot->cancel * sizeof(cdr_cancel_info));
+  dout.signal = (cdr_signal_info*)dz(tot->signal * sizeof(cdr_signal_info));
+  dout.rp = (cdr_reset_point*)dz(tot->rp * sizeof(cdr_reset_point));
+  dout.sa = (cdr_kv*)dz(tot->sa * sizeof(cdr_kv));
+  for (void* p : allocs)
+    if (!p) {
+      free_all();
+      return CDR_API_ENOMEM;
+    }
+  rc = cdr_replay_sliced_async(ctx, &db, &dout, nullptr);
+  if (rc == CDR_API_OK && hipDeviceSynchronize() != hipSuccess) rc = CDR_API_EDEVICE;
+  auto down = [&](void* dst, const void* src, uint64_t bytes) {
+    if (rc == CDR_API_OK && dst && bytes && hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = CDR_API_EDEVICE;
+  };
+  down(out->result, dout.result, (uint64_t)b->n_wfs * sizeof(cdr_wf_result));
+  down(out->exec, dout.exec, (uint64_t)b->n_wfs * sizeof(cdr_exec_info));
+  down(out->repl, dout.repl, (uint64_t)b->n_wfs * sizeof(cdr_repl_state));
+  down(out->vh, dout.vh, tot->vh * sizeof(cdr_vh_item));
+  down(out->act, dout.act, tot->act * sizeof(cdr_activity_info));
+  down(out->timer, dout.timer, tot->timer * sizeof(cdr_timer_info));
+  down(out->child, dout.child, tot->child * sizeof(cdr_child_info));
+  down(out->cancel, dout.cancel, tot->cancel * sizeof(cdr_cancel_info));
+  down(out->signal, dout.signal, tot->signal * sizeof(cdr_signal_info));
+  down(out->rp, dout.rp, tot->rp * sizeof(cdr_reset_point));
+  down(out->sa, dout.sa, tot->sa * sizeof(cdr_kv));
+  free_all();
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,516 @@
+// host.cpp — host-side planning and packing for the replay engine (CPU only).
+//
+// The reference decodes each history batch into []*shared.HistoryEvent and walks it
+// in one goroutine (stateBuilder.go:132-601).  Here the host instead lays a whole
+// batch of decoded histories out as sliced columns (cdr.h: "SELL-64") so that one
+// wavefront replays 64 workflows in lockstep with coalesced loads, and sizes the
+// per-workflow output regions the kernels write into.
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <numeric>
+#include <thread>
+#include <vector>
+
+#include "cdr/cdr.h"
+#include "internal.h"
+
+namespace {
+
+// Arena record sizes (8-byte words) of the types that carry one.
+inline uint32_t arena_words_for(uint32_t type) {
+  switch (type) {
+    case CDR_EV_WF_STARTED:
+      return (sizeof(cdr_attr_wf_started) + 7) / 8;
+    case CDR_EV_AT_SCHEDULED:
+      return (sizeof(cdr_attr_at_scheduled) + 7) / 8;
+    default:
+      return 0;
+  }
+}
+
+int hw_threads(int threads) {
+  if (threads > 0) return threads;
+  unsigned h = std::thread::hardware_concurrency();
+  return h ? (int)std::min(h, 64u) : 4;
+}
+
+template <class F>
+void parallel_for(uint64_t n, int threads, F&& f) {
+  threads = hw_threads(threads);
+  if (threads <= 1 || n < 4096) {
+    for (uint64_t i = 0; i < n; i++) f(i);
+    return;
+  }
+  std::atomic<uint64_t> next{0};
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; t++)
+    pool.emplace_back([&] {
+      for (;;) {
+        uint64_t i0 = next.fetch_add(256);
+        if (i0 >= n) break;
+        uint64_t i1 = std::min(n, i0 + 256);
+        for (uint64_t i = i0; i < i1; i++) f(i);
+      }
+    });
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+
+namespace cdr_internal {
+
+uint32_t arena_words_for(uint32_t type) { return ::arena_words_for(type); }
+
+void caps_one(const cdr_event* ev, uint64_t n, cdr_wf_caps* out) {
+  cdr_wf_caps c{};
+  bool have_ver = false;
+  int64_t last_ver = 0;
+  uint32_t vh = 0;
+  for (uint64_t k = 0; k < n; k++) {
+    const cdr_event& e = ev[k];
+    if (!have_ver || e.version > last_ver) {
+      vh++;
+      last_ver = e.version;
+      have_ver = true;
+    }
+    switch (e.type) {
+      case CDR_EV_WF_STARTED:
+        c.rp_cap += e.a.started.reset_points_len;
+        c.sa_cap += e.a.started.search_attr_len;
+        break;
+      case CDR_EV_DT_COMPLETED:
+        if (e.a.dt.binary_checksum) c.rp_cap++;
+        break;
+      case CDR_EV_AT_SCHEDULED:
+        c.act_cap++;
+        break;
+      case CDR_EV_TIMER_STARTED:
+        c.timer_cap++;
+        break;
+      case CDR_EV_CHILD_INITIATED:
+        c.child_cap++;
+        break;
+      case CDR_EV_RCE_INITIATED:
+        c.cancel_cap++;
+        break;
+      case CDR_EV_SE_INITIATED:
+        c.signal_cap++;
+        break;
+      case CDR_EV_UPSERT_SA:
+        c.sa_cap += e.a.upsert.search_attr_len;
+        break;
+      default:
+        break;
+    }
+  }
+  c.vh_cap = vh;
+  *out = c;
+}
+
+void pack_lane(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t len, uint32_t l, uint64_t apos,
+               const cdr_slices* o) {
+  uint32_t* tf = const_cast<uint32_t*>(o->type_flags);
+  int64_t* eid = const_cast<int64_t*>(o->event_id);
+  int64_t* ver = const_cast<int64_t*>(o->version);
+  int64_t* ts = const_cast<int64_t*>(o->timestamp);
+  int64_t* task = const_cast<int64_t*>(o->task_id);
+  int64_t* key = const_cast<int64_t*>(o->key);
+  int64_t* aux = const_cast<int64_t*>(o->aux);
+  uint32_t* hh = const_cast<uint32_t*>(o->h);
+  int32_t* nn = const_cast<int32_t*>(o->n);
+  uint64_t* arena = const_cast<uint64_t*>(o->arena);
+  for (uint32_t k = 0; k < len; k++) {
+    const uint64_t i = (row0 + k) * CDR_SLICE_WIDTH + l;
+    if (k >= n_ev) {
+      tf[i] = CDR_EV_PAD;
+      eid[i] = ver[i] = ts[i] = task[i] = key[i] = aux[i] = 0;
+      hh[i] = 0;
+      nn[i] = 0;
+      continue;
+    }
+    const cdr_event& e = ev[k];
+    uint32_t flags = (e.flags & CDR_EVF_BATCH_FIRST) || k == 0 ? CDR_SEF_BATCH_FIRST : 0;
+    int64_t kk = 0, ax = 0;
+    uint32_t h = 0;
+    int32_t n = 0;
+    switch (e.type) {
+      case CDR_EV_WF_STARTED:
+        ax = (int64_t)apos;
+        std::memcpy(arena + apos, &e.a.started, sizeof(cdr_attr_wf_started));
+        apos += arena_words_for(e.type);
+        break;
+      case CDR_EV_DT_SCHEDULED:
+        ax = e.a.dt_sched.attempt;
+        n = e.a.dt_sched.start_to_close_s;
+        break;
+      case CDR_EV_DT_STARTED:
+        kk = e.a.dt.scheduled_event_id;
+        h = e.a.dt.request_id;
+        break;
+      case CDR_EV_DT_COMPLETED:
+        kk = e.a.dt.scheduled_event_id;
+        ax = e.a.dt.started_event_id;
+        h = e.a.dt.binary_checksum;
+        break;
+      case CDR_EV_DT_TIMED_OUT:
+        n = e.a.dt.timeout_type;
+        break;
+      case CDR_EV_AT_SCHEDULED:
+        kk = e.a.at_sched.activity_id;
+        ax = (int64_t)apos;
+        std::memcpy(arena + apos, &e.a.at_sched, sizeof(cdr_attr_at_scheduled));
+        apos += arena_words_for(e.type);
+        break;
+      case CDR_EV_AT_STARTED:
+        kk = e.a.at.scheduled_event_id;
+        h = e.a.at.request_id;
+        break;
+      case CDR_EV_AT_COMPLETED:
+      case CDR_EV_AT_FAILED:
+      case CDR_EV_AT_TIMED_OUT:
+      case CDR_EV_AT_CANCELED:
+        kk = e.a.at.scheduled_event_id;
+        break;
+      case CDR_EV_AT_CANCEL_REQUESTED:
+      case CDR_EV_AT_REQ_CANCEL_FAILED:
+        kk = e.a.at.activity_id;
+        break;
+      case CDR_EV_TIMER_STARTED:
+        kk = e.a.timer.timer_id;
+        ax = e.a.timer.start_to_fire_s;
+        break;
+      case CDR_EV_TIMER_FIRED:
+      case CDR_EV_TIMER_CANCELED:
+      case CDR_EV_CANCEL_TIMER_FAILED:
+        kk = e.a.timer.timer_id;
+        break;
+      case CDR_EV_CHILD_INITIATED:
+        kk = e.a.ext.domain;
+        ax = e.a.ext.workflow_type;
+        h = e.a.ext.workflow_id;
+        n = e.a.ext.parent_close_policy;
+        if (e.a.ext.flags & CDR_XF_DOMAIN_MISSING) flags |= CDR_SEF_DOMAIN_MISSING;
+        break;
+      case CDR_EV_RCE_INITIATED:
+        kk = e.a.ext.domain;
+        if (e.a.ext.flags & CDR_XF_DOMAIN_MISSING) flags |= CDR_SEF_DOMAIN_MISSING;
+        break;
+      case CDR_EV_SE_INITIATED:
+        kk = e.a.ext.domain;
+        ax = (int64_t)(((uint64_t)e.a.ext.input << 32) | e.a.ext.control);
+        h = e.a.ext.signal_name;
+        if (e.a.ext.flags & CDR_XF_DOMAIN_MISSING) flags |= CDR_SEF_DOMAIN_MISSING;
+        break;
+      case CDR_EV_CHILD_STARTED:
+        kk = e.a.ref.initiated_event_id;
+        h = e.a.ref.run_id;
+        break;
+      case CDR_EV_CHILD_START_FAILED:
+      case CDR_EV_CHILD_COMPLETED:
+      case CDR_EV_CHILD_FAILED:
+      case CDR_EV_CHILD_CANCELED:
+      case CDR_EV_CHILD_TIMED_OUT:
+      case CDR_EV_CHILD_TERMINATED:
+      case CDR_EV_RCE_FAILED:
+      case CDR_EV_EXT_CANCEL_REQUESTED:
+      case CDR_EV_SE_FAILED:
+      case CDR_EV_EXT_SIGNALED:
+        kk = e.a.ref.initiated_event_id;
+        break;
+      case CDR_EV_UPSERT_SA:
+        ax = e.a.upsert.search_attr_off;
+        h = e.a.upsert.search_attr_len;
+        break;
+      case CDR_EV_WF_CONTINUED_AS_NEW:
+        h = e.a.can.new_execution_run_id;
+        break;
+      default:
+        break;
+    }
+    tf[i] = (e.type & 0xFFu) | flags;
+    eid[i] = e.event_id;
+    ver[i] = e.version;
+    ts[i] = e.timestamp;
+    task[i] = e.task_id;
+    key[i] = kk;
+    aux[i] = ax;
+    hh[i] = h;
+    nn[i] = n;
+  }
+}
+
+}  // namespace cdr_internal
+
+extern "C" {
+
+int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
+  if (!b || !caps || !totals) return CDR_API_EINVAL;
+  cdr_totals t{};
+  for (uint32_t w = 0; w < b->n_wfs; w++) {
+    const cdr_wf_desc& d = b->wfs[w];
+    if (d.ev_off + d.ev_len > b->n_events) return CDR_API_EINVAL;
+    // a continue-as-new entry must describe the run the parent's CAN event names
+    // (stateBuilder.go:559-563): same workflow, RunId = NewExecutionRunId, builder
+    // from newRunNDC
+    if (d.newrun >= 0) {
+      if ((uint32_t)d.newrun >= b->n_wfs) return CDR_API_EINVAL;
+      const cdr_wf_desc& n = b->wfs[d.newrun];
+      if (n.parent != (int32_t)w || n.workflow_id != d.workflow_id ||
+          n.builder != (d.newrun_ndc ? (uint32_t)CDR_BUILDER_NDC : (uint32_t)CDR_BUILDER_2DC))
+        return CDR_API_EINVAL;
+      uint32_t call = 0;
+      for (uint64_t k = 0; k < d.ev_len; k++) {
+        const cdr_event& e = b->events[d.ev_off + k];
+        if (k > 0 && (e.flags & CDR_EVF_BATCH_FIRST)) call++;
+        if (call == d.newrun_call && e.type == CDR_EV_WF_CONTINUED_AS_NEW &&
+            e.a.can.new_execution_run_id != n.run_id)
+          return CDR_API_EINVAL;
+      }
+    }
+    cdr_wf_caps c{};
+    cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, &c);
+    c.act_off = t.act;
+    t.act += c.act_cap;
+    c.timer_off = t.timer;
+    t.timer += c.timer_cap;
+    c.child_off = t.child;
+    t.child += c.child_cap;
+    c.cancel_off = t.cancel;
+    t.cancel += c.cancel_cap;
+    c.signal_off = t.signal;
+    t.signal += c.signal_cap;
+    c.vh_off = t.vh;
+    t.vh += c.vh_cap;
+    c.rp_off = t.rp;
+    t.rp += c.rp_cap;
+    c.sa_off = t.sa;
+    t.sa += c.sa_cap;
+    caps[w] = c;
+  }
+  *totals = t;
+  return CDR_API_OK;
+}
+
+int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, uint32_t* slice_len,
+                    uint64_t* slice_row0, uint32_t* n_slices, uint64_t* n_rows) {
+  if (!wfs && n_wfs) return CDR_API_EINVAL;
+  uint32_t ns = (n_wfs + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH;
+  std::vector<uint32_t> order(n_wfs);
+  std::iota(order.begin(), order.end(), 0u);
+  // longest first: a slice's rows = its longest lane, so neighbours in length
+  // share slices and padding stays small (SELL-C-sigma with sigma = batch).
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint32_t a, uint32_t c) { return wfs[a].ev_len > wfs[c].ev_len; });
+  uint64_t rows = 0;
+  for (uint32_t s = 0; s < ns; s++) {
+    uint32_t len = (uint32_t)wfs[order[(size_t)s * CDR_SLICE_WIDTH]].ev_len;
+    if (slice_len) slice_len[s] = len;
+    if (slice_row0) slice_row0[s] = rows;
+    rows += len;
+    if (lane_wf)
+      for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
+        size_t i = (size_t)s * CDR_SLICE_WIDTH + l;
+        lane_wf[i] = i < n_wfs ? (int32_t)order[i] : -1;
+      }
+  }
+  if (n_slices) *n_slices = ns;
+  if (n_rows) *n_rows = rows;
+  return CDR_API_OK;
+}
+
+uint64_t cdr_plan_arena_words(const cdr_batch* b) {
+  uint64_t w = 0;
+  for (uint64_t i = 0; i < b->n_events; i++) w += arena_words_for(b->events[i].type);
+  return w;
+}
+
+int cdr_pack_slices(const cdr_batch* b, cdr_slices* o, int threads) {
+  if (!b || !o) return CDR_API_EINVAL;
+  // arena offsets: per workflow prefix (natural order), records in event order
+  std::vector<uint64_t> arena_base(b->n_wfs + 1, 0);
+  for (uint32_t w = 0; w < b->n_wfs; w++) {
+    const cdr_wf_desc& d = b->wfs[w];
+    uint64_t words = 0;
+    for (uint64_t k = 0; k < d.ev_len; k++) words += arena_words_for(b->events[d.ev_off + k].type);
+    arena_base[w + 1] = arena_base[w] + words;
+  }
+  if (arena_base[b->n_wfs] > o->arena_words) return CDR_API_EINVAL;
+  std::atomic<int> bad{0};
+  parallel_for(o->n_slices, threads, [&](uint64_t s) {
+    const uint64_t row0 = o->slice_row0[s];
+    const uint32_t len = o->slice_len[s];
+    for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
+      const int32_t w = o->lane_wf[s * CDR_SLICE_WIDTH + l];
+      if (w >= 0 && b->wfs[w].ev_len > len) {
+        bad = 1;
+        continue;
+      }
+      if (w >= 0)
+        cdr_internal::pack_lane(b->events + b->wfs[w].ev_off, b->wfs[w].ev_len, row0, len, l, arena_base[w], o);
+      else
+        cdr_internal::pack_lane(nullptr, 0, row0, len, l, 0, o);
+    }
+  });
+  return bad ? CDR_API_EINVAL : CDR_API_OK;
+}
+
+// ---------------------------------------------------------------- farmhash
+// Fingerprint32 == farmhashmk::Hash32 (github.com/dgryski/go-farm
+// v0.0.0-20190423205320-6a90982ecee2, a port of google/farmhash), used by
+// common.WorkflowIDToHistoryShard (common/util.go:249-252).  Restated from the
+// published algorithm; no reference test pins concrete values (parity unpinned,
+// affects partitioning only).
+static inline uint32_t fh_fetch(const unsigned char* p) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return v;
+}
+static inline uint32_t fh_rot(uint32_t v, int s) { return s == 0 ? v : (v >> s) | (v << (32 - s)); }
+static const uint32_t fh_c1 = 0xcc9e2d51u, fh_c2 = 0x1b873593u;
+static inline uint32_t fh_fmix(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+static inline uint32_t fh_mur(uint32_t a, uint32_t h) {
+  a *= fh_c1;
+  a = fh_rot(a, 17);
+  a *= fh_c2;
+  h ^= a;
+  h = fh_rot(h, 19);
+  return h * 5 + 0xe6546b64u;
+}
+static uint32_t fh_len0to4(const unsigned char* s, size_t len) {
+  uint32_t b = 0, c = 9;
+  for (size_t i = 0; i < len; i++) {
+    int8_t v = (int8_t)s[i];
+    b = b * fh_c1 + (uint32_t)(int32_t)v;
+    c ^= b;
+  }
+  return fh_fmix(fh_mur(b, fh_mur((uint32_t)len, c)));
+}
+static uint32_t fh_len5to12(const unsigned char* s, size_t len) {
+  uint32_t a = (uint32_t)len, b = (uint32_t)len * 5, c = 9, d = b;
+  a += fh_fetch(s);
+  b += fh_fetch(s + len - 4);
+  c += fh_fetch(s + ((len >> 1) & 4));
+  return fh_fmix(fh_mur(c, fh_mur(b, fh_mur(a, d))));
+}
+static uint32_t fh_len13to24(const unsigned char* s, size_t len) {
+  uint32_t a = fh_fetch(s - 4 + (len >> 1));
+  uint32_t b = fh_fetch(s + 4);
+  uint32_t c = fh_fetch(s + len - 8);
+  uint32_t d = fh_fetch(s + (len >> 1));
+  uint32_t e = fh_fetch(s);
+  uint32_t f = fh_fetch(s + len - 4);
+  uint32_t h = d * fh_c1 + (uint32_t)len;
+  a = fh_rot(a, 12) + f;
+  h = fh_mur(c, h) + a;
+  a = fh_rot(a, 3) + c;
+  h = fh_mur(e, h) + a;
+  a = fh_rot(a + f, 12) + d;
+  h = fh_mur(b, h) + a;
+  return fh_fmix(h);
+}
+
+uint32_t cdr_fingerprint32(const char* str, size_t len) {
+  const unsigned char* s = (const unsigned char*)str;
+  if (len <= 24) {
+    return len <= 12 ? (len <= 4 ? fh_len0to4(s, len) : fh_len5to12(s, len)) : fh_len13to24(s, len);
+  }
+  uint32_t h = (uint32_t)len, g = fh_c1 * (uint32_t)len, f = g;
+  uint32_t a0 = fh_rot(fh_fetch(s + len - 4) * fh_c1, 17) * fh_c2;
+  uint32_t a1 = fh_rot(fh_fetch(s + len - 8) * fh_c1, 17) * fh_c2;
+  uint32_t a2 = fh_rot(fh_fetch(s + len - 16) * fh_c1, 17) * fh_c2;
+  uint32_t a3 = fh_rot(fh_fetch(s + len - 12) * fh_c1, 17) * fh_c2;
+  uint32_t a4 = fh_rot(fh_fetch(s + len - 20) * fh_c1, 17) * fh_c2;
+  h ^= a0;
+  h = fh_rot(h, 19);
+  h = h * 5 + 0xe6546b64u;
+  h ^= a2;
+  h = fh_rot(h, 19);
+  h = h * 5 + 0xe6546b64u;
+  g ^= a1;
+  g = fh_rot(g, 19);
+  g = g * 5 + 0xe6546b64u;
+  g ^= a3;
+  g = fh_rot(g, 19);
+  g = g * 5 + 0xe6546b64u;
+  f += a4;
+  f = fh_rot(f, 19) + 113;
+  size_t iters = (len - 1) / 20;
+  do {
+    uint32_t a = fh_fetch(s), b = fh_fetch(s + 4), c = fh_fetch(s + 8), d = fh_fetch(s + 12), e = fh_fetch(s + 16);
+    h += a;
+    g += b;
+    f += c;
+    h = fh_mur(d, h) + e;
+    g = fh_mur(c, g) + a;
+    f = fh_mur(b + e * fh_c1, f) + d;
+    f += g;
+    g += f;
+    s += 20;
+  } while (--iters != 0);
+  g = fh_rot(g, 11) * fh_c1;
+  g = fh_rot(g, 17) * fh_c1;
+  f = fh_rot(f, 11) * fh_c1;
+  f = fh_rot(f, 17) * fh_c1;
+  h = fh_rot(h + g, 19);
+  h = h * 5 + 0xe6546b64u;
+  h = fh_rot(h, 17) * fh_c1;
+  h = fh_rot(h + f, 19);
+  h = h * 5 + 0xe6546b64u;
+  h = fh_rot(h, 17) * fh_c1;
+  return h;
+}
+
+int32_t cdr_workflow_id_to_shard(const char* workflow_id, size_t len, int32_t num_shards) {
+  if (num_shards <= 0) return -1;
+  return (int32_t)(cdr_fingerprint32(workflow_id, len) % (uint32_t)num_shards);
+}
+
+const char* cdr_version(void) { return "cadence_amd-cdr 0.1 (gfx950)"; }
+
+}  // extern "C"
+
+extern "C" {
+// sizeof of the ABI structs, so language bindings can verify their mirrors.
+uint64_t cdr_struct_size(const char* name) {
+  struct E {
+    const char* n;
+    uint64_t s;
+  };
+  static const E table[] = {
+      {"cdr_event", sizeof(cdr_event)},
+      {"cdr_wf_desc", sizeof(cdr_wf_desc)},
+      {"cdr_cluster_meta", sizeof(cdr_cluster_meta)},
+      {"cdr_batch", sizeof(cdr_batch)},
+      {"cdr_kv", sizeof(cdr_kv)},
+      {"cdr_reset_point", sizeof(cdr_reset_point)},
+      {"cdr_attr_wf_started", sizeof(cdr_attr_wf_started)},
+      {"cdr_attr_at_scheduled", sizeof(cdr_attr_at_scheduled)},
+      {"cdr_exec_info", sizeof(cdr_exec_info)},
+      {"cdr_repl_state", sizeof(cdr_repl_state)},
+      {"cdr_vh_item", sizeof(cdr_vh_item)},
+      {"cdr_activity_info", sizeof(cdr_activity_info)},
+      {"cdr_timer_info", sizeof(cdr_timer_info)},
+      {"cdr_child_info", sizeof(cdr_child_info)},
+      {"cdr_cancel_info", sizeof(cdr_cancel_info)},
+      {"cdr_signal_info", sizeof(cdr_signal_info)},
+      {"cdr_wf_result", sizeof(cdr_wf_result)},
+      {"cdr_wf_caps", sizeof(cdr_wf_caps)},
+      {"cdr_totals", sizeof(cdr_totals)},
+      {"cdr_out", sizeof(cdr_out)},
+      {"cdr_slices", sizeof(cdr_slices)},
+      {"cdr_dev_batch", sizeof(cdr_dev_batch)},
+  };
+  for (const E& e : table)
+    if (std::strcmp(e.n, name) == 0) return e.s;
+  return 0;
+}
+}  // extern "C"

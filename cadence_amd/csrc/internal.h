@@ -1,0 +1,22 @@
+// internal.h — helpers shared by the host-side translation units of libcdr.
+#pragma once
+#include <cstdint>
+
+#include "cdr/cdr.h"
+
+namespace cdr_internal {
+
+// arena words of the attribute record of `type` (0 if the type has none)
+uint32_t arena_words_for(uint32_t type);
+
+// Output capacities of one history (cdr_plan_caps restricted to one workflow);
+// offsets are left zero.
+void caps_one(const cdr_event* ev, uint64_t n, cdr_wf_caps* c);
+
+// Pack one workflow's events into lane `lane` of a slice whose first row is row0 and
+// whose length is len (rows beyond n are padding).  `apos` is the workflow's arena
+// word offset; kv/rp offsets inside the events are rebased by kv_base/rp_base.
+void pack_lane(const cdr_event* ev, uint64_t n, uint64_t row0, uint32_t len, uint32_t lane, uint64_t apos,
+               const cdr_slices* o);
+
+}  // namespace cdr_internal

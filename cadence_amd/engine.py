@@ -1,0 +1,220 @@
+"""Host-side engine API over libcdr (the MI355X replay engine's C ABI).
+
+``Batch`` is a decoded history batch in the ABI's natural order (one record per
+HistoryEvent, workflows contiguous); ``Outputs`` are the persisted mutable states
+(include/cdr/schema.h).  ``replay(batch)`` runs the HIP path through
+``cdr_replay_batch``; there is no CPU fallback — without the in-tree libcdr.so or a
+GPU it raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+
+TABLES = ("act", "timer", "child", "cancel", "signal", "vh", "rp", "sa")
+TABLE_TYPES = {
+    "act": abi.CdrActivityInfo, "timer": abi.CdrTimerInfo, "child": abi.CdrChildInfo,
+    "cancel": abi.CdrCancelInfo, "signal": abi.CdrSignalInfo, "vh": abi.CdrVHItem, "rp": abi.CdrResetPoint,
+    "sa": abi.CdrKV,
+}
+TABLE_COUNT = {"act": "n_activity", "timer": "n_timer", "child": "n_child", "cancel": "n_cancel",
+               "signal": "n_signal", "vh": "n_vh", "rp": "n_reset_points", "sa": "n_search_attr"}
+
+
+@dataclass
+class Batch:
+    events: C.Array
+    wfs: C.Array
+    kvs: C.Array
+    rps: C.Array
+    cluster: abi.CdrClusterMeta
+    now_ns: int = 1_700_000_000_000_000_000
+    uuid_seed: int = 1
+    empty_uuid: int = 1
+    strings: list = field(default_factory=list)  # handle -> string (fixture batches)
+
+    @property
+    def n_wfs(self):
+        return len(self.wfs)
+
+    def cstruct(self) -> abi.CdrBatch:
+        b = abi.CdrBatch()
+        b.events = C.cast(self.events, C.POINTER(abi.CdrEvent))
+        b.n_events = len(self.events)
+        b.wfs = C.cast(self.wfs, C.POINTER(abi.CdrWfDesc))
+        b.n_wfs = len(self.wfs)
+        b.empty_uuid = self.empty_uuid
+        b.kvs = C.cast(self.kvs, C.POINTER(abi.CdrKV))
+        b.n_kvs = len(self.kvs)
+        b.rps = C.cast(self.rps, C.POINTER(abi.CdrResetPoint))
+        b.n_rps = len(self.rps)
+        b.cluster = self.cluster
+        b.now_ns = self.now_ns
+        b.uuid_seed = self.uuid_seed
+        self._keep = b
+        return b
+
+
+def default_cluster() -> abi.CdrClusterMeta:
+    c = abi.CdrClusterMeta()
+    c.failover_version_increment = 10
+    c.current_cluster = 0
+    c.n_clusters = 3
+    for i, v in enumerate((1, 2, 3)):
+        c.initial_version[i] = v
+    return c
+
+
+def synth_batch(config: int, n_wfs: int, seed: int, target_len: int = 0, max_len: int = 0,
+                error_rate: float = 0.0, builder: int = -1, rebuild: bool = False) -> Batch:
+    """Deterministic synthetic batch (cadence_amd/csrc/synth.cpp) in natural order."""
+    L = abi.lib()
+    p = abi.CdrSynthParams(config=config, n_wfs=n_wfs, seed=seed, target_len=target_len, max_len=max_len,
+                           error_rate=error_rate, builder=builder, rebuild=1 if rebuild else 0)
+    sz = abi.CdrSynthSizes()
+    rc = L.cdr_synth_size(C.byref(p), C.byref(sz))
+    if rc:
+        raise RuntimeError(f"cdr_synth_size rc={rc}")
+    ev = (abi.CdrEvent * max(1, sz.n_events))()
+    wfs = (abi.CdrWfDesc * sz.n_entries)()
+    kvs = (abi.CdrKV * max(1, sz.n_kvs))()
+    rps = (abi.CdrResetPoint * max(1, sz.n_rps))()
+    cb = abi.CdrBatch()
+    rc = L.cdr_synth_fill(C.byref(p), ev, wfs, kvs, rps, C.byref(cb))
+    if rc:
+        raise RuntimeError(f"cdr_synth_fill rc={rc}")
+    ev = (abi.CdrEvent * sz.n_events).from_buffer(ev) if sz.n_events else (abi.CdrEvent * 0)()
+    kvs = (abi.CdrKV * sz.n_kvs).from_buffer(kvs) if sz.n_kvs else (abi.CdrKV * 0)()
+    rps = (abi.CdrResetPoint * sz.n_rps).from_buffer(rps) if sz.n_rps else (abi.CdrResetPoint * 0)()
+    return Batch(events=ev, wfs=wfs, kvs=kvs, rps=rps, cluster=cb.cluster, now_ns=cb.now_ns,
+                 uuid_seed=cb.uuid_seed, empty_uuid=cb.empty_uuid)
+
+
+@dataclass
+class Plan:
+    caps: C.Array
+    totals: abi.CdrTotals
+
+
+def plan(batch: Batch) -> Plan:
+    L = abi.lib()
+    caps = (abi.CdrWfCaps * max(1, batch.n_wfs))()
+    tot = abi.CdrTotals()
+    rc = L.cdr_plan_caps(C.byref(batch.cstruct()), caps, C.byref(tot))
+    if rc:
+        raise RuntimeError(f"cdr_plan_caps rc={rc}")
+    return Plan(caps=caps, totals=tot)
+
+
+class Outputs:
+    """Host buffers for one batch's persisted mutable states (zero-initialised)."""
+
+    def __init__(self, batch: Batch, pl: Plan):
+        n = max(1, batch.n_wfs)
+        self.n_wfs = batch.n_wfs
+        self.plan = pl
+        self.result = (abi.CdrWfResult * n)()
+        self.exec = (abi.CdrExecInfo * n)()
+        self.repl = (abi.CdrReplState * n)()
+        self.tables = {t: (TABLE_TYPES[t] * max(1, getattr(pl.totals, t)))() for t in TABLES}
+
+    def cstruct(self) -> abi.CdrOut:
+        o = abi.CdrOut()
+        o.result = C.addressof(self.result)
+        o.exec = C.addressof(self.exec)
+        o.repl = C.addressof(self.repl)
+        for t in TABLES:
+            setattr(o, t, C.addressof(self.tables[t]))
+        self._keep = o
+        return o
+
+    # ---- per-workflow accessors
+    def rows(self, w: int, table: str):
+        r = self.result[w]
+        c = self.plan.caps[w]
+        off = getattr(c, {"act": "act_off", "timer": "timer_off", "child": "child_off", "cancel": "cancel_off",
+                          "signal": "signal_off", "vh": "vh_off", "rp": "rp_off", "sa": "sa_off"}[table])
+        n = getattr(r, TABLE_COUNT[table])
+        return [self.tables[table][off + j] for j in range(n)]
+
+
+class Engine:
+    """One device context (the analogue of one stateBuilder provider)."""
+
+    def __init__(self, device: int = 0):
+        L = abi.lib()
+        self.ctx = L.cdr_create(device)
+        if not self.ctx:
+            raise RuntimeError("cdr_create failed: no usable HIP device (the engine has no CPU fallback)")
+
+    def close(self):
+        if self.ctx:
+            abi.lib().cdr_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def replay(self, batch: Batch, pl: Plan | None = None) -> Outputs:
+        pl = pl or plan(batch)
+        out = Outputs(batch, pl)
+        rc = abi.lib().cdr_replay_batch(self.ctx, C.byref(batch.cstruct()), pl.caps, C.byref(pl.totals),
+                                       C.byref(out.cstruct()))
+        if rc:
+            raise RuntimeError(f"cdr_replay_batch rc={rc}")
+        return out
+
+
+# ------------------------------------------------------------------ comparison
+def _bytes(x) -> bytes:
+    return bytes(memoryview(x).cast("B"))
+
+
+def compare(batch: Batch, a: Outputs, b: Outputs, limit: int = 10):
+    """Field-by-field comparison of two output sets (result of every workflow; the
+    persisted state of every OK workflow).  Returns a list of mismatch strings."""
+    bad = []
+    for w in range(batch.n_wfs):
+        ra, rb = a.result[w], b.result[w]
+        ka = (ra.code, ra.flags, ra.fail_event_id, ra.fail_index)
+        kb = (rb.code, rb.flags, rb.fail_event_id, rb.fail_index)
+        if ka != kb:
+            bad.append(f"wf {w}: result {ka} != {kb}")
+        elif ra.code == abi.OK:
+            if _bytes(a.exec[w]) != _bytes(b.exec[w]):
+                diffs = [f for f, _ in abi.CdrExecInfo._fields_
+                         if getattr(a.exec[w], f) != getattr(b.exec[w], f)]
+                bad.append(f"wf {w}: exec differs in {diffs}")
+            if batch.wfs[w].builder == abi.BUILDER_2DC and _bytes(a.repl[w]) != _bytes(b.repl[w]):
+                bad.append(f"wf {w}: replication state differs")
+            for t in TABLES:
+                na, nb = getattr(ra, TABLE_COUNT[t]), getattr(rb, TABLE_COUNT[t])
+                if na != nb:
+                    bad.append(f"wf {w}: {t} count {na} != {nb}")
+                    continue
+                xa = b"".join(_bytes(r) for r in a.rows(w, t))
+                xb = b"".join(_bytes(r) for r in b.rows(w, t))
+                if xa != xb:
+                    rows_a, rows_b = a.rows(w, t), b.rows(w, t)
+                    for j, (p, q) in enumerate(zip(rows_a, rows_b)):
+                        fd = [f for f, _ in type(p)._fields_ if _bytes(p) != _bytes(q) and
+                              getattr(p, f) != getattr(q, f)]
+                        if fd:
+                            bad.append(f"wf {w}: {t}[{j}] differs in {fd}")
+                            break
+        if len(bad) >= limit:
+            break
+    return bad
+
+
+def status_histogram(out: Outputs) -> dict:
+    codes = np.array([out.result[w].code for w in range(out.n_wfs)], dtype=np.int64)
+    vals, cnt = np.unique(codes, return_counts=True)
+    return {abi.STATUS.get(int(v), str(int(v))): int(c) for v, c in zip(vals, cnt)}

@@ -1,0 +1,154 @@
+/*
+ * cdr/cdr.h — C ABI of the MI355X workflow-history replay engine (libcdr.so).
+ *
+ * Drop-in boundary for the reference's replay hot path.  Each entry point names
+ * the reference interface it replaces (paths relative to /root/reference):
+ *
+ *   stateBuilder.applyEvents            service/history/stateBuilder.go:38-52,112-611
+ *     -> cdr_replay_batch (many workflows, each a sequence of applyEvents calls on a
+ *        fresh mutable state) and cdr_replay_sliced (same, device-resident input)
+ *   stateBuilderProvider / newStateBuilder
+ *                                       service/history/historyReplicator.go:54,144
+ *                                       service/history/nDCHistoryReplicator.go:136-141
+ *     -> cdr_create / cdr_destroy (one context per goroutine-equivalent / stream)
+ *   nDCStateRebuilder.rebuild batch loop service/history/nDCStateRebuilder.go:92-160
+ *     -> cdr_replay_batch with cdr_wf_desc.expected_next_event_id set
+ *   common.WorkflowIDToHistoryShard     common/util.go:249-252
+ *     -> cdr_workflow_id_to_shard (farmhash Fingerprint32 % numShards)
+ *
+ * Conventions: plain C, caller-owned buffers, no exceptions across the boundary.
+ * Every call is synchronous on the stream it is given unless named *_async.
+ * Return value: 0 on success, a negative CDR_API_* code on API misuse / device
+ * failure.  Per-workflow replay outcomes (the Go `error` of applyEvents) are in
+ * cdr_wf_result.code, never in the return value.
+ */
+#ifndef CDR_CDR_H
+#define CDR_CDR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cdr/schema.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CDR_API_OK 0
+#define CDR_API_EINVAL (-1)   /* bad arguments / inconsistent batch */
+#define CDR_API_ENODEV (-2)   /* no HIP device or kernel image not loadable */
+#define CDR_API_EDEVICE (-3)  /* HIP runtime error */
+#define CDR_API_ENOMEM (-4)
+
+#define CDR_SLICE_WIDTH 64 /* workflows per slice = one wavefront */
+
+/* Sliced event layout ("SELL-64"): workflows are grouped 64 to a slice (one lane
+ * each, slices sorted by length); event k of lane L of slice s lives at element
+ * (slice_row0[s] + k) * 64 + L of every column, so a wavefront that walks its 64
+ * histories in lockstep reads each column fully coalesced. */
+typedef struct cdr_slices {
+  uint32_t n_slices, _pad;
+  uint64_t n_rows;        /* sum of slice_len */
+  uint64_t arena_words;   /* 8-byte words of attribute records */
+  const uint64_t* slice_row0; /* [n_slices] */
+  const uint32_t* slice_len;  /* [n_slices] */
+  const int32_t* lane_wf;     /* [n_slices*64] workflow index, -1 = empty lane */
+  /* event columns, [n_rows*64] each */
+  const uint32_t* type_flags; /* bits 0-7 cdr_event_type, 8+ CDR_SEF_* */
+  const int64_t* event_id;
+  const int64_t* version;
+  const int64_t* timestamp;
+  const int64_t* task_id;
+  const int64_t* key; /* entity key: scheduled/initiated event id, activity/timer handle ... */
+  const int64_t* aux; /* second operand or arena word offset (type-dependent) */
+  const uint32_t* h;  /* string handle operand (type-dependent) */
+  const int32_t* n;   /* small integer operand (type-dependent) */
+  const uint64_t* arena; /* WorkflowExecutionStarted / ActivityTaskScheduled attribute records */
+} cdr_slices;
+
+#define CDR_SEF_BATCH_FIRST (1u << 8)
+#define CDR_SEF_DOMAIN_MISSING (1u << 9)
+
+/* everything the device needs for one replay launch (all pointers device memory) */
+typedef struct cdr_dev_batch {
+  cdr_slices ev;
+  const cdr_wf_desc* wfs; /* [n_wfs] */
+  const cdr_wf_caps* caps; /* [n_wfs] */
+  const cdr_kv* kvs;
+  const cdr_reset_point* rps;
+  uint32_t n_wfs;
+  uint32_t empty_uuid; /* handle of "emptyUuid" (mutableStateBuilder.go:42) */
+  cdr_cluster_meta cluster;
+  int64_t now_ns;
+  uint64_t uuid_seed;
+} cdr_dev_batch;
+
+/* ------------------------------------------------------------ host planning */
+
+/* Per-workflow output capacities (upper bounds derived from the input: counts of
+ * entity-creating events, version runs, reset points, search-attribute pairs)
+ * and their prefix offsets. */
+int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals);
+
+/* Slice assignment: workflows sorted by event count (descending, stable) and
+ * dealt 64 to a slice.  Outputs lane_wf[n_slices*64], slice_len[n_slices],
+ * slice_row0[n_slices]; returns n_slices via *n_slices and rows via *n_rows.
+ * Call with lane_wf == NULL to query sizes only. */
+int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, uint32_t* slice_len,
+                    uint64_t* slice_row0, uint32_t* n_slices, uint64_t* n_rows);
+
+/* Arena words needed by the batch's attribute records. */
+uint64_t cdr_plan_arena_words(const cdr_batch* b);
+
+/* Pack the natural-order batch into the sliced columns (host memory, sized by the
+ * planners above).  Columns are passed through a cdr_slices whose pointers are
+ * cast away from const by the packer.  `threads` host threads (<=0: hardware). */
+int cdr_pack_slices(const cdr_batch* b, cdr_slices* out, int threads);
+
+/* ------------------------------------------------------------- device entry */
+
+typedef struct cdr_ctx cdr_ctx;
+cdr_ctx* cdr_create(int device);
+void cdr_destroy(cdr_ctx* ctx);
+
+/* Replay a device-resident sliced batch into device-resident outputs on `stream`
+ * (a hipStream_t; NULL = default stream).  Asynchronous: enqueues the replay
+ * kernel and the continue-as-new finalize kernel and returns. */
+int cdr_replay_sliced_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, void* stream);
+
+/* Whole pipeline for host-resident data: plan + pack + H2D + replay + D2H.
+ * `caps` must come from cdr_plan_caps on the same batch; `out` points at host
+ * buffers sized by its totals.  Synchronous. */
+int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* totals,
+                     cdr_out* out);
+
+/* Stream compaction of the per-workflow pending tables into dense tables
+ * (device pointers): for each table, rows [caps.off, caps.off + result.n) of every
+ * workflow are copied to dense[row_base[w] ...]; row_base is an exclusive scan of
+ * the counts (written to `row_base` [n_wfs+1]).  Tables: 0 activity, 1 timer,
+ * 2 child, 3 cancel, 4 signal. */
+int cdr_compact_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out, void* dense,
+                      uint64_t* row_base, void* stream);
+
+/* Order-independent 64-bit checksum of every OK workflow's outputs (sum over
+ * workflows of a per-workflow hash) — reduced across GPUs with RCCL by the
+ * multi-GPU driver.  Writes one u64 to `*dev_sum` (device memory). */
+int cdr_checksum_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, uint64_t* dev_sum,
+                       void* stream);
+
+/* ------------------------------------------------------------------ misc */
+
+/* farmhash Fingerprint32(workflowID) % numShards (common/util.go:249-252) */
+uint32_t cdr_fingerprint32(const char* s, size_t len);
+int32_t cdr_workflow_id_to_shard(const char* workflow_id, size_t len, int32_t num_shards);
+
+/* Kernel statistics of the last replay launch on ctx: average duration (ms) of
+ * the replay kernel measured with HIP events on the launch stream. */
+int cdr_last_kernel_ms(cdr_ctx* ctx, float* replay_ms, float* finalize_ms);
+
+const char* cdr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CDR_CDR_H */

@@ -1,0 +1,495 @@
+/*
+ * cdr/schema.h — data model of the batched workflow-history replay engine.
+ *
+ * This header restates the reference's persisted-state vocabulary (Uber Cadence,
+ * mounted read-only at /root/reference) as plain C types that are shared by the
+ * host packer, the HIP kernels and the test oracle.  Every constant cites the
+ * reference definition it mirrors.
+ *
+ *   event types        .gen/go/shared/shared.go:16404-16445   (EventType 0..41)
+ *   sentinels          common/constants.go:28-41
+ *   states/close stat. common/persistence/dataInterfaces.go:87-105
+ *   timer-task status  service/history/timerBuilder.go:36-47
+ *   timeout types      .gen/go/shared/shared.go:47934-47937
+ *   persisted records  common/persistence/dataInterfaces.go:259-331,610-706
+ *
+ * Strings and byte blobs never cross into the kernels: the host interns them into
+ * u32 handles (0 == "" / nil) and every string-valued field below is a handle.
+ * Nondeterministic values of the reference (uuid.New(), timeSource.Now()) are
+ * injected: a per-call `now_ns` and a seeded UUID function (cdr_uuid below).
+ */
+#ifndef CDR_SCHEMA_H
+#define CDR_SCHEMA_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define CDR_HD __host__ __device__ __forceinline__
+#else
+#define CDR_HD static inline
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- constants */
+
+/* common/constants.go:28-41 */
+#define CDR_FIRST_EVENT_ID ((int64_t)1)
+#define CDR_EMPTY_EVENT_ID ((int64_t)-23)
+#define CDR_EMPTY_VERSION ((int64_t)-24)
+#define CDR_BUFFERED_EVENT_ID ((int64_t)-123)
+#define CDR_TRANSIENT_EVENT_ID ((int64_t)-124)
+
+/* common/persistence/dataInterfaces.go:87-94 */
+enum cdr_wf_state {
+  CDR_STATE_CREATED = 0,
+  CDR_STATE_RUNNING = 1,
+  CDR_STATE_COMPLETED = 2,
+  CDR_STATE_ZOMBIE = 3,
+  CDR_STATE_VOID = 4
+};
+
+/* common/persistence/dataInterfaces.go:97-105 */
+enum cdr_close_status {
+  CDR_CLOSE_NONE = 0,
+  CDR_CLOSE_COMPLETED = 1,
+  CDR_CLOSE_FAILED = 2,
+  CDR_CLOSE_CANCELED = 3,
+  CDR_CLOSE_TERMINATED = 4,
+  CDR_CLOSE_CONTINUED_AS_NEW = 5,
+  CDR_CLOSE_TIMED_OUT = 6
+};
+
+/* service/history/timerBuilder.go:36-47 */
+#define CDR_TIMER_TASK_STATUS_NONE 0
+#define CDR_TIMER_TASK_STATUS_CREATED 1
+#define CDR_TTS_START_TO_CLOSE 1
+#define CDR_TTS_SCHEDULE_TO_START 2
+#define CDR_TTS_SCHEDULE_TO_CLOSE 4
+#define CDR_TTS_HEARTBEAT 8
+
+/* .gen/go/shared/shared.go:47934-47937 */
+enum cdr_timeout_type {
+  CDR_TIMEOUT_START_TO_CLOSE = 0,
+  CDR_TIMEOUT_SCHEDULE_TO_START = 1,
+  CDR_TIMEOUT_SCHEDULE_TO_CLOSE = 2,
+  CDR_TIMEOUT_HEARTBEAT = 3
+};
+
+/* .gen/go/shared/shared.go:16404-16445 */
+enum cdr_event_type {
+  CDR_EV_WF_STARTED = 0,
+  CDR_EV_WF_COMPLETED = 1,
+  CDR_EV_WF_FAILED = 2,
+  CDR_EV_WF_TIMED_OUT = 3,
+  CDR_EV_DT_SCHEDULED = 4,
+  CDR_EV_DT_STARTED = 5,
+  CDR_EV_DT_COMPLETED = 6,
+  CDR_EV_DT_TIMED_OUT = 7,
+  CDR_EV_DT_FAILED = 8,
+  CDR_EV_AT_SCHEDULED = 9,
+  CDR_EV_AT_STARTED = 10,
+  CDR_EV_AT_COMPLETED = 11,
+  CDR_EV_AT_FAILED = 12,
+  CDR_EV_AT_TIMED_OUT = 13,
+  CDR_EV_AT_CANCEL_REQUESTED = 14,
+  CDR_EV_AT_REQ_CANCEL_FAILED = 15,
+  CDR_EV_AT_CANCELED = 16,
+  CDR_EV_TIMER_STARTED = 17,
+  CDR_EV_TIMER_FIRED = 18,
+  CDR_EV_CANCEL_TIMER_FAILED = 19,
+  CDR_EV_TIMER_CANCELED = 20,
+  CDR_EV_WF_CANCEL_REQUESTED = 21,
+  CDR_EV_WF_CANCELED = 22,
+  CDR_EV_RCE_INITIATED = 23, /* RequestCancelExternalWorkflowExecutionInitiated */
+  CDR_EV_RCE_FAILED = 24,    /* RequestCancelExternalWorkflowExecutionFailed */
+  CDR_EV_EXT_CANCEL_REQUESTED = 25,
+  CDR_EV_MARKER_RECORDED = 26,
+  CDR_EV_WF_SIGNALED = 27,
+  CDR_EV_WF_TERMINATED = 28,
+  CDR_EV_WF_CONTINUED_AS_NEW = 29,
+  CDR_EV_CHILD_INITIATED = 30, /* StartChildWorkflowExecutionInitiated */
+  CDR_EV_CHILD_START_FAILED = 31,
+  CDR_EV_CHILD_STARTED = 32,
+  CDR_EV_CHILD_COMPLETED = 33,
+  CDR_EV_CHILD_FAILED = 34,
+  CDR_EV_CHILD_CANCELED = 35,
+  CDR_EV_CHILD_TIMED_OUT = 36,
+  CDR_EV_CHILD_TERMINATED = 37,
+  CDR_EV_SE_INITIATED = 38, /* SignalExternalWorkflowExecutionInitiated */
+  CDR_EV_SE_FAILED = 39,
+  CDR_EV_EXT_SIGNALED = 40,
+  CDR_EV_UPSERT_SA = 41,
+  CDR_EV_NUM_TYPES = 42,
+  CDR_EV_PAD = 0xFF /* padding slot of the sliced layout; never a real event */
+};
+
+/* event flags (cdr_event.flags and the high bits of the sliced type column) */
+#define CDR_EVF_BATCH_FIRST 0x1u /* first event of an applyEvents call (stateBuilder.go:124) */
+
+/* builder kinds: which replication structure the mutable state carries
+ * (mutableStateBuilder.go:137-231) */
+enum cdr_builder {
+  CDR_BUILDER_LOCAL = 0, /* newMutableStateBuilder */
+  CDR_BUILDER_2DC = 1,   /* ...WithReplicationState */
+  CDR_BUILDER_NDC = 2    /* ...WithVersionHistories */
+};
+
+/* ------------------------------------------------------------- status codes */
+/* One code per Go error / panic site on the replay path.  Order of sites inside
+ * one event follows stateBuilder.go:132-600 exactly. */
+enum cdr_status {
+  CDR_OK = 0,
+  CDR_E_HISTORY_EMPTY = 1,          /* stateBuilder.go:121-123 */
+  CDR_E_NEWRUN_HISTORY_EMPTY = 2,   /* stateBuilder.go:538-540 */
+  CDR_E_UNKNOWN_EVENT_TYPE = 3,     /* stateBuilder.go:597-599 BadRequestError */
+  CDR_E_INVALID_STATE_TRANSITION = 4, /* workflowExecutionInfo.go:45-147 */
+  CDR_E_VH_LOWER_VERSION = 5,       /* versionHistory.go:215-220 */
+  CDR_E_VH_LOWER_EVENT_ID = 6,      /* versionHistory.go:222-227 */
+  CDR_E_DECISION_NOT_FOUND = 7,     /* mutableStateDecisionTaskManager.go:212-215 */
+  CDR_E_ACTIVITY_NOT_FOUND = 8,     /* DeleteActivity mutableStateBuilder.go:1251-1256 */
+  CDR_E_ACTIVITY_ID_NOT_FOUND = 9,  /* DeleteActivity mutableStateBuilder.go:1259-1264 */
+  CDR_E_MISSING_ACTIVITY_INFO = 10, /* ReplicateActivityTaskCancelRequested :2270-2273 */
+  CDR_E_DOMAIN_NOT_FOUND = 11,      /* domain cache lookups stateBuilder.go:162,365,417,448 */
+  CDR_E_REBUILD_NEXT_EVENT_ID = 12, /* nDCStateRebuilder.go:139-143 */
+  CDR_E_BAD_INPUT = 13,             /* malformed batch (host validation) */
+  CDR_P_ACTIVITY_STARTED_NIL = 32,  /* nil deref mutableStateBuilder.go:2089-2091 */
+  CDR_P_CHILD_STARTED_NIL = 33,     /* nil deref mutableStateBuilder.go:3319-3320 */
+  CDR_P_VH_ITEM_INVALID = 34,       /* NewVersionHistoryItem panic versionHistory.go:36-42 */
+  CDR_P_UNKNOWN_CLUSTER = 35,       /* ClusterNameForFailoverVersion panic metadata.go:193-200 */
+  CDR_NOT_APPLIED = 64              /* new-run history never applied (parent stopped first) */
+};
+/* cdr_wf_result.flags */
+#define CDR_RF_IN_NEWRUN 0x1u      /* error raised while replaying newRunHistory */
+#define CDR_RF_IS_NEWRUN 0x2u      /* this entry is a continue-as-new run */
+#define CDR_RF_NEWRUN_APPLIED 0x4u /* parent applied its newRunHistory */
+
+/* --------------------------------------------------------- injected values */
+/* Deterministic stand-in for pborman/uuid.New(): 128 bits from (seed, workflow key,
+ * call site, event id).  Sites: */
+enum cdr_uuid_site {
+  CDR_UUID_BRANCH = 1,     /* NewHistoryBranchToken BranchID dataInterfaces.go:2429 */
+  CDR_UUID_CHILD_REQ = 2,  /* stateBuilder.go:357 createRequestID */
+  CDR_UUID_CANCEL_REQ = 3, /* stateBuilder.go:410 cancelRequestID */
+  CDR_UUID_SIGNAL_REQ = 4, /* stateBuilder.go:441 signalRequestID */
+  CDR_UUID_NEWRUN_REQ = 5, /* stateBuilder.go:566 requestID of the new run */
+  CDR_UUID_NEWRUN_KEY = 6  /* derives the new run's workflow key from its parent's */
+};
+
+CDR_HD uint64_t cdr_mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+CDR_HD void cdr_uuid(uint64_t seed, uint64_t wf_key, uint32_t site, int64_t event_id,
+                     uint64_t* lo, uint64_t* hi) {
+  uint64_t a = cdr_mix64(seed ^ cdr_mix64(wf_key));
+  uint64_t b = cdr_mix64(a ^ ((uint64_t)site << 56) ^ (uint64_t)event_id);
+  *lo = b;
+  *hi = cdr_mix64(b ^ 0xD6E8FEB86659FD93ull);
+}
+
+/* ============================================================ HOST INPUT ===
+ * The decoded history a caller hands over: one record per HistoryEvent, workflows
+ * contiguous, events in eventId order, call (batch) boundaries flagged.  Attribute
+ * union members mirror the thrift attribute structs (shared.thrift:492-700) and
+ * carry only the fields the replay path reads.                                */
+
+/* list element types (auxiliary tables addressed by off/len pairs) */
+typedef struct cdr_kv {      /* map<string, binary> entry (SearchAttributes.IndexedFields) */
+  uint32_t key, value;
+} cdr_kv;
+
+#define CDR_RP_HAS_CHECKSUM 0x01u
+#define CDR_RP_HAS_RUN_ID 0x02u
+#define CDR_RP_HAS_FIRST_DC_ID 0x04u
+#define CDR_RP_HAS_CREATED 0x08u
+#define CDR_RP_HAS_EXPIRING 0x10u
+#define CDR_RP_HAS_RESETTABLE 0x20u
+#define CDR_RP_RESETTABLE 0x40u
+typedef struct cdr_reset_point { /* shared.ResetPointInfo */
+  uint32_t binary_checksum, run_id;
+  int64_t first_decision_completed_id;
+  int64_t created_time_nano;
+  int64_t expiring_time_nano;
+  uint32_t flags, _pad;
+} cdr_reset_point;
+
+/* WorkflowExecutionStartedEventAttributes */
+#define CDR_SF_HAS_PARENT_DOMAIN 0x001u    /* ParentWorkflowDomain != nil */
+#define CDR_SF_PARENT_DOMAIN_MISSING 0x002u /* domain-cache lookup failed (host-resolved) */
+#define CDR_SF_HAS_PARENT_EXEC 0x004u      /* ParentWorkflowExecution != nil */
+#define CDR_SF_HAS_PARENT_INITIATED 0x008u /* ParentInitiatedEventId != nil */
+#define CDR_SF_HAS_RETRY 0x010u            /* RetryPolicy != nil */
+#define CDR_SF_HAS_MEMO 0x020u             /* Memo != nil */
+#define CDR_SF_HAS_SEARCH_ATTR 0x040u      /* SearchAttributes != nil */
+#define CDR_SF_HAS_RESET_POINTS 0x080u     /* PrevAutoResetPoints != nil && Points != nil */
+#define CDR_SF_CRON_INITIATOR 0x100u       /* Initiator == CronSchedule (tasks only) */
+typedef struct cdr_attr_wf_started {
+  uint32_t workflow_type, task_list, cron_schedule, flags;
+  uint32_t parent_domain_id, parent_workflow_id, parent_run_id, continued_run_id;
+  int64_t parent_initiated_id;
+  int64_t expiration_ts; /* ExpirationTimestamp, 0 = unset */
+  int32_t exec_timeout_s, task_timeout_s, attempt, first_decision_backoff_s;
+  double backoff_coefficient;
+  int32_t retry_initial_s, retry_max_interval_s, retry_max_attempts, retry_expiration_s;
+  uint32_t nonretriable, memo;
+  uint32_t search_attr_off, search_attr_len;   /* -> cdr_kv table */
+  uint32_t reset_points_off, reset_points_len; /* -> cdr_reset_point table */
+} cdr_attr_wf_started;
+
+typedef struct cdr_attr_dt_scheduled { /* DecisionTaskScheduledEventAttributes */
+  int64_t attempt;
+  int32_t start_to_close_s;
+  uint32_t task_list;
+} cdr_attr_dt_scheduled;
+
+typedef struct cdr_attr_dt { /* DecisionTask{Started,Completed,TimedOut,Failed} */
+  int64_t scheduled_event_id;
+  int64_t started_event_id;
+  uint32_t request_id;      /* Started */
+  uint32_t binary_checksum; /* Completed */
+  int32_t timeout_type;     /* TimedOut */
+  int32_t _pad;
+} cdr_attr_dt;
+
+#define CDR_AF_HAS_RETRY 0x1u
+typedef struct cdr_attr_at_scheduled { /* ActivityTaskScheduledEventAttributes */
+  uint32_t activity_id, task_list;
+  int32_t s2s_s, s2c_s, stc_s, hb_s;
+  uint32_t flags, nonretriable;
+  int32_t retry_initial_s, retry_max_interval_s, retry_max_attempts, retry_expiration_s;
+  double backoff_coefficient;
+} cdr_attr_at_scheduled;
+
+typedef struct cdr_attr_at { /* ActivityTask{Started,Completed,Failed,TimedOut,Canceled,CancelRequested} */
+  int64_t scheduled_event_id;
+  int64_t started_event_id;
+  uint32_t request_id;  /* Started */
+  uint32_t activity_id; /* CancelRequested / RequestCancelActivityTaskFailed */
+  int32_t timeout_type; /* TimedOut */
+  int32_t attempt;      /* Started (not read by replay) */
+} cdr_attr_at;
+
+typedef struct cdr_attr_timer { /* Timer{Started,Fired,Canceled}, CancelTimerFailed */
+  uint32_t timer_id, _pad;
+  int64_t start_to_fire_s; /* Started */
+  int64_t started_event_id;
+} cdr_attr_timer;
+
+#define CDR_XF_DOMAIN_MISSING 0x1u /* target/child domain-cache lookup failed */
+#define CDR_XF_CHILD_ONLY 0x2u
+typedef struct cdr_attr_external { /* StartChild/SignalExternal/RequestCancelExternal ...Initiated */
+  uint32_t domain, workflow_id, run_id, workflow_type;
+  uint32_t signal_name, input, control, flags;
+  int32_t parent_close_policy, _pad;
+} cdr_attr_external;
+
+typedef struct cdr_attr_initiated_ref { /* every event that closes an external/child entity */
+  int64_t initiated_event_id;
+  uint32_t run_id; /* ChildWorkflowExecutionStarted.WorkflowExecution.RunId */
+  uint32_t _pad;
+} cdr_attr_initiated_ref;
+
+typedef struct cdr_attr_can { /* WorkflowExecutionContinuedAsNewEventAttributes */
+  uint32_t new_execution_run_id, _pad;
+} cdr_attr_can;
+
+typedef struct cdr_attr_upsert { /* UpsertWorkflowSearchAttributesEventAttributes */
+  uint32_t search_attr_off, search_attr_len;
+} cdr_attr_upsert;
+
+typedef struct cdr_event {
+  int64_t event_id;
+  int64_t version;
+  int64_t timestamp;
+  int64_t task_id;
+  uint32_t type;  /* cdr_event_type */
+  uint32_t flags; /* CDR_EVF_* */
+  union {
+    cdr_attr_wf_started started;
+    cdr_attr_dt_scheduled dt_sched;
+    cdr_attr_dt dt;
+    cdr_attr_at_scheduled at_sched;
+    cdr_attr_at at;
+    cdr_attr_timer timer;
+    cdr_attr_external ext;
+    cdr_attr_initiated_ref ref;
+    cdr_attr_can can;
+    cdr_attr_upsert upsert;
+    uint8_t raw[112];
+  } a;
+} cdr_event;
+
+/* Per-workflow replay request: the arguments of one stateBuilder.applyEvents
+ * sequence on a fresh mutable state (stateBuilder.go:112-119, builders
+ * mutableStateBuilder.go:137-231).  A continue-as-new run is its own entry
+ * (parent >= 0) so that it replays in parallel with its parent. */
+typedef struct cdr_wf_desc {
+  uint64_t wf_key;         /* stable key for cdr_uuid (host-assigned) */
+  uint64_t ev_off, ev_len; /* events in cdr_batch.events */
+  uint32_t domain_id, workflow_id, run_id, request_id; /* handles */
+  uint32_t builder;        /* cdr_builder */
+  int32_t retention_days;  /* domainEntry.GetRetentionDays(workflowID) */
+  int64_t failover_version; /* domainEntry.GetFailoverVersion() */
+  int64_t expected_next_event_id; /* nDCStateRebuilder check, 0 = none */
+  int32_t parent;          /* index of the parent entry, -1 = none */
+  int32_t newrun;          /* index of the new-run entry, -1 = none */
+  uint32_t newrun_call;    /* call ordinal (0-based) whose newRunHistory is `newrun` */
+  uint32_t newrun_ndc;     /* newRunNDC argument of that call */
+} cdr_wf_desc;
+
+#define CDR_MAX_CLUSTERS 8
+/* cluster.Metadata restated (common/cluster/metadata.go:187-203) */
+typedef struct cdr_cluster_meta {
+  int64_t failover_version_increment;
+  int32_t current_cluster;   /* index of the current cluster */
+  int32_t n_clusters;
+  int64_t initial_version[CDR_MAX_CLUSTERS]; /* cluster i owns versions with v % inc == initial_version[i] */
+} cdr_cluster_meta;
+
+typedef struct cdr_batch {
+  const cdr_event* events;
+  uint64_t n_events;
+  const cdr_wf_desc* wfs;
+  uint32_t n_wfs;
+  uint32_t empty_uuid; /* handle the host interned for "emptyUuid" (mutableStateBuilder.go:42) */
+  const cdr_kv* kvs;
+  uint64_t n_kvs;
+  const cdr_reset_point* rps;
+  uint64_t n_rps;
+  cdr_cluster_meta cluster;
+  int64_t now_ns;     /* injected timeSource.Now() */
+  uint64_t uuid_seed; /* injected uuid.New() */
+} cdr_batch;
+
+/* =========================================================== OUTPUT =======
+ * The persisted WorkflowMutableState (dataInterfaces.go:610-622) as fixed-stride
+ * records.  Fields that the replay path never writes (StartTimestamp,
+ * LastUpdatedTimestamp, ExecutionContext, CompletionEvent, CancelRequestID,
+ * Sticky*, Client*, SignalRequestedIDs, BufferedEvents) are omitted: they stay
+ * at their zero value on a fresh builder. */
+
+#define CDR_XI_CANCEL_REQUESTED 0x001u
+#define CDR_XI_HAS_RETRY 0x002u
+#define CDR_XI_HAS_EXPIRATION 0x004u   /* ExpirationTime is not the Go zero time */
+#define CDR_XI_HAS_BRANCH 0x008u       /* ExecutionInfo.BranchToken set (non-NDC builders) */
+#define CDR_XI_HAS_MEMO 0x010u
+#define CDR_XI_HAS_SEARCH_ATTR 0x020u  /* SearchAttributes map non-nil */
+#define CDR_XI_HAS_RESET_POINTS 0x040u /* AutoResetPoints non-nil */
+#define CDR_XI_STARTED 0x080u          /* a WorkflowExecutionStarted event was applied */
+#define CDR_XI_VH_BRANCH 0x100u        /* branch_* fields hold the NDC VersionHistory token */
+typedef struct cdr_exec_info {
+  uint32_t domain_id, workflow_id, run_id, create_request_id;
+  uint32_t parent_domain_id, parent_workflow_id, parent_run_id, task_list;
+  uint32_t workflow_type, decision_request_id, cron_schedule, memo;
+  uint32_t nonretriable, branch_tree_id, flags, _pad0;
+  int64_t initiated_id, completion_event_batch_id;
+  int32_t workflow_timeout, decision_timeout_value;
+  int32_t state, close_status;
+  int64_t last_first_event_id, last_event_task_id, next_event_id, last_processed_event;
+  int32_t signal_count, decision_timeout;
+  int64_t decision_version, decision_schedule_id, decision_started_id, decision_attempt;
+  int64_t decision_started_ts, decision_scheduled_ts, decision_original_scheduled_ts;
+  int32_t attempt, initial_interval;
+  double backoff_coefficient;
+  int32_t maximum_interval, maximum_attempts;
+  int64_t expiration_time;
+  int32_t expiration_seconds, _pad1;
+  uint64_t branch_id_lo, branch_id_hi;
+  uint32_t reset_points_len, search_attr_len;
+} cdr_exec_info;
+
+/* ReplicationState (dataInterfaces.go:325-331) + LastReplicationInfo map keyed by
+ * cluster index (bit i of lri_mask = entry present) */
+typedef struct cdr_repl_state {
+  int64_t current_version, start_version, last_write_version, last_write_event_id;
+  int64_t lri_version[CDR_MAX_CLUSTERS];
+  int64_t lri_last_event_id[CDR_MAX_CLUSTERS];
+  uint32_t lri_mask, present;
+} cdr_repl_state;
+
+typedef struct cdr_vh_item { int64_t event_id, version; } cdr_vh_item;
+
+#define CDR_AI_CANCEL_REQUESTED 0x1u
+#define CDR_AI_HAS_RETRY 0x2u
+#define CDR_AI_STARTED_TIME_SET 0x4u /* StartedTime / LastHeartBeatUpdatedTime non-zero */
+typedef struct cdr_activity_info { /* ActivityInfo dataInterfaces.go:625-662 */
+  int64_t version, schedule_id, scheduled_event_batch_id, scheduled_time;
+  int64_t started_id, started_time, last_heartbeat_time, expiration_time;
+  int64_t cancel_request_id;
+  uint32_t activity_id, request_id, task_list, nonretriable;
+  int32_t s2s, s2c, stc, hb;
+  int32_t timer_task_status, attempt;
+  int32_t initial_interval, maximum_interval;
+  int32_t maximum_attempts;
+  uint32_t flags;
+  double backoff_coefficient;
+} cdr_activity_info;
+
+typedef struct cdr_timer_info { /* TimerInfo dataInterfaces.go:665-671 */
+  int64_t version, started_id, expiry_time, task_id;
+  uint32_t timer_id, _pad;
+} cdr_timer_info;
+
+typedef struct cdr_child_info { /* ChildExecutionInfo dataInterfaces.go:674-687 */
+  int64_t version, initiated_id, initiated_event_batch_id, started_id;
+  uint64_t create_request_lo, create_request_hi;
+  uint32_t started_workflow_id, started_run_id, domain_name, workflow_type;
+  int32_t parent_close_policy, _pad;
+} cdr_child_info;
+
+typedef struct cdr_cancel_info { /* RequestCancelInfo dataInterfaces.go:690-695 */
+  int64_t version, initiated_event_batch_id, initiated_id;
+  uint64_t cancel_request_lo, cancel_request_hi;
+} cdr_cancel_info;
+
+typedef struct cdr_signal_info { /* SignalInfo dataInterfaces.go:698-706 */
+  int64_t version, initiated_event_batch_id, initiated_id;
+  uint64_t signal_request_lo, signal_request_hi;
+  uint32_t signal_name, input, control, _pad;
+} cdr_signal_info;
+
+/* per-workflow result: status + where each variable-length table lives */
+typedef struct cdr_wf_result {
+  int32_t code;   /* cdr_status */
+  uint32_t flags; /* CDR_RF_* */
+  int64_t fail_event_id; /* eventId of the event that raised `code` */
+  int64_t fail_index;    /* index of that event within the entry's events */
+  uint32_t n_activity, n_timer, n_child, n_cancel, n_signal, n_vh;
+  uint32_t n_reset_points, n_search_attr;
+} cdr_wf_result;
+
+/* Output capacities: one slot range per workflow and table; filled by
+ * cdr_plan() from the input (counts of creating events, version runs, ...). */
+typedef struct cdr_wf_caps {
+  uint64_t act_off, timer_off, child_off, cancel_off, signal_off, vh_off, rp_off, sa_off;
+  uint32_t act_cap, timer_cap, child_cap, cancel_cap, signal_cap, vh_cap, rp_cap, sa_cap;
+} cdr_wf_caps;
+
+typedef struct cdr_totals {
+  uint64_t act, timer, child, cancel, signal, vh, rp, sa;
+} cdr_totals;
+
+/* Caller-allocated output buffers (host or device memory, per the entry point). */
+typedef struct cdr_out {
+  cdr_wf_result* result;   /* [n_wfs] */
+  cdr_exec_info* exec;     /* [n_wfs] */
+  cdr_repl_state* repl;    /* [n_wfs] */
+  cdr_vh_item* vh;         /* [totals.vh]  (per-wf slice at caps.vh_off) */
+  cdr_activity_info* act;  /* [totals.act] */
+  cdr_timer_info* timer;   /* [totals.timer] */
+  cdr_child_info* child;   /* [totals.child] */
+  cdr_cancel_info* cancel; /* [totals.cancel] */
+  cdr_signal_info* signal; /* [totals.signal] */
+  cdr_reset_point* rp;     /* [totals.rp] */
+  cdr_kv* sa;              /* [totals.sa] */
+} cdr_out;
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CDR_SCHEMA_H */

@@ -1,0 +1,42 @@
+/*
+ * cdr/synth.h — deterministic synthetic workflow histories (libcdr test/bench
+ * utility, not part of the replay path).  Shapes: SURVEY §8(d) configs 1-5 after
+ * canary/echo.go:55-79 and common/testing/history_event_util.go:51-960.
+ */
+#ifndef CDR_SYNTH_H
+#define CDR_SYNTH_H
+#include "cdr/cdr.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+typedef struct cdr_synth_params {
+  int32_t config;       /* 1..5 = SURVEY §8(d) configs; 0 = mixed random walk (tests) */
+  uint32_t n_wfs;       /* top-level workflows (continue-as-new runs are added) */
+  uint64_t seed;
+  uint32_t target_len;  /* median history length (0 = config default) */
+  uint32_t max_len;     /* cap (0 = 204800, service.go:264) */
+  double error_rate;    /* fraction of workflows with one injected fault */
+  int32_t builder;      /* -1 = config default, else cdr_builder */
+  int32_t rebuild;      /* set expected_next_event_id (nDCStateRebuilder check) */
+} cdr_synth_params;
+typedef struct cdr_synth_sizes {
+  uint64_t n_events;
+  uint32_t n_entries, _pad;
+  uint64_t n_kvs, n_rps, arena_words;
+} cdr_synth_sizes;
+typedef struct cdr_synth_plan_info {
+  uint64_t n_events;
+  uint32_t n_entries, n_slices;
+  uint64_t n_rows, arena_words, n_kvs, n_rps;
+  cdr_totals totals;
+} cdr_synth_plan_info;
+int cdr_synth_size(const cdr_synth_params* p, cdr_synth_sizes* out);
+int cdr_synth_fill(const cdr_synth_params* p, cdr_event* ev, cdr_wf_desc* wfs, cdr_kv* kvs, cdr_reset_point* rps,
+                   cdr_batch* b);
+int cdr_synth_sliced_plan(const cdr_synth_params* p, cdr_synth_plan_info* info);
+int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc* wfs, cdr_wf_caps* caps,
+                          cdr_kv* kvs, cdr_reset_point* rps, cdr_batch* meta, int threads);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,48 @@
+"""TEST INFRASTRUCTURE ONLY: Python binding of the CPU restatement (replay_ref.cpp).
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+parity checker / CPU baseline.  The product (cadence_amd/) never imports this.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libcdr_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        from cadence_amd import abi
+        L = C.CDLL(LIB)
+        L.cdro_replay_batch.restype = C.c_int
+        L.cdro_replay_batch.argtypes = [C.POINTER(abi.CdrBatch), C.POINTER(abi.CdrWfCaps), C.POINTER(abi.CdrOut),
+                                        C.c_int]
+        L.cdro_vh_add_or_update.restype = C.c_int
+        L.cdro_vh_add_or_update.argtypes = [C.POINTER(abi.CdrVHItem), C.POINTER(C.c_uint32), C.c_uint32,
+                                            C.c_int64, C.c_int64]
+        L.cdro_state_transition.restype = C.c_int
+        L.cdro_state_transition.argtypes = [C.c_int] * 4
+        _lib = L
+    return _lib
+
+
+def replay(batch, pl=None, threads: int = 1):
+    """Oracle replay of a cadence_amd.engine.Batch into host Outputs."""
+    from cadence_amd import engine
+    pl = pl or engine.plan(batch)
+    out = engine.Outputs(batch, pl)
+    rc = lib().cdro_replay_batch(C.byref(batch.cstruct()), pl.caps, C.byref(out.cstruct()), threads)
+    if rc:
+        raise RuntimeError(f"cdro_replay_batch rc={rc}")
+    return out
