@@ -9,6 +9,7 @@
 #include <atomic>
 #include <cstring>
 #include <numeric>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -44,15 +45,22 @@ void parallel_for(uint64_t n, int threads, F&& f) {
   }
   std::atomic<uint64_t> next{0};
   std::vector<std::thread> pool;
-  for (int t = 0; t < threads; t++)
-    pool.emplace_back([&] {
-      for (;;) {
-        uint64_t i0 = next.fetch_add(256);
-        if (i0 >= n) break;
-        uint64_t i1 = std::min(n, i0 + 256);
-        for (uint64_t i = i0; i < i1; i++) f(i);
-      }
-    });
+  auto work = [&] {
+    for (;;) {
+      uint64_t i0 = next.fetch_add(256);
+      if (i0 >= n) break;
+      uint64_t i1 = std::min(n, i0 + 256);
+      for (uint64_t i = i0; i < i1; i++) f(i);
+    }
+  };
+  for (int t = 1; t < threads; t++) {
+    try {
+      pool.emplace_back(work);
+    } catch (const std::system_error&) {
+      break;  // thread limit reached: the caller's thread still drains the queue
+    }
+  }
+  work();
   for (auto& th : pool) th.join();
 }
 

@@ -15,6 +15,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstring>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -576,15 +577,22 @@ void par(uint32_t n, int threads, F&& f) {
   threads = threads_for(threads);
   std::atomic<uint32_t> next{0};
   std::vector<std::thread> pool;
-  for (int t = 0; t < threads; t++)
-    pool.emplace_back([&] {
-      for (;;) {
-        uint32_t i0 = next.fetch_add(64);
-        if (i0 >= n) break;
-        uint32_t i1 = std::min(n, i0 + 64);
-        for (uint32_t i = i0; i < i1; i++) f(i);
-      }
-    });
+  auto work = [&] {
+    for (;;) {
+      uint32_t i0 = next.fetch_add(64);
+      if (i0 >= n) break;
+      uint32_t i1 = std::min(n, i0 + 64);
+      for (uint32_t i = i0; i < i1; i++) f(i);
+    }
+  };
+  for (int t = 1; t < threads && n > 64; t++) {
+    try {
+      pool.emplace_back(work);
+    } catch (const std::system_error&) {
+      break;  // thread limit reached: the caller's thread still drains the queue
+    }
+  }
+  work();
   for (auto& th : pool) th.join();
 }
 

@@ -218,3 +218,54 @@ def status_histogram(out: Outputs) -> dict:
     codes = np.array([out.result[w].code for w in range(out.n_wfs)], dtype=np.int64)
     vals, cnt = np.unique(codes, return_counts=True)
     return {abi.STATUS.get(int(v), str(int(v))): int(c) for v, c in zip(vals, cnt)}
+
+
+# ------------------------------------------------------------------ export
+_HANDLE_FIELDS = {
+    "domain_id", "workflow_id", "run_id", "create_request_id", "parent_domain_id", "parent_workflow_id",
+    "parent_run_id", "task_list", "workflow_type", "decision_request_id", "cron_schedule", "memo", "nonretriable",
+    "branch_tree_id", "activity_id", "request_id", "timer_id", "started_workflow_id", "started_run_id",
+    "domain_name", "signal_name", "input", "control", "binary_checksum", "key", "value",
+}
+
+
+def _rec(x, strings):
+    d = {}
+    for f, ty in type(x)._fields_:
+        if f.startswith("_pad"):
+            continue
+        v = getattr(x, f)
+        if hasattr(v, "__len__") and not isinstance(v, (bytes, str)):
+            v = list(v)
+        elif strings and f in _HANDLE_FIELDS:
+            v = strings[v] if v < len(strings) else v
+        elif isinstance(v, float):
+            v = float.hex(v)  # bit-exact float in JSON
+        d[f] = v
+    return d
+
+
+def export_state(batch: Batch, out: Outputs, w: int) -> dict:
+    """JSON-able persisted state of workflow `w` (handles mapped to strings when the
+    batch carries its string table)."""
+    s = batch.strings or None
+    r = out.result[w]
+    d = {"result": _rec(r, None)}
+    d["result"]["status"] = abi.STATUS.get(r.code, str(r.code))
+    if r.code == abi.OK:
+        d["exec"] = _rec(out.exec[w], s)
+        if batch.wfs[w].builder == abi.BUILDER_2DC:
+            d["repl"] = _rec(out.repl[w], s)
+        for t in TABLES:
+            d[t] = [_rec(x, s) for x in out.rows(w, t)]
+    return d
+
+
+def state_digest(batch: Batch, out: Outputs) -> str:
+    """sha256 over the exported states of every workflow (golden-fixture pin)."""
+    import hashlib
+    import json
+    h = hashlib.sha256()
+    for w in range(batch.n_wfs):
+        h.update(json.dumps(export_state(batch, out, w), sort_keys=True).encode())
+    return h.hexdigest()

@@ -35,6 +35,7 @@
 #include <cstdint>
 #include <cstring>
 #include <map>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -1141,16 +1142,23 @@ int cdro_replay_batch(const cdr_batch* b, const cdr_wf_caps* caps, cdr_out* out,
   }
   std::atomic<uint32_t> next{0};
   std::vector<std::thread> pool;
-  for (int t = 0; t < threads; t++)
-    pool.emplace_back([&] {
-      for (;;) {
-        uint32_t w0 = next.fetch_add(64);
-        if (w0 >= b->n_wfs) break;
-        uint32_t w1 = std::min(b->n_wfs, w0 + 64);
-        for (uint32_t w = w0; w < w1; w++)
-          if (b->wfs[w].parent < 0) replay_one(b, &ctx, w, caps, out);
-      }
-    });
+  auto work = [&] {
+    for (;;) {
+      uint32_t w0 = next.fetch_add(64);
+      if (w0 >= b->n_wfs) break;
+      uint32_t w1 = std::min(b->n_wfs, w0 + 64);
+      for (uint32_t w = w0; w < w1; w++)
+        if (b->wfs[w].parent < 0) replay_one(b, &ctx, w, caps, out);
+    }
+  };
+  for (int t = 1; t < threads; t++) {
+    try {
+      pool.emplace_back(work);
+    } catch (const std::system_error&) {
+      break;
+    }
+  }
+  work();
   for (auto& th : pool) th.join();
   return 0;
 }

@@ -1,0 +1,146 @@
+"""CPU-only checks of the C-ABI library: it loads, exports every symbol the headers
+declare, its struct layouts match the Python mirrors, and the host-side planner and
+packer are correct (no GPU compute is called here)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from cadence_amd import abi, engine
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    names = set()
+    for h in ("cdr.h", "synth.h"):
+        src = open(os.path.join(ROOT, "include", "cdr", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(cdr_[a-z0-9_]+)\s*\(", src))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    L = abi.lib()
+    declared = _declared()
+    assert len(declared) >= 15
+    missing = [n for n in sorted(declared) if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(abi.EXPORTS) >= declared - {"cdr_struct_size"}
+
+
+def test_struct_layouts_match_mirrors():
+    abi.check_layouts()
+
+
+def test_plan_slices_sorted_and_padded():
+    b = engine.synth_batch(0, 300, seed=3)
+    L = abi.lib()
+    ns, rows = C.c_uint32(), C.c_uint64()
+    assert L.cdr_plan_slices(b.wfs, b.n_wfs, None, None, None, C.byref(ns), C.byref(rows)) == 0
+    lane = (C.c_int32 * (ns.value * 64))()
+    slen = (C.c_uint32 * ns.value)()
+    row0 = (C.c_uint64 * ns.value)()
+    assert L.cdr_plan_slices(b.wfs, b.n_wfs, lane, slen, row0, C.byref(ns), C.byref(rows)) == 0
+    lane = np.frombuffer(lane, np.int32)
+    assert sorted(lane[lane >= 0].tolist()) == list(range(b.n_wfs))
+    lens = np.array([b.wfs[w].ev_len if w >= 0 else 0 for w in lane]).reshape(-1, 64)
+    assert (lens.max(1) == np.frombuffer(slen, np.uint32)).all()
+    assert (np.diff(lens.max(1)) <= 0).all()  # longest slices first
+    assert np.frombuffer(row0, np.uint64)[-1] + slen[ns.value - 1] == rows.value
+
+
+def test_pack_round_trip():
+    """Every event lands in its (slice, row, lane) cell with the operands the kernel
+    reads; padding cells are PAD."""
+    b = engine.synth_batch(0, 150, seed=11, error_rate=0.2)
+    L = abi.lib()
+    ns, rows = C.c_uint32(), C.c_uint64()
+    L.cdr_plan_slices(b.wfs, b.n_wfs, None, None, None, C.byref(ns), C.byref(rows))
+    n = rows.value * 64
+    lane = np.zeros(ns.value * 64, np.int32)
+    slen = np.zeros(ns.value, np.uint32)
+    row0 = np.zeros(ns.value, np.uint64)
+    L.cdr_plan_slices(b.wfs, b.n_wfs, lane.ctypes.data, slen.ctypes.data, row0.ctypes.data, C.byref(ns),
+                      C.byref(rows))
+    cols = {k: np.zeros(n, dt) for k, dt in (("type_flags", np.uint32), ("event_id", np.int64),
+                                             ("version", np.int64), ("timestamp", np.int64),
+                                             ("task_id", np.int64), ("key", np.int64), ("aux", np.int64),
+                                             ("h", np.uint32), ("n", np.int32))}
+    aw = L.cdr_plan_arena_words(C.byref(b.cstruct()))
+    arena = np.zeros(max(1, aw), np.uint64)
+    s = abi.CdrSlices(n_slices=ns.value, n_rows=rows.value, arena_words=aw)
+    s.slice_row0, s.slice_len, s.lane_wf = row0.ctypes.data, slen.ctypes.data, lane.ctypes.data
+    for k, v in cols.items():
+        setattr(s, k, v.ctypes.data)
+    s.arena = arena.ctypes.data
+    assert L.cdr_pack_slices(C.byref(b.cstruct()), C.byref(s), 2) == 0
+    for i, w in enumerate(lane):
+        sl, l = divmod(i, 64)
+        if w < 0:
+            continue
+        d = b.wfs[w]
+        for k in range(slen[sl]):
+            j = (int(row0[sl]) + k) * 64 + l
+            if k >= d.ev_len:
+                assert cols["type_flags"][j] == 0xFF
+                continue
+            e = b.events[d.ev_off + k]
+            assert cols["type_flags"][j] & 0xFF == e.type
+            assert bool(cols["type_flags"][j] & (1 << 8)) == bool(e.flags & 1 or k == 0)
+            assert (cols["event_id"][j], cols["version"][j], cols["timestamp"][j], cols["task_id"][j]) == (
+                e.event_id, e.version, e.timestamp, e.task_id)
+            if e.type == abi.EV["ActivityTaskScheduled"]:
+                rec = abi.AttrATSched.from_buffer_copy(arena[cols["aux"][j]:cols["aux"][j] + 7].tobytes())
+                assert bytes(rec) == bytes(e.a.at_sched) and cols["key"][j] == e.a.at_sched.activity_id
+            elif e.type == abi.EV["ActivityTaskStarted"]:
+                assert cols["key"][j] == e.a.at.scheduled_event_id and cols["h"][j] == e.a.at.request_id
+            elif e.type == abi.EV["TimerStarted"]:
+                assert cols["key"][j] == e.a.timer.timer_id and cols["aux"][j] == e.a.timer.start_to_fire_s
+
+
+def test_plan_caps_bound_oracle_outputs():
+    import oracle
+    b = engine.synth_batch(4, 200, seed=5)
+    pl = engine.plan(b)
+    out = oracle.replay(b, pl)
+    for w in range(b.n_wfs):
+        r, c = out.result[w], pl.caps[w]
+        if r.code == abi.OK:
+            assert r.n_activity <= c.act_cap and r.n_timer <= c.timer_cap and r.n_vh <= c.vh_cap
+
+
+def test_plan_rejects_inconsistent_new_run():
+    b = engine.synth_batch(4, 20, seed=9)
+    for w in range(b.n_wfs):
+        if b.wfs[w].newrun >= 0:
+            b.wfs[b.wfs[w].newrun].run_id += 1
+            break
+    with pytest.raises(RuntimeError):
+        engine.plan(b)
+
+
+def test_fingerprint32_shard_mapping():
+    """farmhash Fingerprint32 % numShards (common/util.go:249-252).  No reference
+    test pins concrete hash values (parity unpinned); check determinism, range and
+    spread instead."""
+    L = abi.lib()
+    ids = [f"workflow-{i}".encode() for i in range(20000)]
+    shards = [L.cdr_workflow_id_to_shard(s, len(s), 16384) for s in ids]
+    assert all(0 <= x < 16384 for x in shards)
+    assert shards == [L.cdr_workflow_id_to_shard(s, len(s), 16384) for s in ids]
+    counts = np.bincount([L.cdr_workflow_id_to_shard(s, len(s), 8) for s in ids], minlength=8)
+    assert counts.min() > 2000  # roughly uniform
+    for n in range(0, 40):  # every length branch of Hash32
+        s = bytes(range(65, 65 + n))
+        assert L.cdr_fingerprint32(s, n) == L.cdr_fingerprint32(s, n)
+
+
+def test_engine_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        engine.Engine(0)
