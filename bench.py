@@ -1,0 +1,360 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X batched workflow-history replay engine.
+
+Metric (BASELINE.json): history events replayed/s and workflows rebuilt/s per node,
+as a fraction of the HBM roofline.  Workload (configs[1]): 1M activity-heavy
+workflows x 203 events, synthetic, NDC builder, on each GPU
+(weak scaling: N GPUs replay N x 1M workflows, sharded by historyShardID =
+Fingerprint32(workflowID) % 16384 and assigned shard->GPU greedily).
+
+One "step" = one replay of the whole device-resident batch (k_replay + k_finalize).
+Inputs are uploaded before the timed region; host SoA packing and H2D time are
+reported separately.  The CPU baseline is the CPU restatement (oracle/) run with one
+task per workflow on the host's cores over a bounded sample.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--wfs M] [--config C]
+       (N>1: torchrun --nproc-per-node N bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+from cadence_amd import abi  # noqa: E402
+
+NUM_SHARDS = 16384
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# SURVEY §8(d) canonical algorithmic bytes
+A_TYPE = np.zeros(256, np.int64)
+for _name, _b in (("WorkflowExecutionStarted", 96), ("ActivityTaskScheduled", 48), ("DecisionTaskScheduled", 12),
+                  ("DecisionTaskCompleted", 12), ("TimerStarted", 8), ("StartChildWorkflowExecutionInitiated", 16),
+                  ("SignalExternalWorkflowExecutionInitiated", 12), ("DecisionTaskStarted", 4),
+                  ("ActivityTaskStarted", 4), ("DecisionTaskTimedOut", 4), ("ChildWorkflowExecutionStarted", 4),
+                  ("WorkflowExecutionContinuedAsNew", 4), ("UpsertWorkflowSearchAttributes", 8)):
+    A_TYPE[abi.EV[_name]] = _b
+ROW_BYTES = {"n_activity": 128, "n_timer": 32, "n_child": 48, "n_cancel": 24, "n_signal": 40}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def assign_shards(total_wfs: int, world: int, rank: int, lengths=None):
+    """workflow ids "wf-<i>" -> historyShardID -> GPU (greedy largest-first on events)."""
+    L = abi.lib()
+    shard = np.empty(total_wfs, np.int32)
+    L.cdr_synth_shards(total_wfs, NUM_SHARDS, shard.ctypes.data)
+    w = np.bincount(shard, weights=lengths, minlength=NUM_SHARDS) if lengths is not None else \
+        np.bincount(shard, minlength=NUM_SHARDS).astype(np.float64)
+    owner = np.zeros(NUM_SHARDS, np.int32)
+    load = np.zeros(world)
+    for s in np.argsort(-w, kind="stable"):
+        g = int(np.argmin(load))
+        owner[s] = g
+        load[g] += w[s]
+    mine = np.nonzero(owner[shard] == rank)[0].astype(np.uint32)
+    return mine, load
+
+
+class DeviceBatch:
+    """Synthetic batch generated straight into the sliced layout, uploaded to HBM."""
+
+    def __init__(self, torch, config, index_map, seed, target_len=0):
+        L = abi.lib()
+        self.torch = torch
+        self.index_map = index_map
+        p = abi.CdrSynthParams(config=config, n_wfs=len(index_map), seed=seed, target_len=target_len, max_len=0,
+                               error_rate=0.0, builder=-1, rebuild=0, index_map=index_map.ctypes.data)
+        self.params = p
+        t0 = time.perf_counter()
+        info = abi.CdrSynthPlanInfo()
+        assert L.cdr_synth_sliced_plan(C.byref(p), C.byref(info)) == 0
+        self.info = info
+        n = info.n_rows * 64
+        cols = {"type_flags": np.uint32, "event_id": np.int64, "version": np.int64, "timestamp": np.int64,
+                "task_id": np.int64, "key": np.int64, "aux": np.int64, "h": np.uint32, "n": np.int32}
+        self.h_cols = {k: np.empty(n, dt) for k, dt in cols.items()}
+        self.h_lane = np.empty(info.n_slices * 64, np.int32)
+        self.h_slen = np.empty(info.n_slices, np.uint32)
+        self.h_row0 = np.empty(info.n_slices, np.uint64)
+        self.h_arena = np.empty(max(1, info.arena_words), np.uint64)
+        self.h_wfs = (abi.CdrWfDesc * info.n_entries)()
+        self.h_caps = (abi.CdrWfCaps * info.n_entries)()
+        self.h_kvs = np.zeros(max(1, info.n_kvs) * 2, np.uint32)
+        self.h_rps = (abi.CdrResetPoint * max(1, info.n_rps))()
+        s = abi.CdrSlices(n_slices=info.n_slices, n_rows=info.n_rows, arena_words=info.arena_words)
+        s.slice_row0, s.slice_len, s.lane_wf = self.h_row0.ctypes.data, self.h_slen.ctypes.data, \
+            self.h_lane.ctypes.data
+        for k, v in self.h_cols.items():
+            setattr(s, k, v.ctypes.data)
+        s.arena = self.h_arena.ctypes.data
+        meta = abi.CdrBatch()
+        threads = min(32, os.cpu_count() or 8)
+        rc = L.cdr_synth_sliced_fill(C.byref(p), C.byref(s), self.h_wfs, self.h_caps, self.h_kvs.ctypes.data,
+                                     self.h_rps, C.byref(meta), threads)
+        assert rc == 0, rc
+        self.meta = meta
+        self.pack_s = time.perf_counter() - t0
+        # ---- upload (H2D timed separately)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        t0 = time.perf_counter()
+        self.keep = []
+
+        def up(a):
+            t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to(dev)
+            self.keep.append(t)
+            return t.data_ptr()
+
+        def up_ct(a):
+            return up(np.frombuffer(a, np.uint8))
+
+        db = abi.CdrDevBatch()
+        db.ev.n_slices, db.ev.n_rows, db.ev.arena_words = info.n_slices, info.n_rows, info.arena_words
+        db.ev.slice_row0, db.ev.slice_len, db.ev.lane_wf = up(self.h_row0), up(self.h_slen), up(self.h_lane)
+        for k, v in self.h_cols.items():
+            setattr(db.ev, k, up(v))
+        db.ev.arena = up(self.h_arena)
+        db.wfs, db.caps = up_ct(self.h_wfs), up_ct(self.h_caps)
+        db.kvs, db.rps = up(self.h_kvs), up_ct(self.h_rps)
+        db.n_wfs = info.n_entries
+        db.empty_uuid = meta.empty_uuid
+        db.cluster = meta.cluster
+        db.now_ns = meta.now_ns
+        db.uuid_seed = meta.uuid_seed
+        self.db = db
+        tot = info.totals
+        out = abi.CdrOut()
+        sizes = {"result": info.n_entries * C.sizeof(abi.CdrWfResult),
+                 "exec": info.n_entries * C.sizeof(abi.CdrExecInfo),
+                 "repl": info.n_entries * C.sizeof(abi.CdrReplState),
+                 "vh": tot.vh * C.sizeof(abi.CdrVHItem), "act": tot.act * C.sizeof(abi.CdrActivityInfo),
+                 "timer": tot.timer * C.sizeof(abi.CdrTimerInfo), "child": tot.child * C.sizeof(abi.CdrChildInfo),
+                 "cancel": tot.cancel * C.sizeof(abi.CdrCancelInfo),
+                 "signal": tot.signal * C.sizeof(abi.CdrSignalInfo),
+                 "rp": tot.rp * C.sizeof(abi.CdrResetPoint), "sa": tot.sa * C.sizeof(abi.CdrKV)}
+        self.out_bytes = sum(sizes.values())
+        self.out_t = {}
+        for k, nb in sizes.items():
+            t = torch.zeros(max(8, nb), dtype=torch.uint8, device=dev)
+            self.out_t[k] = t
+            setattr(out, k, t.data_ptr())
+        self.out = out
+        torch.cuda.synchronize()
+        self.h2d_s = time.perf_counter() - t0
+        self.in_bytes = sum(v.nbytes for v in self.h_cols.values()) + self.h_arena.nbytes
+        types = self.h_cols["type_flags"] & 0xFF
+        self.type_counts = np.bincount(types, minlength=256)
+        self.n_events = int(self.type_counts[:abi.EV["UpsertWorkflowSearchAttributes"] + 1].sum())
+
+    def results(self):
+        n = self.info.n_entries
+        raw = self.out_t["result"][: n * C.sizeof(abi.CdrWfResult)].cpu().numpy().copy()
+        return (abi.CdrWfResult * n).from_buffer(raw)
+
+    def algorithmic_bytes(self, res):
+        ev_bytes = int((self.type_counts[:42] * (48 + A_TYPE[:42])).sum())
+        n_ok, vh, rows, repl = 0, 0, 0, 0
+        arr = np.frombuffer(res, dtype=np.dtype([("code", "<i4"), ("flags", "<u4"), ("fid", "<i8"), ("fix", "<i8"),
+                                                   ("n_activity", "<u4"), ("n_timer", "<u4"), ("n_child", "<u4"),
+                                                   ("n_cancel", "<u4"), ("n_signal", "<u4"), ("n_vh", "<u4"),
+                                                   ("n_rp", "<u4"), ("n_sa", "<u4")]))
+        builders = np.frombuffer(self.h_wfs, dtype=np.uint8).reshape(len(self.h_wfs), -1)
+        ok = arr["code"] == 0
+        n_ok = int(ok.sum())
+        vh = int(arr["n_vh"][ok].sum())
+        for f, b in ROW_BYTES.items():
+            rows += int(arr[f][ok].sum()) * b
+        # builder field offset in cdr_wf_desc
+        boff = abi.CdrWfDesc.builder.offset
+        bld = builders[:, boff:boff + 4].copy().view(np.uint32)[:, 0]
+        repl = int(((bld == abi.BUILDER_2DC) & ok).sum()) * 32
+        wf_bytes = len(arr) * (256 + 8) + 16 * vh + repl
+        return ev_bytes + wf_bytes + rows, n_ok, ev_bytes, wf_bytes, rows
+
+
+def stream_peak_gbs(torch, nbytes=4 << 30, reps=5):
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        b.copy_(a)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    del a, b
+    return 2 * nbytes / dt / 1e9
+
+
+def cpu_baseline(config, n_wfs, seed, min_seconds=10.0):
+    """CPU restatement (oracle/) on the box's host cores, one task per workflow (the
+    analogue of the reference's goroutine-per-workflow), over a bounded sample."""
+    import oracle
+    from cadence_amd import engine
+    b = engine.synth_batch(config, n_wfs, seed)
+    pl = engine.plan(b)
+    n_ev = len(b.events)
+    threads = max(1, min(os.cpu_count() or 1, int(os.environ.get("CDR_CPU_THREADS", "16"))))
+    res = {}
+    for th in (threads, 1):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            oracle.replay(b, pl, threads=th)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= (min_seconds if th == threads else min_seconds / 4) or reps >= 200:
+                break
+        res[th] = n_ev * reps / el
+    return {"value": res[threads], "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"config {config}: {n_wfs} workflows x {n_ev // max(1, n_wfs)} events, replayed "
+                      f"{'repeatedly'} for >= {min_seconds:.0f} s; single-thread {res[1]:.4g} events/s; "
+                      f"the Go stateBuilder cannot run here (no Go toolchain)",
+            "single_thread_events_per_s": res[1], "workflows_per_s": res[threads] / (n_ev / max(1, n_wfs))}
+
+
+def load_traffic(workload):
+    p = os.path.join(HERE, "profiles", "traffic_latest.json")
+    try:
+        d = json.load(open(p))
+        if d.get("workload") == workload:
+            return d
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--wfs", type=int, default=1_000_000, help="workflows per GPU")
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=0x5EED0002)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stream-peak", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world, rank, local = dist_env()
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    L = abi.lib()
+    ctx = L.cdr_create(torch.cuda.current_device())
+    if not ctx:
+        raise SystemExit("cdr_create failed (no GPU?) — the engine has no CPU fallback")
+
+    total = args.wfs * world
+    mine, _ = assign_shards(total, world, rank)
+    log(f"[rank {rank}] {len(mine)} of {total} workflows (shard->GPU greedy over {NUM_SHARDS} shards)")
+    db = DeviceBatch(torch, args.config, mine, args.seed)
+    log(f"[rank {rank}] packed {db.n_events:,} events in {db.pack_s:.2f}s (host SoA), H2D {db.h2d_s:.2f}s "
+        f"({db.in_bytes / 1e9:.2f} GB in, {db.out_bytes / 1e9:.2f} GB out buffers)")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        rc = L.cdr_replay_sliced_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"cdr_replay_sliced_async rc={rc}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    L.cdr_timing_begin(ctx, args.steps)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = (C.c_float * args.steps)()
+    n = C.c_uint32(args.steps)
+    L.cdr_timing_read(ctx, ms, C.byref(n))
+    kern_ms = float(np.mean(np.frombuffer(ms, np.float32)[: n.value]))
+
+    # verification + the only collective: RCCL allreduce of counters and checksums
+    res = db.results()
+    alg_bytes, n_ok, ev_b, wf_b, row_b = db.algorithmic_bytes(res)
+    csum = torch.zeros(1, dtype=torch.int64, device="cuda")
+    L.cdr_checksum_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(csum.data_ptr()), C.c_void_p(stream))
+    stats = torch.tensor([db.n_events, db.info.n_entries, n_ok, 0], dtype=torch.int64, device="cuda")
+    stats[3] = csum[0]
+    t_el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(stats)
+        dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
+    torch.cuda.synchronize()
+    elapsed = float(t_el.item())
+    tot_events, tot_wfs, tot_ok, checksum = [int(x) for x in stats.tolist()]
+    if tot_ok != tot_wfs:
+        log(f"WARNING: {tot_wfs - tot_ok} workflows did not replay OK")
+
+    if rank != 0:
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    ms_per_step = elapsed / args.steps * 1e3
+    ev_per_s = tot_events * args.steps / elapsed
+    wf_per_s = tot_wfs * args.steps / elapsed
+    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+    workload = f"C{args.config}-{args.wfs}wf-sliced"
+    traffic = load_traffic(workload)
+    peak_meas = None if args.no_stream_peak else stream_peak_gbs(torch)
+    cpu = None if (args.no_cpu_baseline or args.gpus > 1) else cpu_baseline(args.config, 20000, args.seed)
+    line = {
+        "metric": "history events replayed/sec + workflows rebuilt/sec (node), % of HBM roofline",
+        "value": ev_per_s, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int64", "data": "synthetic (deterministic generator, SURVEY §8(d) shapes)",
+        "config": {"workload": workload, "workflows_per_gpu": args.wfs, "events_per_gpu": db.n_events,
+                   "events_per_workflow": round(db.n_events / max(1, len(mine)), 2), "builder": "NDC",
+                   "sharding": f"Fingerprint32(workflowID) % {NUM_SHARDS} -> greedy shard->GPU",
+                   "parallelism": f"shard{world}"},
+        "workflows_per_s": wf_per_s,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS,
+                     "traffic": traffic["bytes_per_launch"] if traffic else None,
+                     "kernel": "k_replay", "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": alg_bytes,
+                     "bytes_breakdown": {"events": ev_b, "per_workflow": wf_b, "pending_rows": row_b},
+                     "stream_copy_peak_gbs": peak_meas},
+        "cpu_baseline": cpu,
+        "host": {"soa_pack_s": db.pack_s, "h2d_s": db.h2d_s,
+                 "h2d_gbs": db.in_bytes / max(db.h2d_s, 1e-9) / 1e9},
+        "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_workflows": tot_ok,
+    }
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    L.cdr_destroy(ctx)
+
+
+if __name__ == "__main__":
+    main()

@@ -186,7 +186,7 @@ CdrDevBatch = _S("cdr_dev_batch", [
 # ------------------------------------------------------------------ synth
 CdrSynthParams = _S("cdr_synth_params", [
     ("config", i32), ("n_wfs", u32), ("seed", u64), ("target_len", u32), ("max_len", u32), ("error_rate", f64),
-    ("builder", i32), ("rebuild", i32)])
+    ("builder", i32), ("rebuild", i32), ("index_map", C.c_void_p)])
 CdrSynthSizes = _S("cdr_synth_sizes", [("n_events", u64), ("n_entries", u32), ("_pad", u32), ("n_kvs", u64),
                                        ("n_rps", u64), ("arena_words", u64)])
 CdrSynthPlanInfo = _S("cdr_synth_plan_info", [
@@ -222,6 +222,9 @@ EXPORTS = {
     "cdr_workflow_id_to_shard": (i32, [C.c_char_p, C.c_size_t, i32]),
     "cdr_last_kernel_ms": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "cdr_version": (C.c_char_p, []),
+    "cdr_timing_begin": (i32, [C.c_void_p, u32]),
+    "cdr_timing_read": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(u32)]),
+    "cdr_synth_shards": (i32, [u64, i32, C.c_void_p]),
     "cdr_struct_size": (u64, [C.c_char_p]),
     "cdr_synth_size": (i32, [C.POINTER(CdrSynthParams), C.POINTER(CdrSynthSizes)]),
     "cdr_synth_fill": (i32, [C.POINTER(CdrSynthParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

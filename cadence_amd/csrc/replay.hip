@@ -36,12 +36,6 @@
 
 namespace {
 
-struct Ctl {  // per-lane scalar replay state (all in registers)
-  int32_t err;
-  int64_t err_id, err_k;
-  bool dead;
-};
-
 // workflowExecutionInfo.go:45-147 — true if the transition is accepted
 __device__ __forceinline__ bool transition_ok(int cur, int cur_close, int st, int cs) {
   switch (cur) {
@@ -215,229 +209,236 @@ __device__ __forceinline__ int alloc_initiated(const Row* rows, uint32_t& hw, ui
 }  // namespace
 
 // ============================================================== replay kernel
+namespace {
+
+// one event's columns (cdr.h "sliced layout")
+struct Ev {
+  uint32_t tf, h;
+  int32_t n;
+  int64_t id, ver, ts, task, key, aux;
+};
+
+__device__ __forceinline__ Ev load_ev(const cdr_slices& S, uint64_t i) {
+  Ev e;
+  e.tf = S.type_flags[i];
+  e.id = S.event_id[i];
+  e.ver = S.version[i];
+  e.ts = S.timestamp[i];
+  e.task = S.task_id[i];
+  e.key = S.key[i];
+  e.aux = S.aux[i];
+  e.h = S.h[i];
+  e.n = S.n[i];
+  return e;
+}
+
+}  // namespace
+
 __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t s = g >> 6;
   if (s >= B.ev.n_slices) return;
   const int32_t w = B.ev.lane_wf[g];
   if (w < 0) return;
-  const cdr_wf_desc d = B.wfs[w];
-  const cdr_wf_caps cp = B.caps[w];
-  const uint32_t len = (uint32_t)d.ev_len;
+  const cdr_wf_desc& D = B.wfs[w];
+  const cdr_wf_caps& CP = B.caps[w];
+  const uint32_t len = (uint32_t)D.ev_len;
+  const uint32_t builder = D.builder;
   const uint64_t base = B.ev.slice_row0[s] * CDR_SLICE_WIDTH + (g & 63);
   const uint32_t EU = B.empty_uuid;
+  const bool isRS = builder == CDR_BUILDER_2DC;
+  const bool isVH = builder == CDR_BUILDER_NDC;
 
-  cdr_activity_info* act = O.act + cp.act_off;
-  cdr_timer_info* tim = O.timer + cp.timer_off;
-  cdr_child_info* chi = O.child + cp.child_off;
-  cdr_cancel_info* can = O.cancel + cp.cancel_off;
-  cdr_signal_info* sig = O.signal + cp.signal_off;
-  cdr_vh_item* vh = O.vh + cp.vh_off;
-  cdr_reset_point* rp = O.rp + cp.rp_off;
-  cdr_kv* sa = O.sa + cp.sa_off;
+  cdr_activity_info* act = O.act + CP.act_off;
+  cdr_timer_info* tim = O.timer + CP.timer_off;
+  cdr_child_info* chi = O.child + CP.child_off;
+  cdr_cancel_info* can = O.cancel + CP.cancel_off;
+  cdr_signal_info* sig = O.signal + CP.signal_off;
+  cdr_vh_item* vh = O.vh + CP.vh_off;
+  cdr_reset_point* rp = O.rp + CP.rp_off;
+  cdr_kv* sa = O.sa + CP.sa_off;
+  cdr_exec_info* X = O.exec + w;
   cdr_repl_state* RS = O.repl + w;
+  const uint32_t act_cap = CP.act_cap, tim_cap = CP.timer_cap, chi_cap = CP.child_cap, can_cap = CP.cancel_cap,
+                 sig_cap = CP.signal_cap, vh_cap = CP.vh_cap, rp_cap = CP.rp_cap, sa_cap = CP.sa_cap;
 
-  const bool isRS = d.builder == CDR_BUILDER_2DC;
-  const bool isVH = d.builder == CDR_BUILDER_NDC;
-
-  // ---- ExecutionInfo (mutableStateBuilder.go:185-196 defaults)
-  uint32_t x_create_req = 0, x_task_list = 0, x_wf_type = 0, x_cron = 0, x_pdom = 0, x_pwf = 0, x_prun = 0,
-           x_memo = 0, x_nonretr = 0, x_flags = 0;
-  int64_t x_initiated = 0, x_completion_batch = 0, x_last_first = 0, x_last_task = 0,
-          x_next_event = CDR_FIRST_EVENT_ID, x_last_processed = CDR_EMPTY_EVENT_ID;
-  int32_t x_wf_timeout = 0, x_dt_timeout_value = 0, x_state = CDR_STATE_CREATED, x_close = CDR_CLOSE_NONE,
-          x_signals = 0, x_attempt = 0, x_init_int = 0, x_max_int = 0, x_max_att = 0, x_exp_s = 0;
-  double x_backoff = 0.0;
-  int64_t x_exp_time = 0;
-  uint64_t x_br_lo = 0, x_br_hi = 0;
-  // decision (decisionInfo)
+  // ---- ExecutionInfo fields that later events change (registers); the fields only
+  // WorkflowExecutionStarted writes go straight to the output record.
+  uint32_t x_flags = 0;
+  int64_t x_completion_batch = 0, x_last_first = 0, x_last_task = 0, x_next_event = CDR_FIRST_EVENT_ID,
+          x_last_processed = CDR_EMPTY_EVENT_ID;
+  int32_t x_dt_timeout_value = 0, x_state = CDR_STATE_CREATED, x_close = CDR_CLOSE_NONE, x_signals = 0;
+  // decision (decisionInfo, mutableStateDecisionTaskManager.go:677-690)
   int64_t dv = CDR_EMPTY_VERSION, dsched = CDR_EMPTY_EVENT_ID, dstart = CDR_EMPTY_EVENT_ID, datt = 0, dst_ts = 0,
           dsc_ts = 0, dorig_ts = 0;
   uint32_t dreq = EU;
   int32_t dto = 0;
   // versions
-  int64_t curv = d.failover_version;  // NDC currentVersion
-  int64_t rs_cur = d.failover_version, rs_start = d.failover_version, rs_lwv = CDR_EMPTY_VERSION,
-          rs_lwid = CDR_EMPTY_EVENT_ID;
+  int64_t curv = D.failover_version;  // NDC currentVersion
+  int64_t rs_cur = curv, rs_start = curv, rs_lwv = CDR_EMPTY_VERSION, rs_lwid = CDR_EMPTY_EVENT_ID;
   uint32_t rs_mask = 0;
-  int64_t vh_last_id = 0, vh_last_ver = 0;
+  int64_t vh_last_id = 0, vh_last_ver = 0;  // the last VH item lives in registers
   uint32_t n_vh = 0;
   // tables
   uint32_t hw_act = 0, hw_tim = 0, hw_chi = 0, hw_can = 0, hw_sig = 0;
-  uint32_t live_chi = 0, live_can = 0, live_sig = 0;
-  uint32_t n_rp = 0, n_sa = 0;
+  uint32_t live_chi = 0, live_can = 0, live_sig = 0, n_rp = 0, n_sa = 0;
   // calls / errors
-  int64_t call_first_id = 0, call_first_k = 0, prev_id = 0, prev_ver = 0;
-  uint32_t call_idx = 0;
-  bool newrun_applied = false;
-  int32_t err = CDR_OK;
-  int64_t err_id = 0, err_k = 0;
-  bool stop_at_call_end = false;
+  int64_t call_first_id = 0, prev_id = 0, prev_ver = 0;
+  uint32_t call_first_k = 0, call_idx = 0;
+  bool newrun_applied = false, stop_at_call_end = false;
+  int32_t err = len == 0 ? CDR_E_HISTORY_EMPTY : CDR_OK;
+  int64_t err_id = 0;
+  uint32_t err_k = 0;
 
-#define FAIL(code)             \
-  do {                         \
-    err = (code);              \
-    err_id = e_id;             \
-    err_k = k;                 \
-    stop_at_call_end = true;   \
+#define FAIL(code)           \
+  do {                       \
+    err = (code);            \
+    err_id = e.id;           \
+    err_k = k;               \
+    stop_at_call_end = true; \
   } while (0)
 
-  // close the call that ended with event (prev_id, prev_ver): stateBuilder.go:603-604
-  // plus the replication-state writes whose source is the call's last event
-  // (UpdateReplicationStateLastEventID mutableStateBuilder.go:561-581).
-  auto finish_call = [&]() {
-    if (isRS) {
-      rs_lwv = prev_ver;
-      rs_lwid = prev_id;
-      const int src = cluster_for_version(B.cluster, prev_ver);
-      if (src < 0) {
-        // the panic fires at the call's first event, before anything else in the call
-        err = CDR_P_UNKNOWN_CLUSTER;
-        err_id = call_first_id;
-        err_k = call_first_k;
-        return;
-      }
-      if (src != B.cluster.current_cluster) {
-        RS->lri_version[src] = prev_ver;
-        RS->lri_last_event_id[src] = prev_id;
-        rs_mask |= 1u << src;
-      }
-    }
-    if (err == CDR_OK) {
-      x_last_first = call_first_id;
-      x_next_event = prev_id + 1;
-    }
-  };
-
-  if (len == 0) err = CDR_E_HISTORY_EMPTY;
-
+  Ev nxt = len ? load_ev(B.ev, base) : Ev{};
   for (uint32_t k = 0; k < len; k++) {
-    const uint64_t i = base + (uint64_t)k * CDR_SLICE_WIDTH;
-    const uint32_t tf = B.ev.type_flags[i];
-    const uint32_t type = tf & 0xFFu;
-    const int64_t e_id = B.ev.event_id[i];
-    const int64_t e_ver = B.ev.version[i];
-    if ((tf & CDR_SEF_BATCH_FIRST) || k == 0) {
+    const Ev e = nxt;
+    if (k + 1 < len) nxt = load_ev(B.ev, base + (uint64_t)(k + 1) * CDR_SLICE_WIDTH);  // software pipeline
+    const uint32_t type = e.tf & 0xFFu;
+    if ((e.tf & CDR_SEF_BATCH_FIRST) || k == 0) {
       if (k > 0) {
-        finish_call();
+        // ---- end of the previous call: stateBuilder.go:603-604, plus the replication
+        // state whose source is the call's last event (mutableStateBuilder.go:561-581)
+        if (isRS) {
+          rs_lwv = prev_ver;
+          rs_lwid = prev_id;
+          const int src = cluster_for_version(B.cluster, prev_ver);
+          if (src < 0) {  // the panic fires at the call's first event, before anything else
+            err = CDR_P_UNKNOWN_CLUSTER;
+            err_id = call_first_id;
+            err_k = call_first_k;
+          } else if (src != B.cluster.current_cluster) {
+            RS->lri_version[src] = prev_ver;
+            RS->lri_last_event_id[src] = prev_id;
+            rs_mask |= 1u << src;
+          }
+        }
         if (err != CDR_OK) break;
+        x_last_first = call_first_id;
+        x_next_event = prev_id + 1;
         call_idx++;
       }
-      call_first_id = e_id;
+      call_first_id = e.id;
       call_first_k = k;
-    } else if (stop_at_call_end) {
-      prev_id = e_id;
-      prev_ver = e_ver;
-      continue;  // skip the rest of the failed call; only its last event matters for 2DC
     }
-    prev_id = e_id;
-    prev_ver = e_ver;
-    if (stop_at_call_end) continue;
+    prev_id = e.id;
+    prev_ver = e.ver;
+    if (stop_at_call_end) continue;  // rest of a failed call: only its last event matters (2DC)
 
     // ---- version prelude (stateBuilder.go:134-154)
     if (isRS) {
-      rs_cur = e_ver;  // UpdateReplicationStateVersion(v, true)
+      rs_cur = e.ver;  // UpdateReplicationStateVersion(v, true)
     } else if (isVH) {
-      if (x_state == CDR_STATE_CREATED || x_state == CDR_STATE_RUNNING) {
-        if (n_vh) curv = vh_last_ver;  // UpdateCurrentVersion (:445-489)
-        curv = e_ver;
-      }
+      if (x_state == CDR_STATE_CREATED || x_state == CDR_STATE_RUNNING) curv = e.ver;  // UpdateCurrentVersion
       // NewVersionHistoryItem + AddOrUpdateItem (versionHistory.go:31-42,203-236)
-      if (e_id < 0 || (e_ver < 0 && e_ver != CDR_EMPTY_VERSION)) {
+      if (e.id < 0 || (e.ver < 0 && e.ver != CDR_EMPTY_VERSION)) {
         FAIL(CDR_P_VH_ITEM_INVALID);
         continue;
       }
-      if (n_vh == 0) {
-        if (cp.vh_cap == 0) {
+      if (n_vh != 0 && e.ver < vh_last_ver) {
+        FAIL(CDR_E_VH_LOWER_VERSION);
+        continue;
+      }
+      if (n_vh != 0 && e.id <= vh_last_id) {
+        FAIL(CDR_E_VH_LOWER_EVENT_ID);
+        continue;
+      }
+      if (n_vh == 0 || e.ver > vh_last_ver) {
+        if (n_vh >= vh_cap) {
           FAIL(CDR_E_BAD_INPUT);
           continue;
         }
-        vh[0] = cdr_vh_item{e_id, e_ver};
-        n_vh = 1;
-        vh_last_id = e_id;
-        vh_last_ver = e_ver;
-      } else {
-        if (e_ver < vh_last_ver) {
-          FAIL(CDR_E_VH_LOWER_VERSION);
-          continue;
-        }
-        if (e_id <= vh_last_id) {
-          FAIL(CDR_E_VH_LOWER_EVENT_ID);
-          continue;
-        }
-        if (e_ver > vh_last_ver) {
-          if (n_vh >= cp.vh_cap) {
-            FAIL(CDR_E_BAD_INPUT);
-            continue;
-          }
-          vh[n_vh++] = cdr_vh_item{e_id, e_ver};
-        } else {
-          vh[n_vh - 1].event_id = e_id;
-        }
-        vh_last_id = e_id;
-        vh_last_ver = e_ver;
+        if (n_vh) vh[n_vh - 1] = cdr_vh_item{vh_last_id, vh_last_ver};  // close the previous item
+        n_vh++;
+        vh_last_ver = e.ver;
       }
+      vh_last_id = e.id;
     }
-    x_last_task = B.ev.task_id[i];  // :155
+    x_last_task = e.task;  // :155
 
     switch (type) {
       case CDR_EV_WF_STARTED: {  // stateBuilder.go:158-184 -> mutableStateBuilder.go:1639-1716
-        const cdr_attr_wf_started* a =
-            reinterpret_cast<const cdr_attr_wf_started*>(B.ev.arena + (uint64_t)B.ev.aux[i]);
+        const cdr_attr_wf_started* a = reinterpret_cast<const cdr_attr_wf_started*>(B.ev.arena + (uint64_t)e.aux);
         const uint32_t af = a->flags;
         if ((af & CDR_SF_HAS_PARENT_DOMAIN) && (af & CDR_SF_PARENT_DOMAIN_MISSING)) {
           FAIL(CDR_E_DOMAIN_NOT_FOUND);
           break;
         }
-        x_create_req = d.request_id;
-        x_task_list = a->task_list;
-        x_wf_type = a->workflow_type;
-        x_wf_timeout = a->exec_timeout_s;
-        x_dt_timeout_value = a->task_timeout_s;
         if (!transition_ok(x_state, x_close, CDR_STATE_CREATED, CDR_CLOSE_NONE)) {
           FAIL(CDR_E_INVALID_STATE_TRANSITION);
           break;
         }
+        const bool first = !(x_flags & CDR_XI_STARTED);  // fields absent from a first Started stay zero
+        X->domain_id = D.domain_id;
+        X->workflow_id = D.workflow_id;
+        X->run_id = D.run_id;
+        X->create_request_id = D.request_id;
+        X->task_list = a->task_list;
+        X->workflow_type = a->workflow_type;
+        X->workflow_timeout = a->exec_timeout_s;
+        X->cron_schedule = a->cron_schedule;
+        X->attempt = a->attempt;
+        X->initiated_id = (af & CDR_SF_HAS_PARENT_INITIATED) ? a->parent_initiated_id : CDR_EMPTY_EVENT_ID;
+        x_dt_timeout_value = a->task_timeout_s;
         x_state = CDR_STATE_CREATED;
         x_close = CDR_CLOSE_NONE;
         x_last_processed = CDR_EMPTY_EVENT_ID;
-        x_last_first = e_id;
+        x_last_first = e.id;
         dv = CDR_EMPTY_VERSION;
         dsched = CDR_EMPTY_EVENT_ID;
         dstart = CDR_EMPTY_EVENT_ID;
         dreq = EU;
         dto = 0;
-        x_cron = a->cron_schedule;
-        if (af & CDR_SF_HAS_PARENT_DOMAIN) x_pdom = a->parent_domain_id;
+        if (af & CDR_SF_HAS_PARENT_DOMAIN) X->parent_domain_id = a->parent_domain_id;
+        else if (first) X->parent_domain_id = 0;
         if (af & CDR_SF_HAS_PARENT_EXEC) {
-          x_pwf = a->parent_workflow_id;
-          x_prun = a->parent_run_id;
+          X->parent_workflow_id = a->parent_workflow_id;
+          X->parent_run_id = a->parent_run_id;
+        } else if (first) {
+          X->parent_workflow_id = 0;
+          X->parent_run_id = 0;
         }
-        x_initiated = (af & CDR_SF_HAS_PARENT_INITIATED) ? a->parent_initiated_id : CDR_EMPTY_EVENT_ID;
-        x_attempt = a->attempt;
         if (a->expiration_ts != 0) {
-          x_exp_time = a->expiration_ts;
+          X->expiration_time = a->expiration_ts;
           x_flags |= CDR_XI_HAS_EXPIRATION;
+        } else if (first) {
+          X->expiration_time = 0;
         }
         if (af & CDR_SF_HAS_RETRY) {
           x_flags |= CDR_XI_HAS_RETRY;
-          x_backoff = a->backoff_coefficient;
-          x_exp_s = a->retry_expiration_s;
-          x_init_int = a->retry_initial_s;
-          x_max_att = a->retry_max_attempts;
-          x_max_int = a->retry_max_interval_s;
-          x_nonretr = a->nonretriable;
+          X->backoff_coefficient = a->backoff_coefficient;
+          X->expiration_seconds = a->retry_expiration_s;
+          X->initial_interval = a->retry_initial_s;
+          X->maximum_attempts = a->retry_max_attempts;
+          X->maximum_interval = a->retry_max_interval_s;
+          X->nonretriable = a->nonretriable;
+        } else if (first) {
+          X->backoff_coefficient = 0.0;
+          X->expiration_seconds = 0;
+          X->initial_interval = 0;
+          X->maximum_attempts = 0;
+          X->maximum_interval = 0;
+          X->nonretriable = 0;
         }
         // rolloverAutoResetPointsWithExpiringTime (:3184-3205)
         n_rp = 0;
         x_flags &= ~CDR_XI_HAS_RESET_POINTS;
         if (af & CDR_SF_HAS_RESET_POINTS) {
           x_flags |= CDR_XI_HAS_RESET_POINTS;
-          const int64_t expiring = B.ev.timestamp[i] + (int64_t)d.retention_days * 24ll * 3600ll * NS_PER_S;
-          for (uint32_t q = 0; q < a->reset_points_len && q < cp.rp_cap; q++) {
-            cdr_reset_point p = B.rps[a->reset_points_off + q];
+          const int64_t expiring = e.ts + (int64_t)D.retention_days * 24ll * 3600ll * NS_PER_S;
+          const uint32_t crun = a->continued_run_id, off = a->reset_points_off, cnt = a->reset_points_len;
+          for (uint32_t q = 0; q < cnt && q < rp_cap; q++) {
+            cdr_reset_point p = B.rps[off + q];
             const uint32_t run = (p.flags & CDR_RP_HAS_RUN_ID) ? p.run_id : 0u;
-            if (run == a->continued_run_id) {
+            if (run == crun) {
               p.flags |= CDR_RP_HAS_EXPIRING;
               p.expiring_time_nano = expiring;
             }
@@ -446,50 +447,51 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         }
         if (af & CDR_SF_HAS_MEMO) {
           x_flags |= CDR_XI_HAS_MEMO;
-          x_memo = a->memo;
+          X->memo = a->memo;
+        } else if (first) {
+          X->memo = 0;
         }
         if (af & CDR_SF_HAS_SEARCH_ATTR) {
           n_sa = 0;
-          for (uint32_t q = 0; q < a->search_attr_len && q < cp.sa_cap; q++) sa[n_sa++] = B.kvs[a->search_attr_off + q];
+          const uint32_t off = a->search_attr_off, cnt = a->search_attr_len;
+          for (uint32_t q = 0; q < cnt && q < sa_cap; q++) sa[n_sa++] = B.kvs[off + q];
           if (n_sa) x_flags |= CDR_XI_HAS_SEARCH_ATTR;
           else x_flags &= ~CDR_XI_HAS_SEARCH_ATTR;
         }
         x_flags |= CDR_XI_STARTED;
         // SetHistoryTree (:313-339): branch token on ExecutionInfo, or on the VH for NDC
-        cdr_uuid(B.uuid_seed, d.wf_key, CDR_UUID_BRANCH, e_id, &x_br_lo, &x_br_hi);
+        uint64_t lo, hi;
+        cdr_uuid(B.uuid_seed, D.wf_key, CDR_UUID_BRANCH, e.id, &lo, &hi);
+        X->branch_tree_id = D.run_id;
+        X->branch_id_lo = lo;
+        X->branch_id_hi = hi;
         x_flags |= isVH ? CDR_XI_VH_BRANCH : CDR_XI_HAS_BRANCH;
-        if (isRS) rs_start = e_ver;  // :182-184
+        if (isRS) rs_start = e.ver;  // :182-184
         break;
       }
       case CDR_EV_DT_SCHEDULED:  // :186-200 -> mutableStateDecisionTaskManager.go:143-167
-        dv = e_ver;
-        dsched = e_id;
+        dv = e.ver;
+        dsched = e.id;
         dstart = CDR_EMPTY_EVENT_ID;
         dreq = EU;
-        dto = B.ev.n[i];
-        datt = B.ev.aux[i];
-        dsc_ts = B.ev.timestamp[i];
+        dto = e.n;
+        datt = e.aux;
+        dsc_ts = e.ts;
         dst_ts = 0;
-        dorig_ts = dsc_ts;
+        dorig_ts = e.ts;
         break;
-      case CDR_EV_DT_STARTED: {  // :202-213 -> :200-253
-        const int64_t sid = B.ev.key[i];
-        if (sid != dsched) {
+      case CDR_EV_DT_STARTED:  // :202-213 -> :200-253
+        if (e.key != dsched) {
           FAIL(CDR_E_DECISION_NOT_FOUND);
           break;
         }
-        if (x_state == CDR_STATE_CREATED) {
-          // Created -> Running is always accepted (workflowExecutionInfo.go:56-60)
-          x_state = CDR_STATE_RUNNING;
-          x_close = CDR_CLOSE_NONE;
-        }
-        dv = e_ver;
-        dstart = e_id;
-        dreq = B.ev.h[i];
+        if (x_state == CDR_STATE_CREATED) x_state = CDR_STATE_RUNNING;  // always accepted (:56-60)
+        dv = e.ver;
+        dstart = e.id;
+        dreq = e.h;
         datt = 0;
-        dst_ts = B.ev.timestamp[i];
+        dst_ts = e.ts;
         break;
-      }
       case CDR_EV_DT_COMPLETED: {  // :215-219 -> :255-262,659-674,789-800
         dv = CDR_EMPTY_VERSION;
         dsched = CDR_EMPTY_EVENT_ID;
@@ -499,30 +501,29 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         datt = 0;
         dst_ts = 0;
         dsc_ts = 0;  // OriginalScheduledTimestamp kept
-        x_last_processed = B.ev.aux[i];
-        const uint32_t cks = B.ev.h[i];
+        x_last_processed = e.aux;
+        const uint32_t cks = e.h;
         if (cks) {  // addBinaryCheckSumIfNotExists (mutableStateBuilder.go:1798-1842)
           bool exists = false;
           for (uint32_t q = 0; q < n_rp; q++) {
-            const uint32_t c = (rp[q].flags & CDR_RP_HAS_CHECKSUM) ? rp[q].binary_checksum : 0u;
-            exists |= c == cks;
+            const cdr_reset_point& p = rp[q];
+            exists |= ((p.flags & CDR_RP_HAS_CHECKSUM) ? p.binary_checksum : 0u) == cks;
           }
           if (!exists) {
-            if (n_rp >= cp.rp_cap) {
+            if (n_rp >= rp_cap) {
               FAIL(CDR_E_BAD_INPUT);
               break;
             }
             const bool resettable = live_chi == 0 && live_can == 0 && live_sig == 0;
-            cdr_reset_point p;
+            cdr_reset_point& p = rp[n_rp++];
             p.binary_checksum = cks;
-            p.run_id = d.run_id;
-            p.first_decision_completed_id = e_id;
+            p.run_id = D.run_id;
+            p.first_decision_completed_id = e.id;
             p.created_time_nano = B.now_ns;
             p.expiring_time_nano = 0;
             p.flags = CDR_RP_HAS_CHECKSUM | CDR_RP_HAS_RUN_ID | CDR_RP_HAS_FIRST_DC_ID | CDR_RP_HAS_CREATED |
                       CDR_RP_HAS_RESETTABLE | (resettable ? CDR_RP_RESETTABLE : 0u);
             p._pad = 0;
-            rp[n_rp++] = p;
             x_flags |= CDR_XI_HAS_RESET_POINTS;
           }
         }
@@ -530,8 +531,8 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
       }
       case CDR_EV_DT_TIMED_OUT:  // :221-239 -> FailDecision :635-656 + transient :169-198
       case CDR_EV_DT_FAILED: {   // :241-257
-        const bool inc = type == CDR_EV_DT_FAILED || B.ev.n[i] != CDR_TIMEOUT_SCHEDULE_TO_START;
-        const int64_t a1 = inc ? datt + 1 : 0;
+        const bool inc = type == CDR_EV_DT_FAILED || e.n != CDR_TIMEOUT_SCHEDULE_TO_START;
+        datt = inc ? datt + 1 : 0;
         dv = CDR_EMPTY_VERSION;
         dsched = CDR_EMPTY_EVENT_ID;
         dstart = CDR_EMPTY_EVENT_ID;
@@ -539,9 +540,8 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         dto = 0;
         dst_ts = 0;
         dorig_ts = 0;
-        datt = a1;
         dsc_ts = inc ? B.now_ns : 0;
-        if (datt != 0) {  // no pending decision here by construction
+        if (datt != 0) {  // transient decision: no decision is pending here by construction
           dv = isRS ? rs_cur : (isVH ? curv : CDR_EMPTY_VERSION);
           dsched = x_next_event;  // NextEventID as of the call's start
           dto = x_dt_timeout_value;
@@ -550,72 +550,69 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         break;
       }
       case CDR_EV_AT_SCHEDULED: {  // :259-269 -> mutableStateBuilder.go:1982-2028
-        const cdr_attr_at_scheduled* a =
-            reinterpret_cast<const cdr_attr_at_scheduled*>(B.ev.arena + (uint64_t)B.ev.aux[i]);
-        const uint32_t aid = (uint32_t)B.ev.key[i];
+        const cdr_attr_at_scheduled* a = reinterpret_cast<const cdr_attr_at_scheduled*>(B.ev.arena + (uint64_t)e.aux);
+        const uint32_t aid = (uint32_t)e.key;
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++) {
-          if (act[j].schedule_id == DEAD_KEY) {
+          cdr_activity_info& r = act[j];
+          if (r.schedule_id == DEAD_KEY) {
             if (slot < 0) slot = (int)j;
-          } else if (act[j].activity_id == aid && (act[j].flags & AI_IN_AID_MAP)) {
-            act[j].flags &= ~AI_IN_AID_MAP;  // byActivityID[aid] is overwritten
+          } else if (r.activity_id == aid && (r.flags & AI_IN_AID_MAP)) {
+            r.flags &= ~AI_IN_AID_MAP;  // byActivityID[aid] is overwritten
           }
         }
         if (slot < 0) {
-          if (hw_act >= cp.act_cap) {
+          if (hw_act >= act_cap) {
             FAIL(CDR_E_BAD_INPUT);
             break;
           }
           slot = (int)hw_act++;
         }
-        const int64_t ts = B.ev.timestamp[i];
-        cdr_activity_info r;
-        r.version = e_ver;
-        r.schedule_id = e_id;
+        const int32_t s2c = a->s2c_s, xs = a->retry_expiration_s;
+        const bool retry = (a->flags & CDR_AF_HAS_RETRY) != 0;
+        cdr_activity_info& r = act[slot];
+        r.version = e.ver;
+        r.schedule_id = e.id;
         r.scheduled_event_batch_id = call_first_id;
-        r.scheduled_time = ts;
+        r.scheduled_time = e.ts;
         r.started_id = CDR_EMPTY_EVENT_ID;
         r.started_time = 0;
         r.last_heartbeat_time = 0;
-        r.expiration_time = ts + (int64_t)a->s2c_s * NS_PER_S;
+        r.expiration_time = e.ts + (int64_t)((retry && xs > s2c) ? xs : s2c) * NS_PER_S;
         r.cancel_request_id = CDR_EMPTY_EVENT_ID;
         r.activity_id = aid;
         r.request_id = 0;
         r.task_list = a->task_list;
+        r.nonretriable = retry ? a->nonretriable : 0u;
         r.s2s = a->s2s_s;
-        r.s2c = a->s2c_s;
+        r.s2c = s2c;
         r.stc = a->stc_s;
         r.hb = a->hb_s;
         r.timer_task_status = CDR_TIMER_TASK_STATUS_NONE;
         r.attempt = 0;
-        const bool retry = (a->flags & CDR_AF_HAS_RETRY) != 0;
         r.initial_interval = retry ? a->retry_initial_s : 0;
         r.maximum_interval = retry ? a->retry_max_interval_s : 0;
         r.maximum_attempts = retry ? a->retry_max_attempts : 0;
-        r.nonretriable = retry ? a->nonretriable : 0u;
-        r.backoff_coefficient = retry ? a->backoff_coefficient : 0.0;
-        if (retry && a->retry_expiration_s > a->s2c_s) r.expiration_time = ts + (int64_t)a->retry_expiration_s * NS_PER_S;
         r.flags = (retry ? CDR_AI_HAS_RETRY : 0u) | AI_IN_AID_MAP;
-        act[slot] = r;
+        r.backoff_coefficient = retry ? a->backoff_coefficient : 0.0;
         activity_timer_pick(act, hw_act);
         break;
       }
       case CDR_EV_AT_STARTED: {  // :271-278 -> :2083-2098
-        const int64_t sid = B.ev.key[i];
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++)
-          if (act[j].schedule_id == sid) slot = (int)j;
+          if (act[j].schedule_id == e.key) slot = (int)j;
         if (slot < 0) {
           FAIL(CDR_P_ACTIVITY_STARTED_NIL);  // nil deref in Go
           break;
         }
-        const int64_t ts = B.ev.timestamp[i];
-        act[slot].version = e_ver;
-        act[slot].started_id = e_id;
-        act[slot].request_id = B.ev.h[i];
-        act[slot].started_time = ts;
-        act[slot].last_heartbeat_time = ts;
-        act[slot].flags |= CDR_AI_STARTED_TIME_SET;
+        cdr_activity_info& r = act[slot];
+        r.version = e.ver;
+        r.started_id = e.id;
+        r.request_id = e.h;
+        r.started_time = e.ts;
+        r.last_heartbeat_time = e.ts;
+        r.flags |= CDR_AI_STARTED_TIME_SET;
         activity_timer_pick(act, hw_act);
         break;
       }
@@ -623,20 +620,19 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
       case CDR_EV_AT_FAILED:
       case CDR_EV_AT_TIMED_OUT:
       case CDR_EV_AT_CANCELED: {
-        const int64_t sid = B.ev.key[i];
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++)
-          if (act[j].schedule_id == sid) slot = (int)j;
+          if (act[j].schedule_id == e.key) slot = (int)j;
         if (slot < 0) {
           FAIL(CDR_E_ACTIVITY_NOT_FOUND);
           break;
         }
         const uint32_t aid = act[slot].activity_id;
-        const bool own = (act[slot].flags & AI_IN_AID_MAP) != 0;
+        const uint32_t fl = act[slot].flags;
         act[slot].schedule_id = DEAD_KEY;
-        act[slot].flags &= ~AI_IN_AID_MAP;
-        bool found = own;
-        if (!own)
+        act[slot].flags = fl & ~AI_IN_AID_MAP;
+        bool found = (fl & AI_IN_AID_MAP) != 0;
+        if (!found)
           for (uint32_t j = 0; j < hw_act; j++)
             if (act[j].schedule_id != DEAD_KEY && act[j].activity_id == aid && (act[j].flags & AI_IN_AID_MAP)) {
               act[j].flags &= ~AI_IN_AID_MAP;
@@ -650,7 +646,7 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         break;
       }
       case CDR_EV_AT_CANCEL_REQUESTED: {  // :307-310 -> :2264-2285
-        const uint32_t aid = (uint32_t)B.ev.key[i];
+        const uint32_t aid = (uint32_t)e.key;
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++)
           if (act[j].schedule_id != DEAD_KEY && act[j].activity_id == aid && (act[j].flags & AI_IN_AID_MAP))
@@ -659,13 +655,13 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
           FAIL(CDR_E_MISSING_ACTIVITY_INFO);
           break;
         }
-        act[slot].version = e_ver;
+        act[slot].version = e.ver;
         act[slot].flags |= CDR_AI_CANCEL_REQUESTED;
-        act[slot].cancel_request_id = e_id;
+        act[slot].cancel_request_id = e.id;
         break;
       }
       case CDR_EV_TIMER_STARTED: {  // :324-332 -> :2877-2900
-        const uint32_t tid = (uint32_t)B.ev.key[i];
+        const uint32_t tid = (uint32_t)e.key;
         int slot = -1, free_slot = -1;
         for (uint32_t j = 0; j < hw_tim; j++) {
           if (tim[j].started_id == DEAD_KEY) {
@@ -676,62 +672,63 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         }
         if (slot < 0) slot = free_slot;
         if (slot < 0) {
-          if (hw_tim >= cp.timer_cap) {
+          if (hw_tim >= tim_cap) {
             FAIL(CDR_E_BAD_INPUT);
             break;
           }
           slot = (int)hw_tim++;
         }
-        cdr_timer_info t;
-        t.version = e_ver;
-        t.started_id = e_id;
-        t.expiry_time = B.ev.timestamp[i] + B.ev.aux[i] * NS_PER_S;
+        cdr_timer_info& t = tim[slot];
+        t.version = e.ver;
+        t.started_id = e.id;
+        t.expiry_time = e.ts + e.aux * NS_PER_S;
         t.task_id = CDR_TIMER_TASK_STATUS_NONE;
         t.timer_id = tid;
         t._pad = 0;
-        tim[slot] = t;
         user_timer_pick(tim, hw_tim);
         break;
       }
-      case CDR_EV_TIMER_FIRED:     // :334-341
+      case CDR_EV_TIMER_FIRED:       // :334-341
       case CDR_EV_TIMER_CANCELED: {  // :343-350
-        const uint32_t tid = (uint32_t)B.ev.key[i];
+        const uint32_t tid = (uint32_t)e.key;
         for (uint32_t j = 0; j < hw_tim; j++)
           if (tim[j].started_id != DEAD_KEY && tim[j].timer_id == tid) tim[j].started_id = DEAD_KEY;
         user_timer_pick(tim, hw_tim);
         break;
       }
       case CDR_EV_CHILD_INITIATED: {  // :355-371 -> :3256-3280
-        int slot = alloc_initiated(chi, hw_chi, cp.child_cap);
+        const int slot = alloc_initiated(chi, hw_chi, chi_cap);
         if (slot < 0) {
           FAIL(CDR_E_BAD_INPUT);
           break;
         }
-        cdr_child_info c;
-        c.version = e_ver;
-        c.initiated_id = e_id;
+        cdr_child_info& c = chi[slot];
+        c.version = e.ver;
+        c.initiated_id = e.id;
         c.initiated_event_batch_id = call_first_id;
         c.started_id = CDR_EMPTY_EVENT_ID;
-        cdr_uuid(B.uuid_seed, d.wf_key, CDR_UUID_CHILD_REQ, e_id, &c.create_request_lo, &c.create_request_hi);
-        c.started_workflow_id = B.ev.h[i];
+        uint64_t lo, hi;
+        cdr_uuid(B.uuid_seed, D.wf_key, CDR_UUID_CHILD_REQ, e.id, &lo, &hi);
+        c.create_request_lo = lo;
+        c.create_request_hi = hi;
+        c.started_workflow_id = e.h;
         c.started_run_id = 0;
-        c.domain_name = (uint32_t)B.ev.key[i];
-        c.workflow_type = (uint32_t)B.ev.aux[i];
-        c.parent_close_policy = B.ev.n[i];
+        c.domain_name = (uint32_t)e.key;
+        c.workflow_type = (uint32_t)e.aux;
+        c.parent_close_policy = e.n;
         c._pad = 0;
-        chi[slot] = c;
         live_chi++;
-        if (tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
+        if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
         break;
       }
       case CDR_EV_CHILD_STARTED: {  // :378-381 -> :3312-3325
-        const int slot = find_initiated(chi, hw_chi, B.ev.key[i]);
+        const int slot = find_initiated(chi, hw_chi, e.key);
         if (slot < 0) {
           FAIL(CDR_P_CHILD_STARTED_NIL);
           break;
         }
-        chi[slot].started_id = e_id;
-        chi[slot].started_run_id = B.ev.h[i];
+        chi[slot].started_id = e.id;
+        chi[slot].started_run_id = e.h;
         break;
       }
       case CDR_EV_CHILD_START_FAILED:
@@ -740,7 +737,7 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
       case CDR_EV_CHILD_CANCELED:
       case CDR_EV_CHILD_TIMED_OUT:
       case CDR_EV_CHILD_TERMINATED: {  // DeletePendingChildExecution :1138-1144
-        const int slot = find_initiated(chi, hw_chi, B.ev.key[i]);
+        const int slot = find_initiated(chi, hw_chi, e.key);
         if (slot >= 0) {
           chi[slot].initiated_id = DEAD_KEY;
           live_chi--;
@@ -748,24 +745,26 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         break;
       }
       case CDR_EV_RCE_INITIATED: {  // :408-427 -> :2577-2596
-        int slot = alloc_initiated(can, hw_can, cp.cancel_cap);
+        const int slot = alloc_initiated(can, hw_can, can_cap);
         if (slot < 0) {
           FAIL(CDR_E_BAD_INPUT);
           break;
         }
-        cdr_cancel_info c;
-        c.version = e_ver;
+        cdr_cancel_info& c = can[slot];
+        c.version = e.ver;
         c.initiated_event_batch_id = call_first_id;
-        c.initiated_id = e_id;
-        cdr_uuid(B.uuid_seed, d.wf_key, CDR_UUID_CANCEL_REQ, e_id, &c.cancel_request_lo, &c.cancel_request_hi);
-        can[slot] = c;
+        c.initiated_id = e.id;
+        uint64_t lo, hi;
+        cdr_uuid(B.uuid_seed, D.wf_key, CDR_UUID_CANCEL_REQ, e.id, &lo, &hi);
+        c.cancel_request_lo = lo;
+        c.cancel_request_hi = hi;
         live_can++;
-        if (tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
+        if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
         break;
       }
       case CDR_EV_RCE_FAILED:
       case CDR_EV_EXT_CANCEL_REQUESTED: {  // DeletePendingRequestCancel :1147-1153
-        const int slot = find_initiated(can, hw_can, B.ev.key[i]);
+        const int slot = find_initiated(can, hw_can, e.key);
         if (slot >= 0) {
           can[slot].initiated_id = DEAD_KEY;
           live_can--;
@@ -773,29 +772,30 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         break;
       }
       case CDR_EV_SE_INITIATED: {  // :439-458 -> :2701-2723
-        int slot = alloc_initiated(sig, hw_sig, cp.signal_cap);
+        const int slot = alloc_initiated(sig, hw_sig, sig_cap);
         if (slot < 0) {
           FAIL(CDR_E_BAD_INPUT);
           break;
         }
-        const uint64_t io = (uint64_t)B.ev.aux[i];
-        cdr_signal_info c;
-        c.version = e_ver;
+        cdr_signal_info& c = sig[slot];
+        c.version = e.ver;
         c.initiated_event_batch_id = call_first_id;
-        c.initiated_id = e_id;
-        cdr_uuid(B.uuid_seed, d.wf_key, CDR_UUID_SIGNAL_REQ, e_id, &c.signal_request_lo, &c.signal_request_hi);
-        c.signal_name = B.ev.h[i];
-        c.input = (uint32_t)(io >> 32);
-        c.control = (uint32_t)io;
+        c.initiated_id = e.id;
+        uint64_t lo, hi;
+        cdr_uuid(B.uuid_seed, D.wf_key, CDR_UUID_SIGNAL_REQ, e.id, &lo, &hi);
+        c.signal_request_lo = lo;
+        c.signal_request_hi = hi;
+        c.signal_name = e.h;
+        c.input = (uint32_t)((uint64_t)e.aux >> 32);
+        c.control = (uint32_t)e.aux;
         c._pad = 0;
-        sig[slot] = c;
         live_sig++;
-        if (tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
+        if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
         break;
       }
       case CDR_EV_SE_FAILED:
       case CDR_EV_EXT_SIGNALED: {  // DeletePendingSignal :1156-1162
-        const int slot = find_initiated(sig, hw_sig, B.ev.key[i]);
+        const int slot = find_initiated(sig, hw_sig, e.key);
         if (slot >= 0) {
           sig[slot].initiated_id = DEAD_KEY;
           live_sig--;
@@ -832,8 +832,8 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         break;
       }
       case CDR_EV_UPSERT_SA: {  // :533-535 -> :2746-2768
-        const uint64_t off = (uint64_t)B.ev.aux[i];
-        const uint32_t cnt = B.ev.h[i];
+        const uint64_t off = (uint64_t)e.aux;
+        const uint32_t cnt = e.h;
         for (uint32_t q = 0; q < cnt; q++) {
           const cdr_kv kv = B.kvs[off + q];
           bool found = false;
@@ -842,16 +842,13 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
               sa[j].value = kv.value;
               found = true;
             }
-          if (!found) {
-            if (n_sa >= cp.sa_cap) break;
-            sa[n_sa++] = kv;
-          }
+          if (!found && n_sa < sa_cap) sa[n_sa++] = kv;
         }
         x_flags |= CDR_XI_HAS_SEARCH_ATTR;
         break;
       }
       case CDR_EV_WF_CONTINUED_AS_NEW: {  // :537-595
-        if (d.newrun < 0 || call_idx != d.newrun_call || B.wfs[d.newrun].ev_len == 0) {
+        if (D.newrun < 0 || call_idx != D.newrun_call || B.wfs[D.newrun].ev_len == 0) {
           FAIL(CDR_E_NEWRUN_HISTORY_EMPTY);
           break;
         }
@@ -870,119 +867,130 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         break;
     }
   }
-  if (len > 0 && err == CDR_OK) finish_call();
-  else if (len > 0 && stop_at_call_end && isRS) {
-    // a failed call still raises the cluster panic first if its last event's version is unknown
-    const int src = cluster_for_version(B.cluster, prev_ver);
-    if (src < 0) {
-      err = CDR_P_UNKNOWN_CLUSTER;
-      err_id = call_first_id;
-      err_k = call_first_k;
+#undef FAIL
+  // ---- end of the last call
+  if (len > 0 && (err == CDR_OK || stop_at_call_end)) {
+    if (isRS) {
+      rs_lwv = prev_ver;
+      rs_lwid = prev_id;
+      const int src = cluster_for_version(B.cluster, prev_ver);
+      if (src < 0) {
+        err = CDR_P_UNKNOWN_CLUSTER;
+        err_id = call_first_id;
+        err_k = call_first_k;
+      } else if (src != B.cluster.current_cluster && err == CDR_OK) {
+        RS->lri_version[src] = prev_ver;
+        RS->lri_last_event_id[src] = prev_id;
+        rs_mask |= 1u << src;
+      }
+    }
+    if (err == CDR_OK) {
+      x_last_first = call_first_id;
+      x_next_event = prev_id + 1;
     }
   }
-  if (err == CDR_OK && d.parent < 0 && d.expected_next_event_id != 0 && x_next_event != d.expected_next_event_id) {
+  if (err == CDR_OK && D.parent < 0 && D.expected_next_event_id != 0 && x_next_event != D.expected_next_event_id) {
     err = CDR_E_REBUILD_NEXT_EVENT_ID;  // nDCStateRebuilder.go:139-143
     err_id = prev_id;
     err_k = len;
   }
-#undef FAIL
 
   cdr_wf_result r;
   r.code = err;
-  r.flags = newrun_applied ? CDR_RF_NEWRUN_APPLIED : 0u;
-  if (d.parent >= 0) r.flags |= CDR_RF_IS_NEWRUN;
+  r.flags = (newrun_applied ? CDR_RF_NEWRUN_APPLIED : 0u) | (D.parent >= 0 ? CDR_RF_IS_NEWRUN : 0u);
   r.fail_event_id = err_id;
   r.fail_index = err_k;
-  r.n_activity = r.n_timer = r.n_child = r.n_cancel = r.n_signal = 0;
-  r.n_vh = r.n_reset_points = r.n_search_attr = 0;
-  if (err == CDR_OK) {
-    r.n_activity = compact_sorted(act, hw_act, ActKey{});
-    for (uint32_t j = 0; j < r.n_activity; j++) act[j].flags &= ~AI_IN_AID_MAP;
-    r.n_timer = compact_sorted(tim, hw_tim, TimerKey{});
-    r.n_child = compact_sorted(chi, hw_chi, ChildKey{});
-    r.n_cancel = compact_sorted(can, hw_can, CancelKey{});
-    r.n_signal = compact_sorted(sig, hw_sig, SignalKey{});
-    r.n_vh = n_vh;
-    r.n_reset_points = n_rp;
-    // SearchAttributes is a Go map: canonical output order is ascending key
-    for (uint32_t a = 1; a < n_sa; a++) {
-      cdr_kv v = sa[a];
-      uint32_t b = a;
-      while (b > 0 && sa[b - 1].key > v.key) {
-        sa[b] = sa[b - 1];
-        b--;
-      }
-      sa[b] = v;
-    }
-    r.n_search_attr = n_sa;
-
-    cdr_exec_info x;
-    x.domain_id = (x_flags & CDR_XI_STARTED) ? d.domain_id : 0u;
-    x.workflow_id = (x_flags & CDR_XI_STARTED) ? d.workflow_id : 0u;
-    x.run_id = (x_flags & CDR_XI_STARTED) ? d.run_id : 0u;
-    x.create_request_id = x_create_req;
-    x.parent_domain_id = x_pdom;
-    x.parent_workflow_id = x_pwf;
-    x.parent_run_id = x_prun;
-    x.task_list = x_task_list;
-    x.workflow_type = x_wf_type;
-    x.decision_request_id = dreq;
-    x.cron_schedule = x_cron;
-    x.memo = x_memo;
-    x.nonretriable = x_nonretr;
-    x.branch_tree_id = (x_flags & (CDR_XI_HAS_BRANCH | CDR_XI_VH_BRANCH)) ? d.run_id : 0u;
-    x.flags = x_flags;
-    x._pad0 = 0;
-    x.initiated_id = x_initiated;
-    x.completion_event_batch_id = x_completion_batch;
-    x.workflow_timeout = x_wf_timeout;
-    x.decision_timeout_value = x_dt_timeout_value;
-    x.state = x_state;
-    x.close_status = x_close;
-    x.last_first_event_id = x_last_first;
-    x.last_event_task_id = x_last_task;
-    x.next_event_id = x_next_event;
-    x.last_processed_event = x_last_processed;
-    x.signal_count = x_signals;
-    x.decision_timeout = dto;
-    x.decision_version = dv;
-    x.decision_schedule_id = dsched;
-    x.decision_started_id = dstart;
-    x.decision_attempt = datt;
-    x.decision_started_ts = dst_ts;
-    x.decision_scheduled_ts = dsc_ts;
-    x.decision_original_scheduled_ts = dorig_ts;
-    x.attempt = x_attempt;
-    x.initial_interval = x_init_int;
-    x.backoff_coefficient = x_backoff;
-    x.maximum_interval = x_max_int;
-    x.maximum_attempts = x_max_att;
-    x.expiration_time = x_exp_time;
-    x.expiration_seconds = x_exp_s;
-    x._pad1 = 0;
-    x.branch_id_lo = x_br_lo;
-    x.branch_id_hi = x_br_hi;
-    x.reset_points_len = n_rp;
-    x.search_attr_len = n_sa;
-    O.exec[w] = x;
-    if (isRS) {
-      RS->current_version = rs_cur;
-      RS->start_version = rs_start;
-      RS->last_write_version = rs_lwv;
-      RS->last_write_event_id = rs_lwid;
-      for (int c = 0; c < CDR_MAX_CLUSTERS; c++)
-        if (!(rs_mask & (1u << c))) {
-          RS->lri_version[c] = 0;
-          RS->lri_last_event_id[c] = 0;
-        }
-      RS->lri_mask = rs_mask;
-      RS->present = 1;
-    } else {
-      cdr_repl_state z = {};
-      *RS = z;
-    }
-  }
+  // table high-water marks; k_tables compacts them to live counts
+  r.n_activity = hw_act;
+  r.n_timer = hw_tim;
+  r.n_child = hw_chi;
+  r.n_cancel = hw_can;
+  r.n_signal = hw_sig;
+  r.n_vh = n_vh;
+  r.n_reset_points = n_rp;
+  r.n_search_attr = n_sa;
   O.result[w] = r;
+  if (err != CDR_OK) return;
+  if (n_vh) vh[n_vh - 1] = cdr_vh_item{vh_last_id, vh_last_ver};
+  if (!(x_flags & CDR_XI_STARTED)) {  // no WorkflowExecutionStarted: its fields keep their zero values
+    X->domain_id = X->workflow_id = X->run_id = X->create_request_id = 0;
+    X->parent_domain_id = X->parent_workflow_id = X->parent_run_id = X->task_list = 0;
+    X->workflow_type = X->cron_schedule = X->memo = X->nonretriable = X->branch_tree_id = 0;
+    X->initiated_id = 0;
+    X->workflow_timeout = X->attempt = X->initial_interval = X->maximum_interval = X->maximum_attempts = 0;
+    X->expiration_seconds = 0;
+    X->backoff_coefficient = 0.0;
+    X->expiration_time = 0;
+    X->branch_id_lo = X->branch_id_hi = 0;
+  }
+  X->decision_request_id = dreq;
+  X->flags = x_flags;
+  X->_pad0 = 0;
+  X->completion_event_batch_id = x_completion_batch;
+  X->decision_timeout_value = x_dt_timeout_value;
+  X->state = x_state;
+  X->close_status = x_close;
+  X->last_first_event_id = x_last_first;
+  X->last_event_task_id = x_last_task;
+  X->next_event_id = x_next_event;
+  X->last_processed_event = x_last_processed;
+  X->signal_count = x_signals;
+  X->decision_timeout = dto;
+  X->decision_version = dv;
+  X->decision_schedule_id = dsched;
+  X->decision_started_id = dstart;
+  X->decision_attempt = datt;
+  X->decision_started_ts = dst_ts;
+  X->decision_scheduled_ts = dsc_ts;
+  X->decision_original_scheduled_ts = dorig_ts;
+  X->_pad1 = 0;
+  X->reset_points_len = n_rp;
+  X->search_attr_len = n_sa;
+  if (isRS) {
+    RS->current_version = rs_cur;
+    RS->start_version = rs_start;
+    RS->last_write_version = rs_lwv;
+    RS->last_write_event_id = rs_lwid;
+    for (int c = 0; c < CDR_MAX_CLUSTERS; c++)
+      if (!(rs_mask & (1u << c))) {
+        RS->lri_version[c] = 0;
+        RS->lri_last_event_id[c] = 0;
+      }
+    RS->lri_mask = rs_mask;
+    RS->present = 1;
+  } else {
+    *RS = cdr_repl_state{};
+  }
+}
+
+// Per-workflow table epilogue: move live rows to the front in key order (the
+// canonical order of the Go maps' keys), drop kernel-private flags, sort the
+// SearchAttributes map by key, and turn high-water marks into live counts.
+__global__ __launch_bounds__(256) void k_tables(cdr_dev_batch B, cdr_out O) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= B.n_wfs) return;
+  cdr_wf_result& r = O.result[w];
+  if (r.code != CDR_OK) return;
+  const cdr_wf_caps& cp = B.caps[w];
+  cdr_activity_info* act = O.act + cp.act_off;
+  const uint32_t na = compact_sorted(act, r.n_activity, ActKey{});
+  for (uint32_t j = 0; j < na; j++) act[j].flags &= ~AI_IN_AID_MAP;
+  r.n_activity = na;
+  r.n_timer = compact_sorted(O.timer + cp.timer_off, r.n_timer, TimerKey{});
+  r.n_child = compact_sorted(O.child + cp.child_off, r.n_child, ChildKey{});
+  r.n_cancel = compact_sorted(O.cancel + cp.cancel_off, r.n_cancel, CancelKey{});
+  r.n_signal = compact_sorted(O.signal + cp.signal_off, r.n_signal, SignalKey{});
+  cdr_kv* sa = O.sa + cp.sa_off;
+  const uint32_t n = r.n_search_attr;
+  for (uint32_t a = 1; a < n; a++) {
+    const cdr_kv v = sa[a];
+    uint32_t b = a;
+    while (b > 0 && sa[b - 1].key > v.key) {
+      sa[b] = sa[b - 1];
+      b--;
+    }
+    sa[b] = v;
+  }
 }
 
 // continue-as-new stitching (stateBuilder.go:557-574): a parent that applied its new
@@ -1017,8 +1025,10 @@ __global__ void k_finalize(cdr_dev_batch B, cdr_out O) {
 struct cdr_ctx {
   int device;
   hipEvent_t ev[4];
-  float replay_ms, finalize_ms;
   bool timed;
+  // optional per-launch timing ring (bench): event pairs around every replay kernel
+  std::vector<hipEvent_t> ring;
+  uint32_t ring_used = 0;
 };
 
 #define HIPCHK(x)                                                                      \
@@ -1050,6 +1060,7 @@ cdr_ctx* cdr_create(int device) {
 void cdr_destroy(cdr_ctx* c) {
   if (!c) return;
   for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
+  for (hipEvent_t e : c->ring) (void)hipEventDestroy(e);
   delete c;
 }
 
@@ -1059,11 +1070,20 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   HIPCHK(hipSetDevice(c->device));
   const uint32_t threads = in->ev.n_slices * CDR_SLICE_WIDTH;
   const uint32_t blocks = (threads + 255) / 256;
-  HIPCHK(hipEventRecord(c->ev[0], st));
+  const bool ring = c->ring_used + 2 <= c->ring.size();
+  HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
   if (blocks) hipLaunchKernelGGL(k_replay, dim3(blocks), dim3(256), 0, st, *in, *out);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(c->ev[1], st));
+  HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used + 1] : c->ev[1], st));
+  if (ring) {
+    // keep ev[0..1] meaningful for cdr_last_kernel_ms as well
+    c->ring_used += 2;
+    HIPCHK(hipEventRecord(c->ev[0], st));
+    HIPCHK(hipEventRecord(c->ev[1], st));
+  }
   const uint32_t fb = (in->n_wfs + 255) / 256;
+  if (fb) hipLaunchKernelGGL(k_tables, dim3(fb), dim3(256), 0, st, *in, *out);
+  HIPCHK(hipGetLastError());
   if (fb) hipLaunchKernelGGL(k_finalize, dim3(fb), dim3(256), 0, st, *in, *out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[2], st));
@@ -1079,6 +1099,38 @@ int cdr_last_kernel_ms(cdr_ctx* c, float* replay_ms, float* finalize_ms) {
   HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
   if (replay_ms) *replay_ms = a;
   if (finalize_ms) *finalize_ms = b;
+  return CDR_API_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// Start recording the replay kernel of the next `max_launches` launches with HIP
+// events on their launch stream (bench.py's in-process kernel timing).
+int cdr_timing_begin(cdr_ctx* c, uint32_t max_launches) {
+  if (!c) return CDR_API_EINVAL;
+  HIPCHK(hipSetDevice(c->device));
+  while (c->ring.size() < 2ull * max_launches) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    c->ring.push_back(e);
+  }
+  c->ring_used = 0;
+  return CDR_API_OK;
+}
+
+// Synchronise and return the recorded replay-kernel durations (ms); *n in = capacity,
+// out = launches recorded.  Stops recording.
+int cdr_timing_read(cdr_ctx* c, float* ms, uint32_t* n) {
+  if (!c || !n) return CDR_API_EINVAL;
+  const uint32_t k = c->ring_used / 2;
+  for (uint32_t i = 0; i < k && i < *n; i++) {
+    HIPCHK(hipEventSynchronize(c->ring[2 * i + 1]));
+    HIPCHK(hipEventElapsedTime(&ms[i], c->ring[2 * i], c->ring[2 * i + 1]));
+  }
+  *n = k < *n ? k : *n;
+  c->ring_used = (uint32_t)c->ring.size();  // full: later launches are not recorded
   return CDR_API_OK;
 }
 

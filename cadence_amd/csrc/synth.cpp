@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <system_error>
 #include <thread>
@@ -518,7 +519,8 @@ int default_builder(int cfg, Rng& r) {
 }
 
 // generate workflow `w` (pure function of params and w)
-void gen_one(const cdr_synth_params& P, uint32_t w, WfOut& o) {
+void gen_one(const cdr_synth_params& P, uint32_t local, WfOut& o) {
+  const uint32_t w = P.index_map ? P.index_map[local] : local;  // global workflow index
   Gen g(P, w, o);
   Rng r2(P.seed ^ cdr_mix64(0xB17D + (uint64_t)w));
   const int builder = P.builder >= 0 ? P.builder : default_builder(P.config, r2);
@@ -904,6 +906,16 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
   cluster_meta(&meta->cluster);
   meta->now_ns = 1700000000000000000ll;
   meta->uuid_seed = p->seed * 0x9E3779B97F4A7C15ull + 1;
+  return CDR_API_OK;
+}
+
+int cdr_synth_shards(uint64_t n, int32_t num_shards, int32_t* out) {
+  if (!out || num_shards <= 0) return CDR_API_EINVAL;
+  par((uint32_t)n, 0, [&](uint32_t i) {
+    char buf[32];
+    int len = snprintf(buf, sizeof buf, "wf-%u", i);
+    out[i] = cdr_workflow_id_to_shard(buf, (size_t)len, num_shards);
+  });
   return CDR_API_OK;
 }
 

@@ -146,6 +146,11 @@ int32_t cdr_workflow_id_to_shard(const char* workflow_id, size_t len, int32_t nu
  * the replay kernel measured with HIP events on the launch stream. */
 int cdr_last_kernel_ms(cdr_ctx* ctx, float* replay_ms, float* finalize_ms);
 
+/* Per-launch timing ring: record the replay kernel of the next max_launches launches
+ * with HIP events on their stream; read back durations (ms) after the fact. */
+int cdr_timing_begin(cdr_ctx* ctx, uint32_t max_launches);
+int cdr_timing_read(cdr_ctx* ctx, float* ms, uint32_t* n);
+
 const char* cdr_version(void);
 
 #ifdef __cplusplus

@@ -18,6 +18,7 @@ typedef struct cdr_synth_params {
   double error_rate;    /* fraction of workflows with one injected fault */
   int32_t builder;      /* -1 = config default, else cdr_builder */
   int32_t rebuild;      /* set expected_next_event_id (nDCStateRebuilder check) */
+  const uint32_t* index_map; /* optional [n_wfs]: global index of each generated workflow */
 } cdr_synth_params;
 typedef struct cdr_synth_sizes {
   uint64_t n_events;
@@ -36,6 +37,9 @@ int cdr_synth_fill(const cdr_synth_params* p, cdr_event* ev, cdr_wf_desc* wfs, c
 int cdr_synth_sliced_plan(const cdr_synth_params* p, cdr_synth_plan_info* info);
 int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc* wfs, cdr_wf_caps* caps,
                           cdr_kv* kvs, cdr_reset_point* rps, cdr_batch* meta, int threads);
+/* history shard of synthetic workflow ids "wf-<i>", i in [0, n): farmhash
+ * Fingerprint32 % num_shards (common/util.go:249-252) */
+int cdr_synth_shards(uint64_t n, int32_t num_shards, int32_t* out);
 #ifdef __cplusplus
 }
 #endif
