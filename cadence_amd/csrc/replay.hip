@@ -900,7 +900,9 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
   r.flags = (newrun_applied ? CDR_RF_NEWRUN_APPLIED : 0u) | (D.parent >= 0 ? CDR_RF_IS_NEWRUN : 0u);
   r.fail_event_id = err_id;
   r.fail_index = err_k;
-  // table high-water marks; k_tables compacts them to live counts
+  // table high-water marks; k_tables compacts them to live counts (a failed
+  // workflow reports no state)
+  if (err != CDR_OK) hw_act = hw_tim = hw_chi = hw_can = hw_sig = n_vh = n_rp = n_sa = 0;
   r.n_activity = hw_act;
   r.n_timer = hw_tim;
   r.n_child = hw_chi;

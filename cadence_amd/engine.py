@@ -183,10 +183,10 @@ def compare(batch: Batch, a: Outputs, b: Outputs, limit: int = 10):
     bad = []
     for w in range(batch.n_wfs):
         ra, rb = a.result[w], b.result[w]
-        ka = (ra.code, ra.flags, ra.fail_event_id, ra.fail_index)
-        kb = (rb.code, rb.flags, rb.fail_event_id, rb.fail_index)
+        ka = _bytes(ra)
+        kb = _bytes(rb)
         if ka != kb:
-            bad.append(f"wf {w}: result {ka} != {kb}")
+            bad.append(f"wf {w}: result {_rec(ra, None)} != {_rec(rb, None)}")
         elif ra.code == abi.OK:
             if _bytes(a.exec[w]) != _bytes(b.exec[w]):
                 diffs = [f for f, _ in abi.CdrExecInfo._fields_
