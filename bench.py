@@ -94,6 +94,9 @@ class DeviceBatch:
         self.h_lane = np.empty(info.n_slices * 64, np.int32)
         self.h_slen = np.empty(info.n_slices, np.uint32)
         self.h_row0 = np.empty(info.n_slices, np.uint64)
+        self.h_sc_off = np.zeros(info.n_slices, np.uint64)
+        self.h_sc_act = np.zeros(info.n_slices, np.uint32)
+        self.h_sc_tim = np.zeros(info.n_slices, np.uint32)
         self.h_arena = np.empty(max(1, info.arena_words), np.uint64)
         self.h_wfs = (abi.CdrWfDesc * info.n_entries)()
         self.h_caps = (abi.CdrWfCaps * info.n_entries)()
@@ -105,6 +108,8 @@ class DeviceBatch:
         for k, v in self.h_cols.items():
             setattr(s, k, v.ctypes.data)
         s.arena = self.h_arena.ctypes.data
+        s.slice_scratch_off, s.slice_act_slots, s.slice_tim_slots = (
+            self.h_sc_off.ctypes.data, self.h_sc_act.ctypes.data, self.h_sc_tim.ctypes.data)
         meta = abi.CdrBatch()
         threads = min(32, os.cpu_count() or 8)
         rc = L.cdr_synth_sliced_fill(C.byref(p), C.byref(s), self.h_wfs, self.h_caps, self.h_kvs.ctypes.data,
@@ -131,6 +136,13 @@ class DeviceBatch:
         for k, v in self.h_cols.items():
             setattr(db.ev, k, up(v))
         db.ev.arena = up(self.h_arena)
+        db.ev.slice_scratch_off = up(self.h_sc_off)
+        db.ev.slice_act_slots = up(self.h_sc_act)
+        db.ev.slice_tim_slots = up(self.h_sc_tim)
+        L.cdr_plan_scratch(self.h_caps, self.h_lane.ctypes.data, info.n_slices, None, None, None,
+                           C.byref(sc_words := C.c_uint64()))
+        self.scratch_t = torch.zeros(max(8, sc_words.value * 8), dtype=torch.uint8, device=dev)
+        db.scratch = self.scratch_t.data_ptr()
         db.wfs, db.caps = up_ct(self.h_wfs), up_ct(self.h_caps)
         db.kvs, db.rps = up(self.h_kvs), up_ct(self.h_rps)
         db.n_wfs = info.n_entries

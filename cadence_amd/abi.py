@@ -171,16 +171,17 @@ CdrWfResult = _S("cdr_wf_result", [
 CdrWfCaps = _S("cdr_wf_caps", [
     ("act_off", u64), ("timer_off", u64), ("child_off", u64), ("cancel_off", u64), ("signal_off", u64),
     ("vh_off", u64), ("rp_off", u64), ("sa_off", u64), ("act_cap", u32), ("timer_cap", u32), ("child_cap", u32),
-    ("cancel_cap", u32), ("signal_cap", u32), ("vh_cap", u32), ("rp_cap", u32), ("sa_cap", u32)])
+    ("cancel_cap", u32), ("signal_cap", u32), ("vh_cap", u32), ("rp_cap", u32), ("sa_cap", u32),
+    ("act_live", u32), ("timer_live", u32)])
 CdrTotals = _S("cdr_totals", [(n, u64) for n in ("act", "timer", "child", "cancel", "signal", "vh", "rp", "sa")])
 CdrOut = _S("cdr_out", [(n, C.c_void_p) for n in (
     "result", "exec", "repl", "vh", "act", "timer", "child", "cancel", "signal", "rp", "sa")])
 CdrSlices = _S("cdr_slices", [
     ("n_slices", u32), ("_pad", u32), ("n_rows", u64), ("arena_words", u64)] + [(n, C.c_void_p) for n in (
         "slice_row0", "slice_len", "lane_wf", "type_flags", "event_id", "version", "timestamp", "task_id", "key",
-        "aux", "h", "n", "arena")])
+        "aux", "h", "n", "arena", "slice_scratch_off", "slice_act_slots", "slice_tim_slots")])
 CdrDevBatch = _S("cdr_dev_batch", [
-    ("ev", CdrSlices), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
+    ("ev", CdrSlices), ("scratch", C.c_void_p), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
     ("n_wfs", u32), ("empty_uuid", u32), ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64)])
 
 # ------------------------------------------------------------------ synth
@@ -209,6 +210,7 @@ EXPORTS = {
     "cdr_plan_slices": (i32, [C.POINTER(CdrWfDesc), u32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(u32),
                               C.POINTER(u64)]),
     "cdr_plan_arena_words": (u64, [C.POINTER(CdrBatch)]),
+    "cdr_plan_scratch": (i32, [C.c_void_p, C.c_void_p, u32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(u64)]),
     "cdr_pack_slices": (i32, [C.POINTER(CdrBatch), C.POINTER(CdrSlices), i32]),
     "cdr_create": (C.c_void_p, [i32]),
     "cdr_destroy": (None, [C.c_void_p]),

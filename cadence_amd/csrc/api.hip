@@ -245,6 +245,15 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   db.ev.h = (const uint32_t*)up(hh.data(), ne * 4);
   db.ev.n = (const int32_t*)up(nn.data(), ne * 4);
   db.ev.arena = (const uint64_t*)up(arena.data(), arena.size() * 8);
+  std::vector<uint64_t> sc_off(ns);
+  std::vector<uint32_t> sc_act(ns), sc_tim(ns);
+  uint64_t sc_words = 0;
+  rc = cdr_plan_scratch(caps, lane.data(), ns, sc_off.data(), sc_act.data(), sc_tim.data(), &sc_words);
+  if (rc) return rc;
+  db.ev.slice_scratch_off = (const uint64_t*)up(sc_off.data(), ns * 8ull);
+  db.ev.slice_act_slots = (const uint32_t*)up(sc_act.data(), ns * 4ull);
+  db.ev.slice_tim_slots = (const uint32_t*)up(sc_tim.data(), ns * 4ull);
+  db.scratch = (uint64_t*)dz(sc_words * 8);
   db.wfs = (const cdr_wf_desc*)up(b->wfs, (uint64_t)b->n_wfs * sizeof(cdr_wf_desc));
   db.caps = (const cdr_wf_caps*)up(caps, (uint64_t)b->n_wfs * sizeof(cdr_wf_caps));
   db.kvs = (const cdr_kv*)up(b->kvs, b->n_kvs * sizeof(cdr_kv));

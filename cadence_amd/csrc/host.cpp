@@ -76,8 +76,15 @@ void caps_one(const cdr_event* ev, uint64_t n, cdr_wf_caps* out) {
   bool have_ver = false;
   int64_t last_ver = 0;
   uint32_t vh = 0;
+  int64_t live = 0, live_max = 0;
   for (uint64_t k = 0; k < n; k++) {
     const cdr_event& e = ev[k];
+    // live-activity bound: a close of a missing activity stops the replay, so before
+    // the first error every close removed one live activity
+    if (e.type == CDR_EV_AT_SCHEDULED) live_max = std::max(live_max, ++live);
+    if (e.type == CDR_EV_AT_COMPLETED || e.type == CDR_EV_AT_FAILED || e.type == CDR_EV_AT_TIMED_OUT ||
+        e.type == CDR_EV_AT_CANCELED)
+      live = std::max<int64_t>(0, live - 1);
     if (!have_ver || e.version > last_ver) {
       vh++;
       last_ver = e.version;
@@ -114,6 +121,8 @@ void caps_one(const cdr_event* ev, uint64_t n, cdr_wf_caps* out) {
     }
   }
   c.vh_cap = vh;
+  c.act_live = (uint32_t)live_max;
+  c.timer_live = c.timer_cap;
   *out = c;
 }
 
@@ -325,6 +334,27 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
   }
   if (n_slices) *n_slices = ns;
   if (n_rows) *n_rows = rows;
+  return CDR_API_OK;
+}
+
+int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n_slices, uint64_t* scratch_off,
+                     uint32_t* act_slots, uint32_t* tim_slots, uint64_t* total_words) {
+  if (!caps || !lane_wf || !total_words) return CDR_API_EINVAL;
+  uint64_t off = 0;
+  for (uint32_t s = 0; s < n_slices; s++) {
+    uint32_t a = 0, t = 0;
+    for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
+      const int32_t w = lane_wf[(size_t)s * CDR_SLICE_WIDTH + l];
+      if (w < 0) continue;
+      a = std::max(a, caps[w].act_live);
+      t = std::max(t, caps[w].timer_live);
+    }
+    if (scratch_off) scratch_off[s] = off;
+    if (act_slots) act_slots[s] = a;
+    if (tim_slots) tim_slots[s] = t;
+    off += ((uint64_t)a * CDR_ACT_PLANES + (uint64_t)t * CDR_TIM_PLANES) * CDR_SLICE_WIDTH;
+  }
+  *total_words = off;
   return CDR_API_OK;
 }
 

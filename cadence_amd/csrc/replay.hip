@@ -70,81 +70,6 @@ __device__ __forceinline__ int cluster_for_version(const cdr_cluster_meta& m, in
   return r;
 }
 
-// activity timer pick over the live slots (timerBuilder.go:211-312): head candidate by
-// (time, scheduleID, candidate order); OR its bit into TimerTaskStatus if not set.
-__device__ void activity_timer_pick(cdr_activity_info* rows, uint32_t hw) {
-  int best = -1;
-  int64_t bt = 0, bs = 0;
-  int bo = 0;
-  int32_t bbit = 0;
-  for (uint32_t j = 0; j < hw; j++) {
-    const cdr_activity_info& r = rows[j];
-    const int64_t sched = r.schedule_id;
-    if (sched == DEAD_KEY) continue;
-    int64_t t = r.scheduled_time + (int64_t)r.s2c * NS_PER_S;
-    if (r.expiration_time < t) t = r.expiration_time;  // ExpirationTime is always set on replay
-    int o = 0;
-    int32_t bit = CDR_TTS_SCHEDULE_TO_CLOSE;
-    int64_t t2, t3 = 0;
-    int32_t bit2;
-    bool has3 = false;
-    if (r.started_id != CDR_EMPTY_EVENT_ID) {
-      const int64_t st = r.started_time;
-      t2 = st + (int64_t)r.stc * NS_PER_S;
-      bit2 = CDR_TTS_START_TO_CLOSE;
-      if (r.hb > 0) {
-        int64_t lhb = r.last_heartbeat_time;
-        if (lhb < st) lhb = st;
-        t3 = lhb + (int64_t)r.hb * NS_PER_S;
-        has3 = true;
-      }
-    } else {
-      t2 = r.scheduled_time + (int64_t)r.s2s * NS_PER_S;
-      bit2 = CDR_TTS_SCHEDULE_TO_START;
-    }
-    // best of this activity (append order breaks ties: S2C, then STC/S2S, then HB)
-    if (t2 < t) {
-      t = t2;
-      o = 1;
-      bit = bit2;
-    }
-    if (has3 && t3 < t) {
-      t = t3;
-      o = 2;
-      bit = CDR_TTS_HEARTBEAT;
-    }
-    if (best < 0 || t < bt || (t == bt && (sched < bs || (sched == bs && o < bo)))) {
-      best = (int)j;
-      bt = t;
-      bs = sched;
-      bo = o;
-      bbit = bit;
-    }
-  }
-  if (best >= 0) {
-    int32_t st = rows[best].timer_task_status;
-    if (!(st & bbit)) rows[best].timer_task_status = st | bbit;
-  }
-}
-
-// user timer pick (timerBuilder.go:171-184,233-247): head by (ExpiryTime, StartedID)
-__device__ void user_timer_pick(cdr_timer_info* rows, uint32_t hw) {
-  int best = -1;
-  int64_t be = 0, bs = 0;
-  for (uint32_t j = 0; j < hw; j++) {
-    const int64_t s = rows[j].started_id;
-    if (s == DEAD_KEY) continue;
-    const int64_t e = rows[j].expiry_time;
-    if (best < 0 || e < be || (e == be && s < bs)) {
-      best = (int)j;
-      be = e;
-      bs = s;
-    }
-  }
-  if (best >= 0 && rows[best].task_id != CDR_TIMER_TASK_STATUS_CREATED)
-    rows[best].task_id = CDR_TIMER_TASK_STATUS_CREATED;
-}
-
 // Move live rows (key != DEAD) to the front, ascending by key (selection sort; live
 // sets are small).  Returns the live count.
 template <class Row, class KeyF>
@@ -208,6 +133,102 @@ __device__ __forceinline__ int alloc_initiated(const Row* rows, uint32_t& hw, ui
 
 }  // namespace
 
+// ---- lane-interleaved working state (cdr.h: slice_scratch_off)
+// activity working slot planes (8-byte words); plane p of slot j of lane L lives at
+// word (j*CDR_ACT_PLANES + p)*64 + L of the slice's scratch, so a wavefront that
+// touches slot j of its 64 workflows issues one coalesced 512-B access.
+enum : uint32_t {
+  AP_SID = 0,       // scheduleID (DEAD_KEY = free slot)
+  AP_META = 1,      // activityID handle | flags << 32
+  AP_TTS = 2,       // TimerTaskStatus | RequestID handle << 32
+  AP_VER = 3,
+  AP_TS2C = 4,      // ScheduleToClose candidate: min(sched + s2c, ExpirationTime)
+  AP_TALT = 5,      // ScheduleToStart candidate before start, StartToClose after
+  AP_THB = 6,       // Heartbeat candidate (started and hb > 0) else INT64_MAX
+  AP_STARTED_ID = 7,
+  AP_STARTED_TIME = 8,
+  AP_CANCEL_ID = 9,
+  AP_AREC = 10,     // arena word offset of the ActivityTaskScheduled record
+  AP_SCHED_TIME = 11,
+  AP_BATCH = 12,
+  AP_EXP = 13,
+  AP_STC_HB = 14,   // StartToClose | HeartbeatTimeout << 32 (seconds)
+};
+static_assert(AP_STC_HB + 1 == CDR_ACT_PLANES, "activity planes");
+enum : uint32_t { TP_SID = 0, TP_TID_TASK = 1, TP_EXPIRY = 2, TP_VER = 3 };
+static_assert(TP_VER + 1 == CDR_TIM_PLANES, "timer planes");
+#define AF_AIDMAP 0x1u    /* this slot holds byActivityID[aid] */
+#define AF_STARTED 0x2u
+#define AF_CANCEL 0x4u
+#define T_NONE ((int64_t)0x7FFFFFFFFFFFFFFFll)
+
+struct Lanes {  // slot/plane addressing of one lane's working state
+  uint64_t* base;
+  uint32_t P;
+  __device__ __forceinline__ int64_t& operator()(uint32_t slot, uint32_t plane) const {
+    return *reinterpret_cast<int64_t*>(base + ((uint64_t)slot * P + plane) * CDR_SLICE_WIDTH);
+  }
+};
+
+// activity timer pick (timerBuilder.go:211-312) over the live working slots
+__device__ __forceinline__ void act_pick(const Lanes& A, uint32_t hw) {
+  int best = -1;
+  int64_t bt = 0, bs = 0;
+  int bo = 0;
+  uint32_t bbit = 0;
+  for (uint32_t j = 0; j < hw; j++) {
+    const int64_t sid = A(j, AP_SID);
+    if (sid == DEAD_KEY) continue;
+    const uint32_t fl = (uint32_t)((uint64_t)A(j, AP_META) >> 32);
+    int64_t t = A(j, AP_TS2C);
+    int o = 0;
+    uint32_t bit = CDR_TTS_SCHEDULE_TO_CLOSE;
+    const int64_t ta = A(j, AP_TALT), th = A(j, AP_THB);
+    if (ta < t) {  // append order breaks ties: S2C, then STC/S2S, then HB
+      t = ta;
+      o = 1;
+      bit = (fl & AF_STARTED) ? CDR_TTS_START_TO_CLOSE : CDR_TTS_SCHEDULE_TO_START;
+    }
+    if (th < t) {
+      t = th;
+      o = 2;
+      bit = CDR_TTS_HEARTBEAT;
+    }
+    if (best < 0 || t < bt || (t == bt && (sid < bs || (sid == bs && o < bo)))) {
+      best = (int)j;
+      bt = t;
+      bs = sid;
+      bo = o;
+      bbit = bit;
+    }
+  }
+  if (best >= 0) {
+    const uint64_t v = (uint64_t)A((uint32_t)best, AP_TTS);
+    if (!((uint32_t)v & bbit)) A((uint32_t)best, AP_TTS) = (int64_t)(v | bbit);
+  }
+}
+
+// user timer pick (timerBuilder.go:171-184,233-247): head by (ExpiryTime, StartedID)
+__device__ __forceinline__ void tim_pick(const Lanes& T, uint32_t hw) {
+  int best = -1;
+  int64_t be = 0, bs = 0;
+  for (uint32_t j = 0; j < hw; j++) {
+    const int64_t sid = T(j, TP_SID);
+    if (sid == DEAD_KEY) continue;
+    const int64_t ex = T(j, TP_EXPIRY);
+    if (best < 0 || ex < be || (ex == be && sid < bs)) {
+      best = (int)j;
+      be = ex;
+      bs = sid;
+    }
+  }
+  if (best >= 0) {
+    const uint64_t v = (uint64_t)T((uint32_t)best, TP_TID_TASK);
+    if ((v >> 32) != CDR_TIMER_TASK_STATUS_CREATED)
+      T((uint32_t)best, TP_TID_TASK) = (int64_t)((v & 0xFFFFFFFFull) | ((uint64_t)CDR_TIMER_TASK_STATUS_CREATED << 32));
+  }
+}
+
 // ============================================================== replay kernel
 namespace {
 
@@ -259,8 +280,14 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
   cdr_kv* sa = O.sa + CP.sa_off;
   cdr_exec_info* X = O.exec + w;
   cdr_repl_state* RS = O.repl + w;
-  const uint32_t act_cap = CP.act_cap, tim_cap = CP.timer_cap, chi_cap = CP.child_cap, can_cap = CP.cancel_cap,
-                 sig_cap = CP.signal_cap, vh_cap = CP.vh_cap, rp_cap = CP.rp_cap, sa_cap = CP.sa_cap;
+  const uint32_t chi_cap = CP.child_cap, can_cap = CP.cancel_cap, sig_cap = CP.signal_cap, vh_cap = CP.vh_cap,
+                 rp_cap = CP.rp_cap, sa_cap = CP.sa_cap;
+  // working slots of pending activities / user timers (lane-interleaved scratch)
+  const uint32_t act_cap = B.ev.slice_act_slots[s], tim_cap = B.ev.slice_tim_slots[s];
+  uint64_t* const lane_scratch = B.scratch + B.ev.slice_scratch_off[s] + (g & 63);
+  const Lanes A{lane_scratch, CDR_ACT_PLANES};
+  const Lanes T{lane_scratch + (uint64_t)act_cap * CDR_ACT_PLANES * CDR_SLICE_WIDTH, CDR_TIM_PLANES};
+  uint32_t cks_ok = 0;  // a binary checksum known to be in AutoResetPoints
 
   // ---- ExecutionInfo fields that later events change (registers); the fields only
   // WorkflowExecutionStarted writes go straight to the output record.
@@ -430,6 +457,7 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         }
         // rolloverAutoResetPointsWithExpiringTime (:3184-3205)
         n_rp = 0;
+        cks_ok = 0;
         x_flags &= ~CDR_XI_HAS_RESET_POINTS;
         if (af & CDR_SF_HAS_RESET_POINTS) {
           x_flags |= CDR_XI_HAS_RESET_POINTS;
@@ -503,7 +531,7 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         dsc_ts = 0;  // OriginalScheduledTimestamp kept
         x_last_processed = e.aux;
         const uint32_t cks = e.h;
-        if (cks) {  // addBinaryCheckSumIfNotExists (mutableStateBuilder.go:1798-1842)
+        if (cks && cks != cks_ok) {  // addBinaryCheckSumIfNotExists (mutableStateBuilder.go:1798-1842)
           bool exists = false;
           for (uint32_t q = 0; q < n_rp; q++) {
             const cdr_reset_point& p = rp[q];
@@ -526,6 +554,7 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
             p._pad = 0;
             x_flags |= CDR_XI_HAS_RESET_POINTS;
           }
+          cks_ok = cks;  // the list only grows until the next WorkflowExecutionStarted
         }
         break;
       }
@@ -554,11 +583,12 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
         const uint32_t aid = (uint32_t)e.key;
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++) {
-          cdr_activity_info& r = act[j];
-          if (r.schedule_id == DEAD_KEY) {
+          if (A(j, AP_SID) == DEAD_KEY) {
             if (slot < 0) slot = (int)j;
-          } else if (r.activity_id == aid && (r.flags & AI_IN_AID_MAP)) {
-            r.flags &= ~AI_IN_AID_MAP;  // byActivityID[aid] is overwritten
+          } else {
+            const uint64_t m = (uint64_t)A(j, AP_META);
+            if ((uint32_t)m == aid && ((m >> 32) & AF_AIDMAP))  // byActivityID[aid] is overwritten
+              A(j, AP_META) = (int64_t)(m & ~((uint64_t)AF_AIDMAP << 32));
           }
         }
         if (slot < 0) {
@@ -568,52 +598,48 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
           }
           slot = (int)hw_act++;
         }
+        const uint32_t j = (uint32_t)slot;
         const int32_t s2c = a->s2c_s, xs = a->retry_expiration_s;
         const bool retry = (a->flags & CDR_AF_HAS_RETRY) != 0;
-        cdr_activity_info& r = act[slot];
-        r.version = e.ver;
-        r.schedule_id = e.id;
-        r.scheduled_event_batch_id = call_first_id;
-        r.scheduled_time = e.ts;
-        r.started_id = CDR_EMPTY_EVENT_ID;
-        r.started_time = 0;
-        r.last_heartbeat_time = 0;
-        r.expiration_time = e.ts + (int64_t)((retry && xs > s2c) ? xs : s2c) * NS_PER_S;
-        r.cancel_request_id = CDR_EMPTY_EVENT_ID;
-        r.activity_id = aid;
-        r.request_id = 0;
-        r.task_list = a->task_list;
-        r.nonretriable = retry ? a->nonretriable : 0u;
-        r.s2s = a->s2s_s;
-        r.s2c = s2c;
-        r.stc = a->stc_s;
-        r.hb = a->hb_s;
-        r.timer_task_status = CDR_TIMER_TASK_STATUS_NONE;
-        r.attempt = 0;
-        r.initial_interval = retry ? a->retry_initial_s : 0;
-        r.maximum_interval = retry ? a->retry_max_interval_s : 0;
-        r.maximum_attempts = retry ? a->retry_max_attempts : 0;
-        r.flags = (retry ? CDR_AI_HAS_RETRY : 0u) | AI_IN_AID_MAP;
-        r.backoff_coefficient = retry ? a->backoff_coefficient : 0.0;
-        activity_timer_pick(act, hw_act);
+        const int64_t exp = e.ts + (int64_t)((retry && xs > s2c) ? xs : s2c) * NS_PER_S;
+        const int64_t t_s2c = e.ts + (int64_t)s2c * NS_PER_S;
+        A(j, AP_SID) = e.id;
+        A(j, AP_META) = (int64_t)(aid | ((uint64_t)AF_AIDMAP << 32));
+        A(j, AP_TTS) = CDR_TIMER_TASK_STATUS_NONE;
+        A(j, AP_VER) = e.ver;
+        A(j, AP_TS2C) = exp < t_s2c ? exp : t_s2c;
+        A(j, AP_TALT) = e.ts + (int64_t)a->s2s_s * NS_PER_S;
+        A(j, AP_THB) = T_NONE;
+        A(j, AP_STARTED_ID) = CDR_EMPTY_EVENT_ID;
+        A(j, AP_STARTED_TIME) = 0;
+        A(j, AP_CANCEL_ID) = CDR_EMPTY_EVENT_ID;
+        A(j, AP_AREC) = e.aux;
+        A(j, AP_SCHED_TIME) = e.ts;
+        A(j, AP_BATCH) = call_first_id;
+        A(j, AP_EXP) = exp;
+        A(j, AP_STC_HB) = (int64_t)((uint32_t)a->stc_s | ((uint64_t)(uint32_t)a->hb_s << 32));
+        act_pick(A, hw_act);
         break;
       }
       case CDR_EV_AT_STARTED: {  // :271-278 -> :2083-2098
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++)
-          if (act[j].schedule_id == e.key) slot = (int)j;
+          if (A(j, AP_SID) == e.key) slot = (int)j;
         if (slot < 0) {
           FAIL(CDR_P_ACTIVITY_STARTED_NIL);  // nil deref in Go
           break;
         }
-        cdr_activity_info& r = act[slot];
-        r.version = e.ver;
-        r.started_id = e.id;
-        r.request_id = e.h;
-        r.started_time = e.ts;
-        r.last_heartbeat_time = e.ts;
-        r.flags |= CDR_AI_STARTED_TIME_SET;
-        activity_timer_pick(act, hw_act);
+        const uint32_t j = (uint32_t)slot;
+        const uint64_t th = (uint64_t)A(j, AP_STC_HB);
+        const int32_t stc = (int32_t)(uint32_t)th, hb = (int32_t)(uint32_t)(th >> 32);
+        A(j, AP_VER) = e.ver;
+        A(j, AP_STARTED_ID) = e.id;
+        A(j, AP_TTS) = (int64_t)(((uint64_t)(uint32_t)A(j, AP_TTS)) | ((uint64_t)e.h << 32));
+        A(j, AP_STARTED_TIME) = e.ts;  // LastHeartBeatUpdatedTime = StartedTime
+        A(j, AP_META) = (int64_t)((uint64_t)A(j, AP_META) | ((uint64_t)AF_STARTED << 32));
+        A(j, AP_TALT) = e.ts + (int64_t)stc * NS_PER_S;
+        A(j, AP_THB) = hb > 0 ? e.ts + (int64_t)hb * NS_PER_S : T_NONE;
+        act_pick(A, hw_act);
         break;
       }
       case CDR_EV_AT_COMPLETED:  // :280-305,312-319 -> DeleteActivity :1247-1269
@@ -622,51 +648,57 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
       case CDR_EV_AT_CANCELED: {
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++)
-          if (act[j].schedule_id == e.key) slot = (int)j;
+          if (A(j, AP_SID) == e.key) slot = (int)j;
         if (slot < 0) {
           FAIL(CDR_E_ACTIVITY_NOT_FOUND);
           break;
         }
-        const uint32_t aid = act[slot].activity_id;
-        const uint32_t fl = act[slot].flags;
-        act[slot].schedule_id = DEAD_KEY;
-        act[slot].flags = fl & ~AI_IN_AID_MAP;
-        bool found = (fl & AI_IN_AID_MAP) != 0;
+        const uint64_t m = (uint64_t)A((uint32_t)slot, AP_META);
+        const uint32_t aid = (uint32_t)m;
+        A((uint32_t)slot, AP_SID) = DEAD_KEY;
+        A((uint32_t)slot, AP_META) = (int64_t)(m & ~((uint64_t)AF_AIDMAP << 32));
+        bool found = ((m >> 32) & AF_AIDMAP) != 0;
         if (!found)
-          for (uint32_t j = 0; j < hw_act; j++)
-            if (act[j].schedule_id != DEAD_KEY && act[j].activity_id == aid && (act[j].flags & AI_IN_AID_MAP)) {
-              act[j].flags &= ~AI_IN_AID_MAP;
+          for (uint32_t j = 0; j < hw_act; j++) {
+            if (A(j, AP_SID) == DEAD_KEY) continue;
+            const uint64_t mj = (uint64_t)A(j, AP_META);
+            if ((uint32_t)mj == aid && ((mj >> 32) & AF_AIDMAP)) {
+              A(j, AP_META) = (int64_t)(mj & ~((uint64_t)AF_AIDMAP << 32));
               found = true;
             }
+          }
         if (!found) {
           FAIL(CDR_E_ACTIVITY_ID_NOT_FOUND);
           break;
         }
-        activity_timer_pick(act, hw_act);
+        act_pick(A, hw_act);
         break;
       }
       case CDR_EV_AT_CANCEL_REQUESTED: {  // :307-310 -> :2264-2285
         const uint32_t aid = (uint32_t)e.key;
         int slot = -1;
-        for (uint32_t j = 0; j < hw_act; j++)
-          if (act[j].schedule_id != DEAD_KEY && act[j].activity_id == aid && (act[j].flags & AI_IN_AID_MAP))
-            slot = (int)j;
+        for (uint32_t j = 0; j < hw_act; j++) {
+          if (A(j, AP_SID) == DEAD_KEY) continue;
+          const uint64_t mj = (uint64_t)A(j, AP_META);
+          if ((uint32_t)mj == aid && ((mj >> 32) & AF_AIDMAP)) slot = (int)j;
+        }
         if (slot < 0) {
           FAIL(CDR_E_MISSING_ACTIVITY_INFO);
           break;
         }
-        act[slot].version = e.ver;
-        act[slot].flags |= CDR_AI_CANCEL_REQUESTED;
-        act[slot].cancel_request_id = e.id;
+        const uint32_t j = (uint32_t)slot;
+        A(j, AP_VER) = e.ver;
+        A(j, AP_META) = (int64_t)((uint64_t)A(j, AP_META) | ((uint64_t)AF_CANCEL << 32));
+        A(j, AP_CANCEL_ID) = e.id;
         break;
       }
       case CDR_EV_TIMER_STARTED: {  // :324-332 -> :2877-2900
         const uint32_t tid = (uint32_t)e.key;
         int slot = -1, free_slot = -1;
         for (uint32_t j = 0; j < hw_tim; j++) {
-          if (tim[j].started_id == DEAD_KEY) {
+          if (T(j, TP_SID) == DEAD_KEY) {
             if (free_slot < 0) free_slot = (int)j;
-          } else if (tim[j].timer_id == tid) {
+          } else if ((uint32_t)T(j, TP_TID_TASK) == tid) {
             slot = (int)j;
           }
         }
@@ -678,22 +710,20 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
           }
           slot = (int)hw_tim++;
         }
-        cdr_timer_info& t = tim[slot];
-        t.version = e.ver;
-        t.started_id = e.id;
-        t.expiry_time = e.ts + e.aux * NS_PER_S;
-        t.task_id = CDR_TIMER_TASK_STATUS_NONE;
-        t.timer_id = tid;
-        t._pad = 0;
-        user_timer_pick(tim, hw_tim);
+        const uint32_t j = (uint32_t)slot;
+        T(j, TP_SID) = e.id;
+        T(j, TP_TID_TASK) = (int64_t)tid;  // TaskID = TimerTaskStatusNone
+        T(j, TP_EXPIRY) = e.ts + e.aux * NS_PER_S;
+        T(j, TP_VER) = e.ver;
+        tim_pick(T, hw_tim);
         break;
       }
       case CDR_EV_TIMER_FIRED:       // :334-341
       case CDR_EV_TIMER_CANCELED: {  // :343-350
         const uint32_t tid = (uint32_t)e.key;
         for (uint32_t j = 0; j < hw_tim; j++)
-          if (tim[j].started_id != DEAD_KEY && tim[j].timer_id == tid) tim[j].started_id = DEAD_KEY;
-        user_timer_pick(tim, hw_tim);
+          if (T(j, TP_SID) != DEAD_KEY && (uint32_t)T(j, TP_TID_TASK) == tid) T(j, TP_SID) = DEAD_KEY;
+        tim_pick(T, hw_tim);
         break;
       }
       case CDR_EV_CHILD_INITIATED: {  // :355-371 -> :3256-3280
@@ -903,14 +933,67 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
   // table high-water marks; k_tables compacts them to live counts (a failed
   // workflow reports no state)
   if (err != CDR_OK) hw_act = hw_tim = hw_chi = hw_can = hw_sig = n_vh = n_rp = n_sa = 0;
-  r.n_activity = hw_act;
-  r.n_timer = hw_tim;
+  r.n_activity = 0;  // set by the emission below
+  r.n_timer = 0;
   r.n_child = hw_chi;
   r.n_cancel = hw_can;
   r.n_signal = hw_sig;
   r.n_vh = n_vh;
   r.n_reset_points = n_rp;
   r.n_search_attr = n_sa;
+  if (err == CDR_OK) {
+    // emit the live working slots as persisted rows (k_tables orders them by key)
+    uint32_t n = 0;
+    for (uint32_t j = 0; j < hw_act; j++) {
+      const int64_t sid = A(j, AP_SID);
+      if (sid == DEAD_KEY) continue;
+      const cdr_attr_at_scheduled* a = reinterpret_cast<const cdr_attr_at_scheduled*>(B.ev.arena + (uint64_t)A(j, AP_AREC));
+      const uint64_t m = (uint64_t)A(j, AP_META), tts = (uint64_t)A(j, AP_TTS);
+      const uint32_t fl = (uint32_t)(m >> 32);
+      const bool retry = (a->flags & CDR_AF_HAS_RETRY) != 0;
+      cdr_activity_info& o = act[n++];
+      o.version = A(j, AP_VER);
+      o.schedule_id = sid;
+      o.scheduled_event_batch_id = A(j, AP_BATCH);
+      o.scheduled_time = A(j, AP_SCHED_TIME);
+      o.started_id = A(j, AP_STARTED_ID);
+      o.started_time = A(j, AP_STARTED_TIME);
+      o.last_heartbeat_time = o.started_time;
+      o.expiration_time = A(j, AP_EXP);
+      o.cancel_request_id = A(j, AP_CANCEL_ID);
+      o.activity_id = (uint32_t)m;
+      o.request_id = (uint32_t)(tts >> 32);
+      o.task_list = a->task_list;
+      o.nonretriable = retry ? a->nonretriable : 0u;
+      o.s2s = a->s2s_s;
+      o.s2c = a->s2c_s;
+      o.stc = a->stc_s;
+      o.hb = a->hb_s;
+      o.timer_task_status = (int32_t)(uint32_t)tts;
+      o.attempt = 0;
+      o.initial_interval = retry ? a->retry_initial_s : 0;
+      o.maximum_interval = retry ? a->retry_max_interval_s : 0;
+      o.maximum_attempts = retry ? a->retry_max_attempts : 0;
+      o.flags = (retry ? CDR_AI_HAS_RETRY : 0u) | ((fl & AF_CANCEL) ? CDR_AI_CANCEL_REQUESTED : 0u) |
+                ((fl & AF_STARTED) ? CDR_AI_STARTED_TIME_SET : 0u);
+      o.backoff_coefficient = retry ? a->backoff_coefficient : 0.0;
+    }
+    r.n_activity = n;
+    n = 0;
+    for (uint32_t j = 0; j < hw_tim; j++) {
+      const int64_t sid = T(j, TP_SID);
+      if (sid == DEAD_KEY) continue;
+      const uint64_t tt = (uint64_t)T(j, TP_TID_TASK);
+      cdr_timer_info& o = tim[n++];
+      o.version = T(j, TP_VER);
+      o.started_id = sid;
+      o.expiry_time = T(j, TP_EXPIRY);
+      o.task_id = (int64_t)(tt >> 32);
+      o.timer_id = (uint32_t)tt;
+      o._pad = 0;
+    }
+    r.n_timer = n;
+  }
   O.result[w] = r;
   if (err != CDR_OK) return;
   if (n_vh) vh[n_vh - 1] = cdr_vh_item{vh_last_id, vh_last_ver};

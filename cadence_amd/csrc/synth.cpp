@@ -852,6 +852,12 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
                            const_cast<uint64_t*>(o->slice_row0), &ns, &rows);
   if (rc) return rc;
   if (ns != o->n_slices || rows != o->n_rows) return CDR_API_EINVAL;
+  if (o->slice_scratch_off && o->slice_act_slots && o->slice_tim_slots) {
+    uint64_t words = 0;
+    rc = cdr_plan_scratch(caps, o->lane_wf, ns, const_cast<uint64_t*>(o->slice_scratch_off),
+                          const_cast<uint32_t*>(o->slice_act_slots), const_cast<uint32_t*>(o->slice_tim_slots), &words);
+    if (rc) return rc;
+  }
   // entry -> (slice, lane)
   std::vector<uint32_t> where(ent);
   for (uint32_t i = 0; i < ns * (uint32_t)CDR_SLICE_WIDTH; i++)

@@ -64,7 +64,15 @@ typedef struct cdr_slices {
   const uint32_t* h;  /* string handle operand (type-dependent) */
   const int32_t* n;   /* small integer operand (type-dependent) */
   const uint64_t* arena; /* WorkflowExecutionStarted / ActivityTaskScheduled attribute records */
+  /* working-state scratch of each slice (cdr_plan_scratch): pending activities and
+   * user timers are kept lane-interleaved ("plane j*P+p, lane L") while they are live */
+  const uint64_t* slice_scratch_off; /* [n_slices] 8-byte-word offset into the scratch buffer */
+  const uint32_t* slice_act_slots;   /* [n_slices] activity working slots per lane */
+  const uint32_t* slice_tim_slots;   /* [n_slices] user-timer working slots per lane */
 } cdr_slices;
+
+#define CDR_ACT_PLANES 15 /* words per activity working slot (replay.hip) */
+#define CDR_TIM_PLANES 4  /* words per user-timer working slot */
 
 #define CDR_SEF_BATCH_FIRST (1u << 8)
 #define CDR_SEF_DOMAIN_MISSING (1u << 9)
@@ -72,6 +80,7 @@ typedef struct cdr_slices {
 /* everything the device needs for one replay launch (all pointers device memory) */
 typedef struct cdr_dev_batch {
   cdr_slices ev;
+  uint64_t* scratch; /* working-state buffer, cdr_plan_scratch words (device) */
   const cdr_wf_desc* wfs; /* [n_wfs] */
   const cdr_wf_caps* caps; /* [n_wfs] */
   const cdr_kv* kvs;
@@ -96,6 +105,12 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals);
  * Call with lane_wf == NULL to query sizes only. */
 int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, uint32_t* slice_len,
                     uint64_t* slice_row0, uint32_t* n_slices, uint64_t* n_rows);
+
+/* Working-state scratch layout: per slice, slots = max over its lanes of the live
+ * bounds in caps; returns the total words via *total_words.  Outputs sized
+ * [n_slices]; pass NULL outputs to query the total only. */
+int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n_slices, uint64_t* scratch_off,
+                     uint32_t* act_slots, uint32_t* tim_slots, uint64_t* total_words);
 
 /* Arena words needed by the batch's attribute records. */
 uint64_t cdr_plan_arena_words(const cdr_batch* b);

@@ -468,6 +468,9 @@ typedef struct cdr_wf_result {
 typedef struct cdr_wf_caps {
   uint64_t act_off, timer_off, child_off, cancel_off, signal_off, vh_off, rp_off, sa_off;
   uint32_t act_cap, timer_cap, child_cap, cancel_cap, signal_cap, vh_cap, rp_cap, sa_cap;
+  /* upper bounds of the live set (working slots): activities = max over prefixes of
+   * (#scheduled - #closed), timers = #TimerStarted */
+  uint32_t act_live, timer_live;
 } cdr_wf_caps;
 
 typedef struct cdr_totals {
