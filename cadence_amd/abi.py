@@ -237,7 +237,7 @@ EXPORTS = {
 }
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libcdr.so")
+LIB_PATH = os.environ.get("CDR_LIB") or os.path.join(PKG_DIR, "libcdr.so")
 _lib = None
 
 
@@ -245,19 +245,24 @@ class NativeLibraryMissing(RuntimeError):
     pass
 
 
+def load(path: str):
+    """Load a libcdr build and declare its C ABI (``lib()`` caches the default one)."""
+    if not os.path.exists(path):
+        raise NativeLibraryMissing(
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(path)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
 def lib():
     """Load the in-tree libcdr.so (fails loudly: there is no fallback path)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise NativeLibraryMissing(
-                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
-        L = C.CDLL(LIB_PATH)
-        for name, (res, args) in EXPORTS.items():
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
-        _lib = L
+        _lib = load(LIB_PATH)
     return _lib
 
 

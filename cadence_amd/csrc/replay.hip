@@ -30,6 +30,12 @@
 
 #include "cdr/cdr.h"
 
+#ifndef CDR_PF
+#define CDR_PF 1
+#endif
+#ifndef CDR_MINW
+#define CDR_MINW 1
+#endif
 #define DEAD_KEY ((int64_t)0x8000000000000000ll)
 #define AI_IN_AID_MAP 0x80000000u /* kernel-private: this row holds byActivityID[aid] */
 #define NS_PER_S 1000000000ll
@@ -162,11 +168,22 @@ static_assert(TP_VER + 1 == CDR_TIM_PLANES, "timer planes");
 #define AF_CANCEL 0x4u
 #define T_NONE ((int64_t)0x7FFFFFFFFFFFFFFFll)
 
+// The first CDR_LDS_SLOTS working slots of every lane live in LDS (the common live
+// set: a workflow rarely has more than one or two activities / timers in flight);
+// further slots spill to the lane-interleaved global scratch.  Accesses go through a
+// generic (flat) pointer so one code path serves both tiers.
+#ifndef CDR_LDS_SLOTS
+#define CDR_LDS_SLOTS 2
+#endif
+#define LDS_WORDS (CDR_LDS_SLOTS ? (CDR_LDS_SLOTS * (CDR_ACT_PLANES + CDR_TIM_PLANES)) * 256 : 1)
 struct Lanes {  // slot/plane addressing of one lane's working state
-  uint64_t* base;
+  uint64_t* base;  // global scratch: plane p of slot j at ((j*P)+p)*64
+  uint64_t* lds;   // LDS: plane p of slot j at ((j*P)+p)*256 (256 threads per block)
   uint32_t P;
   __device__ __forceinline__ int64_t& operator()(uint32_t slot, uint32_t plane) const {
-    return *reinterpret_cast<int64_t*>(base + ((uint64_t)slot * P + plane) * CDR_SLICE_WIDTH);
+    uint64_t* q = slot < CDR_LDS_SLOTS ? lds + ((uint64_t)slot * P + plane) * 256
+                                       : base + ((uint64_t)slot * P + plane) * CDR_SLICE_WIDTH;
+    return *reinterpret_cast<int64_t*>(q);
   }
 };
 
@@ -255,7 +272,7 @@ __device__ __forceinline__ Ev load_ev(const cdr_slices& S, uint64_t i) {
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
+__global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_out O) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t s = g >> 6;
   if (s >= B.ev.n_slices) return;
@@ -285,8 +302,10 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
   // working slots of pending activities / user timers (lane-interleaved scratch)
   const uint32_t act_cap = B.ev.slice_act_slots[s], tim_cap = B.ev.slice_tim_slots[s];
   uint64_t* const lane_scratch = B.scratch + B.ev.slice_scratch_off[s] + (g & 63);
-  const Lanes A{lane_scratch, CDR_ACT_PLANES};
-  const Lanes T{lane_scratch + (uint64_t)act_cap * CDR_ACT_PLANES * CDR_SLICE_WIDTH, CDR_TIM_PLANES};
+  __shared__ uint64_t lds_ws[LDS_WORDS];
+  const Lanes A{lane_scratch, lds_ws + threadIdx.x, CDR_ACT_PLANES};
+  const Lanes T{lane_scratch + (uint64_t)act_cap * CDR_ACT_PLANES * CDR_SLICE_WIDTH,
+                lds_ws + CDR_LDS_SLOTS * CDR_ACT_PLANES * 256 + threadIdx.x, CDR_TIM_PLANES};
   uint32_t cks_ok = 0;  // a binary checksum known to be in AutoResetPoints
 
   // ---- ExecutionInfo fields that later events change (registers); the fields only
@@ -325,10 +344,31 @@ __global__ __launch_bounds__(256) void k_replay(cdr_dev_batch B, cdr_out O) {
     stop_at_call_end = true; \
   } while (0)
 
+  // software pipeline of the column loads (CDR_PF: 1 = next event issued at the top
+  // of the iteration, 2 = at the bottom, 3 = two events ahead)
+#if CDR_PF == 3
   Ev nxt = len ? load_ev(B.ev, base) : Ev{};
-  for (uint32_t k = 0; k < len; k++) {
+  Ev nxt2 = len > 1 ? load_ev(B.ev, base + CDR_SLICE_WIDTH) : Ev{};
+#else
+  Ev nxt = len ? load_ev(B.ev, base) : Ev{};
+#endif
+  for (uint32_t k = 0; k < len;
+#if CDR_PF == 2
+       nxt = (k + 1 < len) ? load_ev(B.ev, base + (uint64_t)(k + 1) * CDR_SLICE_WIDTH) : nxt, k++
+#else
+       k++
+#endif
+  ) {
+#if CDR_PF == 3
     const Ev e = nxt;
-    if (k + 1 < len) nxt = load_ev(B.ev, base + (uint64_t)(k + 1) * CDR_SLICE_WIDTH);  // software pipeline
+    nxt = nxt2;
+    if (k + 2 < len) nxt2 = load_ev(B.ev, base + (uint64_t)(k + 2) * CDR_SLICE_WIDTH);
+#elif CDR_PF == 2
+    const Ev e = nxt;
+#else
+    const Ev e = nxt;
+    if (k + 1 < len) nxt = load_ev(B.ev, base + (uint64_t)(k + 1) * CDR_SLICE_WIDTH);
+#endif
     const uint32_t type = e.tf & 0xFFu;
     if ((e.tf & CDR_SEF_BATCH_FIRST) || k == 0) {
       if (k > 0) {

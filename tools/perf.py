@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""A/B timing of libcdr kernel variants on one device-resident batch (interleaved
+rounds in one process, cdr_timing ring = HIP events on the launch stream).
+usage: python tools/perf.py [--config 2] [--wfs 1000000] [--rounds 5] variants/libcdr_a.so ..."""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from cadence_amd import abi  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--wfs", type=int, default=1_000_000)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    import bench
+    torch.cuda.set_device(0)
+    idx = np.arange(args.wfs, dtype=np.uint32)
+    db = bench.DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config)
+    stream = torch.cuda.current_stream().cuda_stream
+    libs = [(p, abi.load(p)) for p in args.libs]
+    ctxs = [L.cdr_create(0) for _, L in libs]
+    times = {p: [] for p, _ in libs}
+    sums = {}
+    for rnd in range(args.rounds):
+        for (p, L), ctx in zip(libs, ctxs):
+            L.cdr_replay_sliced_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(stream))
+            L.cdr_timing_begin(ctx, args.reps)
+            for _ in range(args.reps):
+                L.cdr_replay_sliced_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(stream))
+            ms = (C.c_float * args.reps)()
+            n = C.c_uint32(args.reps)
+            L.cdr_timing_read(ctx, ms, C.byref(n))
+            times[p] += list(ms)[: n.value]
+            if rnd == 0:
+                cs = torch.zeros(1, dtype=torch.int64, device="cuda")
+                L.cdr_checksum_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(cs.data_ptr()),
+                                     C.c_void_p(stream))
+                torch.cuda.synchronize()
+                sums[p] = int(cs.item())
+    base = None
+    for p, _ in libs:
+        t = np.array(times[p])
+        med = float(np.median(t))
+        base = base or med
+        print(json.dumps({"lib": os.path.basename(p), "median_ms": round(med, 4), "min_ms": round(float(t.min()), 4),
+                          "events_per_s": db.n_events / (med / 1e3), "rel": round(med / base, 4),
+                          "checksum": sums[p] & 0xFFFFFFFFFFFFFFFF}), flush=True)
+    if len(set(sums.values())) != 1:
+        print("CHECKSUM MISMATCH between variants", file=sys.stderr)
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
