@@ -146,6 +146,8 @@ class DeviceBatch:
         db.wfs, db.caps = up_ct(self.h_wfs), up_ct(self.h_caps)
         db.kvs, db.rps = up(self.h_kvs), up_ct(self.h_rps)
         db.n_wfs = info.n_entries
+        db.max_act_slots = int(self.h_sc_act.max()) if len(self.h_sc_act) else 0
+        db.max_tim_slots = int(self.h_sc_tim.max()) if len(self.h_sc_tim) else 0
         db.empty_uuid = meta.empty_uuid
         db.cluster = meta.cluster
         db.now_ns = meta.now_ns

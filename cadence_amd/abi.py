@@ -182,7 +182,8 @@ CdrSlices = _S("cdr_slices", [
         "aux", "h", "n", "arena", "slice_scratch_off", "slice_act_slots", "slice_tim_slots")])
 CdrDevBatch = _S("cdr_dev_batch", [
     ("ev", CdrSlices), ("scratch", C.c_void_p), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
-    ("n_wfs", u32), ("empty_uuid", u32), ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64)])
+    ("n_wfs", u32), ("empty_uuid", u32), ("max_act_slots", u32), ("max_tim_slots", u32),
+    ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64)])
 
 # ------------------------------------------------------------------ synth
 CdrSynthParams = _S("cdr_synth_params", [

@@ -253,6 +253,10 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   db.ev.slice_scratch_off = (const uint64_t*)up(sc_off.data(), ns * 8ull);
   db.ev.slice_act_slots = (const uint32_t*)up(sc_act.data(), ns * 4ull);
   db.ev.slice_tim_slots = (const uint32_t*)up(sc_tim.data(), ns * 4ull);
+  for (uint32_t i = 0; i < ns; i++) {
+    db.max_act_slots = sc_act[i] > db.max_act_slots ? sc_act[i] : db.max_act_slots;
+    db.max_tim_slots = sc_tim[i] > db.max_tim_slots ? sc_tim[i] : db.max_tim_slots;
+  }
   db.scratch = (uint64_t*)dz(sc_words * 8);
   db.wfs = (const cdr_wf_desc*)up(b->wfs, (uint64_t)b->n_wfs * sizeof(cdr_wf_desc));
   db.caps = (const cdr_wf_caps*)up(caps, (uint64_t)b->n_wfs * sizeof(cdr_wf_caps));

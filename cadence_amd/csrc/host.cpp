@@ -174,12 +174,18 @@ void pack_lane(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t len, 
       case CDR_EV_DT_TIMED_OUT:
         n = e.a.dt.timeout_type;
         break;
-      case CDR_EV_AT_SCHEDULED:
-        kk = e.a.at_sched.activity_id;
-        ax = (int64_t)apos;
-        std::memcpy(arena + apos, &e.a.at_sched, sizeof(cdr_attr_at_scheduled));
+      case CDR_EV_AT_SCHEDULED: {
+        // the four timeouts travel in the columns (the replay loop never reads the
+        // arena record; only the final emission of a still-pending activity does)
+        const cdr_attr_at_scheduled& a = e.a.at_sched;
+        kk = (int64_t)((uint64_t)a.activity_id | ((uint64_t)(uint32_t)a.stc_s << 32));
+        h = (uint32_t)a.s2c_s;
+        n = a.s2s_s;
+        ax = (int64_t)((apos & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)a.hb_s << 32));
+        std::memcpy(arena + apos, &a, sizeof(cdr_attr_at_scheduled));
         apos += arena_words_for(e.type);
         break;
+      }
       case CDR_EV_AT_STARTED:
         kk = e.a.at.scheduled_event_id;
         h = e.a.at.request_id;
@@ -375,6 +381,7 @@ int cdr_pack_slices(const cdr_batch* b, cdr_slices* o, int threads) {
     arena_base[w + 1] = arena_base[w] + words;
   }
   if (arena_base[b->n_wfs] > o->arena_words) return CDR_API_EINVAL;
+  if (o->arena_words >= (1ull << 32)) return CDR_API_EINVAL;  // u32 arena offsets (cdr.h)
   std::atomic<int> bad{0};
   parallel_for(o->n_slices, threads, [&](uint64_t s) {
     const uint64_t row0 = o->slice_row0[s];

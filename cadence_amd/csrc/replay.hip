@@ -4,19 +4,27 @@
 // 112-611) driving mutableStateBuilder.Replicate*Event, one goroutine per workflow.
 //
 // MI355X design (DESIGN.md has the full argument):
-//   * Input arrives in the sliced layout of cdr.h: 64 workflows of similar length per
-//     slice, event k of all 64 stored contiguously per column.  One wavefront owns one
-//     slice, one lane owns one workflow; at step k the wave loads event k of its 64
-//     workflows with fully coalesced 256-512 B column loads.  A column is only loaded
-//     when some lane's event type needs it, so HBM traffic tracks the algorithmic bytes.
-//   * Per-workflow scalar state (ExecutionInfo, decision FSM, version history head,
+//   * One wavefront = one 64-thread workgroup = one slice of the sliced layout (cdr.h):
+//     64 workflows of similar length, one per lane, walked in lockstep.  Column loads
+//     are buffer loads through per-slice descriptors built once from wave-uniform
+//     values, so each load of a step is one fully coalesced 256/512-B wave access.
+//   * Type-directed loads.  The type column runs two steps ahead of the operand
+//     columns; a column the lane's event type never reads gets an out-of-range buffer
+//     offset, which returns 0 without touching memory.  The load is still issued, so
+//     every step issues a fixed number of vector-memory ops and the compiler's
+//     s_waitcnt vmcnt(N) counts stay exact: the operands of event k are waited for only
+//     when event k is processed, CDR_DEPTH steps after they were issued.
+//   * Per-workflow scalar state (ExecutionInfo, decision FSM, version-history head,
 //     replication state, call bookkeeping) lives in VGPRs for the whole history.
-//   * Pending entities live in the workflow's slot range of the output tables
-//     (capacity planned on the host); a deleted entity frees its slot and the next
-//     creation reuses the lowest free slot, so a steady-state workflow keeps touching
-//     the same few L2-resident lines and only its final rows reach HBM.
-//   * The order-dependent timer picks (timerBuilder.go:171-312) are a min-scan over the
-//     workflow's live slots after each activity/timer event.
+//   * Live activities and user timers, which the order-dependent timer picks
+//     (timerBuilder.go:171-312) scan after every activity/timer event, live in LDS
+//     working slots, lane-interleaved (plane p of slot j of lane L at word
+//     (j*P+p)*64+L: conflict-free ds_read_b64).  Slices whose live sets exceed the LDS
+//     budget replay in a second launch whose slots live in global scratch.  The tiers
+//     are never mixed behind one pointer: a generic pointer compiles to flat_*, whose
+//     out-of-order return forces vmcnt(0) on every use and serialises the prefetch.
+//   * Children / request-cancels / signals write straight into their output slot
+//     ranges (rare, never scanned by a pick).
 //   * Errors: the first error/panic of a workflow stops it (the caller discards the
 //     mutable state); its code and event are reported per workflow.
 //   * Continue-as-new runs are separate lanes; k_finalize stitches their status into
@@ -26,19 +34,32 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "cdr/cdr.h"
 
-#ifndef CDR_PF
-#define CDR_PF 1
+#ifndef CDR_DEPTH
+#define CDR_DEPTH 2 /* events whose operand loads are in flight beyond the one processed */
 #endif
-#ifndef CDR_MINW
-#define CDR_MINW 1
+#ifndef CDR_TYPED
+#define CDR_TYPED 1 /* 1: read only the operand columns the event's type needs */
 #endif
+#ifndef CDR_WPE
+#define CDR_WPE 3 /* waves per SIMD the register allocator must leave room for */
+#endif
+#ifndef CDR_LDS_ACT_MAX
+#define CDR_LDS_ACT_MAX 1 /* activity working slots per lane kept in LDS */
+#endif
+#ifndef CDR_LDS_TIM_MAX
+#define CDR_LDS_TIM_MAX 4 /* user-timer working slots per lane kept in LDS */
+#endif
+
+#define GAS __attribute__((address_space(1)))
 #define DEAD_KEY ((int64_t)0x8000000000000000ll)
-#define AI_IN_AID_MAP 0x80000000u /* kernel-private: this row holds byActivityID[aid] */
 #define NS_PER_S 1000000000ll
+#define T_NONE ((int64_t)0x7FFFFFFFFFFFFFFFll)
+#define OOB 0x80000000u /* buffer offset beyond every slice: load returns 0, no memory access */
 
 namespace {
 
@@ -66,6 +87,7 @@ __device__ __forceinline__ bool transition_ok(int cur, int cur_close, int st, in
   return false;
 }
 
+// ClusterNameForFailoverVersion (common/cluster/metadata.go:187-203): -1 = no owner
 __device__ __forceinline__ int cluster_for_version(const cdr_cluster_meta& m, int64_t v) {
   if (v == CDR_EMPTY_VERSION) return m.current_cluster;
   int64_t init = v % m.failover_version_increment;
@@ -123,88 +145,205 @@ struct SignalKey {
   __device__ int64_t key(const cdr_signal_info& r) const { return r.initiated_id; }
 };
 
+// whole-record copies to / from global memory (C++ copy operators do not cross
+// address spaces); every record is a multiple of 8 bytes
+template <class T>
+__device__ __forceinline__ void gput(GAS T* p, const T& v) {
+  static_assert(sizeof(T) % 8 == 0, "record size");
+  const uint64_t* s = reinterpret_cast<const uint64_t*>(&v);
+  GAS uint64_t* d = (GAS uint64_t*)p;
+#pragma unroll
+  for (uint32_t i = 0; i < sizeof(T) / 8; i++) d[i] = s[i];
+}
+template <class T>
+__device__ __forceinline__ T gget(const GAS T* p) {
+  static_assert(sizeof(T) % 8 == 0, "record size");
+  T v;
+  uint64_t* d = reinterpret_cast<uint64_t*>(&v);
+  const GAS uint64_t* s = (const GAS uint64_t*)p;
+#pragma unroll
+  for (uint32_t i = 0; i < sizeof(T) / 8; i++) d[i] = s[i];
+  return v;
+}
+
+// Opaque copy of a wave-uniform base pointer: loads through it cannot be hoisted out
+// of the replay loop, so per-workflow descriptors and table bases are re-read in the
+// (rare) event types that need them instead of occupying VGPRs for the whole history.
+template <class T>
+__device__ __forceinline__ GAS T* late(T* base) {
+  GAS T* p = (GAS T*)base;
+  asm volatile("" : "+s"(p));
+  return p;
+}
+template <class T>
+__device__ __forceinline__ const GAS T* late(const T* base) {
+  const GAS T* p = (const GAS T*)base;
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 template <class Row>
-__device__ __forceinline__ int find_initiated(const Row* rows, uint32_t hw, int64_t id) {
+__device__ __forceinline__ int find_initiated(const GAS Row* rows, uint32_t hw, int64_t id) {
   for (uint32_t j = 0; j < hw; j++)
     if (rows[j].initiated_id == id) return (int)j;
   return -1;
 }
 template <class Row>
-__device__ __forceinline__ int alloc_initiated(const Row* rows, uint32_t& hw, uint32_t cap) {
+__device__ __forceinline__ int alloc_initiated(const GAS Row* rows, uint32_t& hw, uint32_t cap) {
   for (uint32_t j = 0; j < hw; j++)
     if (rows[j].initiated_id == DEAD_KEY) return (int)j;
   if (hw < cap) return (int)(hw++);
   return -1;
 }
 
-}  // namespace
+// ---------------------------------------------------------------- event columns
+// Which operand columns each event type reads (bit = cdr_event_type).  Every type
+// reads type_flags, event_id and version (prelude, stateBuilder.go:134-155).
+#define TB(t) (1ull << (t))
+constexpr uint64_t NEED_TS = TB(CDR_EV_WF_STARTED) | TB(CDR_EV_DT_SCHEDULED) | TB(CDR_EV_DT_STARTED) |
+                             TB(CDR_EV_AT_SCHEDULED) | TB(CDR_EV_AT_STARTED) | TB(CDR_EV_TIMER_STARTED);
+constexpr uint64_t NEED_KEY =
+    TB(CDR_EV_DT_STARTED) | TB(CDR_EV_AT_SCHEDULED) | TB(CDR_EV_AT_STARTED) | TB(CDR_EV_AT_COMPLETED) |
+    TB(CDR_EV_AT_FAILED) | TB(CDR_EV_AT_TIMED_OUT) | TB(CDR_EV_AT_CANCELED) | TB(CDR_EV_AT_CANCEL_REQUESTED) |
+    TB(CDR_EV_TIMER_STARTED) | TB(CDR_EV_TIMER_FIRED) | TB(CDR_EV_TIMER_CANCELED) | TB(CDR_EV_CHILD_INITIATED) |
+    TB(CDR_EV_CHILD_STARTED) | TB(CDR_EV_CHILD_START_FAILED) | TB(CDR_EV_CHILD_COMPLETED) |
+    TB(CDR_EV_CHILD_FAILED) | TB(CDR_EV_CHILD_CANCELED) | TB(CDR_EV_CHILD_TIMED_OUT) |
+    TB(CDR_EV_CHILD_TERMINATED) | TB(CDR_EV_RCE_FAILED) | TB(CDR_EV_EXT_CANCEL_REQUESTED) | TB(CDR_EV_SE_FAILED) |
+    TB(CDR_EV_EXT_SIGNALED);
+constexpr uint64_t NEED_AUX = TB(CDR_EV_WF_STARTED) | TB(CDR_EV_DT_SCHEDULED) | TB(CDR_EV_DT_COMPLETED) |
+                              TB(CDR_EV_AT_SCHEDULED) | TB(CDR_EV_TIMER_STARTED) | TB(CDR_EV_CHILD_INITIATED) |
+                              TB(CDR_EV_SE_INITIATED) | TB(CDR_EV_UPSERT_SA);
+constexpr uint64_t NEED_H = TB(CDR_EV_DT_STARTED) | TB(CDR_EV_DT_COMPLETED) | TB(CDR_EV_AT_SCHEDULED) |
+                            TB(CDR_EV_AT_STARTED) | TB(CDR_EV_CHILD_INITIATED) | TB(CDR_EV_CHILD_STARTED) |
+                            TB(CDR_EV_SE_INITIATED) | TB(CDR_EV_UPSERT_SA);
+constexpr uint64_t NEED_N =
+    TB(CDR_EV_DT_SCHEDULED) | TB(CDR_EV_DT_TIMED_OUT) | TB(CDR_EV_AT_SCHEDULED) | TB(CDR_EV_CHILD_INITIATED);
+#undef TB
 
-// ---- lane-interleaved working state (cdr.h: slice_scratch_off)
-// activity working slot planes (8-byte words); plane p of slot j of lane L lives at
-// word (j*CDR_ACT_PLANES + p)*64 + L of the slice's scratch, so a wavefront that
-// touches slot j of its 64 workflows issues one coalesced 512-B access.
-enum : uint32_t {
-  AP_SID = 0,       // scheduleID (DEAD_KEY = free slot)
-  AP_META = 1,      // activityID handle | flags << 32
-  AP_TTS = 2,       // TimerTaskStatus | RequestID handle << 32
-  AP_VER = 3,
-  AP_TS2C = 4,      // ScheduleToClose candidate: min(sched + s2c, ExpirationTime)
-  AP_TALT = 5,      // ScheduleToStart candidate before start, StartToClose after
-  AP_THB = 6,       // Heartbeat candidate (started and hb > 0) else INT64_MAX
-  AP_STARTED_ID = 7,
-  AP_STARTED_TIME = 8,
-  AP_CANCEL_ID = 9,
-  AP_AREC = 10,     // arena word offset of the ActivityTaskScheduled record
-  AP_SCHED_TIME = 11,
-  AP_BATCH = 12,
-  AP_EXP = 13,
-  AP_STC_HB = 14,   // StartToClose | HeartbeatTimeout << 32 (seconds)
+__device__ __forceinline__ bool needs(uint64_t mask, uint32_t t) { return t < 64 && ((mask >> t) & 1ull); }
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+struct Cols {  // buffer descriptors of one slice's columns
+  rsrc_t tf, id, ver, ts, key, aux, h, n;
 };
-static_assert(AP_STC_HB + 1 == CDR_ACT_PLANES, "activity planes");
+__device__ __forceinline__ rsrc_t slice_rsrc(const void* col, uint64_t row0, uint32_t rows, uint32_t esz) {
+  const char* p = (const char*)col + row0 * CDR_SLICE_WIDTH * esz;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(rows * CDR_SLICE_WIDTH * esz), 0x00020000);
+}
+__device__ __forceinline__ int64_t bld64(rsrc_t r, uint32_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return (int64_t)(((uint64_t)v[1] << 32) | (uint64_t)v[0]);
+}
+__device__ __forceinline__ uint32_t bld32(rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+
+// one event's operands (cdr.h "operand columns per type"); task_id is read once,
+// for the last event, after the loop (only the last applied event's value survives)
+struct Ev {
+  uint32_t tf, h;
+  int32_t n;
+  int64_t id, ver, ts, key, aux;
+};
+
+__device__ __forceinline__ uint32_t load_tf(const Cols& C, uint32_t k, uint32_t len, uint32_t lane) {
+  return bld32(C.tf, k < len ? (k * CDR_SLICE_WIDTH + lane) * 4u : OOB);
+}
+__device__ __forceinline__ Ev load_ops(const Cols& C, uint32_t k, uint32_t len, uint32_t lane, uint32_t tf) {
+  const bool in = k < len;
+  const uint32_t t = tf & 0xFFu;
+  const uint32_t o4 = in ? (k * CDR_SLICE_WIDTH + lane) * 4u : OOB;
+  const uint32_t o8 = in ? (k * CDR_SLICE_WIDTH + lane) * 8u : OOB;
+  Ev e;
+  e.tf = tf;
+  e.id = bld64(C.id, o8);
+  e.ver = bld64(C.ver, o8);
+#if CDR_TYPED
+  e.ts = bld64(C.ts, needs(NEED_TS, t) ? o8 : OOB);
+  e.key = bld64(C.key, needs(NEED_KEY, t) ? o8 : OOB);
+  e.aux = bld64(C.aux, needs(NEED_AUX, t) ? o8 : OOB);
+  e.h = bld32(C.h, needs(NEED_H, t) ? o4 : OOB);
+  e.n = (int32_t)bld32(C.n, needs(NEED_N, t) ? o4 : OOB);
+#else
+  (void)t;
+  e.ts = bld64(C.ts, o8);
+  e.key = bld64(C.key, o8);
+  e.aux = bld64(C.aux, o8);
+  e.h = bld32(C.h, o4);
+  e.n = (int32_t)bld32(C.n, o4);
+#endif
+  return e;
+}
+
+// ---------------------------------------------------------------- working slots
+// activity working-slot planes (8-byte words)
+enum : uint32_t {
+  AP_SID = 0,          // scheduleID (DEAD_KEY = free slot)
+  AP_TS2C = 1,         // ScheduleToClose candidate: sched + s2c (ExpirationTime is never earlier)
+  AP_TALT = 2,         // ScheduleToStart candidate before start, StartToClose after
+  AP_THB = 3,          // Heartbeat candidate (started and hb > 0) else T_NONE
+  AP_META = 4,         // activityID handle | AF_* << 32 | TimerTaskStatus << 40
+  AP_VER = 5,
+  AP_STARTED_ID = 6,
+  AP_STARTED_TIME = 7,
+  AP_CANCEL_ID = 8,
+  AP_ROWS = 9,         // row of the ActivityTaskScheduled event | row of its call's first event << 32
+  AP_STC_HB = 10,      // StartToClose | HeartbeatTimeout << 32 (seconds)
+  AP_REQ = 11,         // RequestID handle
+};
+static_assert(AP_REQ + 1 == CDR_ACT_PLANES, "activity planes");
 enum : uint32_t { TP_SID = 0, TP_TID_TASK = 1, TP_EXPIRY = 2, TP_VER = 3 };
 static_assert(TP_VER + 1 == CDR_TIM_PLANES, "timer planes");
-#define AF_AIDMAP 0x1u    /* this slot holds byActivityID[aid] */
-#define AF_STARTED 0x2u
-#define AF_CANCEL 0x4u
-#define T_NONE ((int64_t)0x7FFFFFFFFFFFFFFFll)
+#define AF_AIDMAP 0x1ull /* this slot holds byActivityID[aid] */
+#define AF_STARTED 0x2ull
+#define AF_CANCEL 0x4ull
+#define META_FLAG(f) ((f) << 32)
+#define META_TTS_SHIFT 40
 
-// The first CDR_LDS_SLOTS working slots of every lane live in LDS (the common live
-// set: a workflow rarely has more than one or two activities / timers in flight);
-// further slots spill to the lane-interleaved global scratch.  Accesses go through a
-// generic (flat) pointer so one code path serves both tiers.
-#ifndef CDR_LDS_SLOTS
-#define CDR_LDS_SLOTS 2
-#endif
-#define LDS_WORDS (CDR_LDS_SLOTS ? (CDR_LDS_SLOTS * (CDR_ACT_PLANES + CDR_TIM_PLANES)) * 256 : 1)
-struct Lanes {  // slot/plane addressing of one lane's working state
-  uint64_t* base;  // global scratch: plane p of slot j at ((j*P)+p)*64
-  uint64_t* lds;   // LDS: plane p of slot j at ((j*P)+p)*256 (256 threads per block)
-  uint32_t P;
-  __device__ __forceinline__ int64_t& operator()(uint32_t slot, uint32_t plane) const {
-    uint64_t* q = slot < CDR_LDS_SLOTS ? lds + ((uint64_t)slot * P + plane) * 256
-                                       : base + ((uint64_t)slot * P + plane) * CDR_SLICE_WIDTH;
-    return *reinterpret_cast<int64_t*>(q);
+extern __shared__ uint64_t cdr_lds[];
+
+// LDS tier: this lane's plane 0 of slot 0 at word l
+template <uint32_t P>
+struct LdsSlots {
+  uint32_t l;
+  __device__ __forceinline__ int64_t ld(uint32_t j, uint32_t p) const {
+    return (int64_t)cdr_lds[l + (j * P + p) * CDR_SLICE_WIDTH];
+  }
+  __device__ __forceinline__ void st(uint32_t j, uint32_t p, int64_t v) const {
+    cdr_lds[l + (j * P + p) * CDR_SLICE_WIDTH] = (uint64_t)v;
+  }
+};
+// global tier: the slice's lane-interleaved scratch (same plane layout)
+template <uint32_t P>
+struct GlbSlots {
+  GAS uint64_t* g;
+  __device__ __forceinline__ int64_t ld(uint32_t j, uint32_t p) const {
+    return (int64_t)g[((uint64_t)j * P + p) * CDR_SLICE_WIDTH];
+  }
+  __device__ __forceinline__ void st(uint32_t j, uint32_t p, int64_t v) const {
+    g[((uint64_t)j * P + p) * CDR_SLICE_WIDTH] = (uint64_t)v;
   }
 };
 
 // activity timer pick (timerBuilder.go:211-312) over the live working slots
-__device__ __forceinline__ void act_pick(const Lanes& A, uint32_t hw) {
+template <class A>
+__device__ __forceinline__ void act_pick(const A& S, uint32_t hw) {
   int best = -1;
   int64_t bt = 0, bs = 0;
   int bo = 0;
   uint32_t bbit = 0;
   for (uint32_t j = 0; j < hw; j++) {
-    const int64_t sid = A(j, AP_SID);
+    const int64_t sid = S.ld(j, AP_SID);
     if (sid == DEAD_KEY) continue;
-    const uint32_t fl = (uint32_t)((uint64_t)A(j, AP_META) >> 32);
-    int64_t t = A(j, AP_TS2C);
+    const uint64_t meta = (uint64_t)S.ld(j, AP_META);
+    int64_t t = S.ld(j, AP_TS2C);
     int o = 0;
     uint32_t bit = CDR_TTS_SCHEDULE_TO_CLOSE;
-    const int64_t ta = A(j, AP_TALT), th = A(j, AP_THB);
+    const int64_t ta = S.ld(j, AP_TALT), th = S.ld(j, AP_THB);
     if (ta < t) {  // append order breaks ties: S2C, then STC/S2S, then HB
       t = ta;
       o = 1;
-      bit = (fl & AF_STARTED) ? CDR_TTS_START_TO_CLOSE : CDR_TTS_SCHEDULE_TO_START;
+      bit = (meta & META_FLAG(AF_STARTED)) ? CDR_TTS_START_TO_CLOSE : CDR_TTS_SCHEDULE_TO_START;
     }
     if (th < t) {
       t = th;
@@ -220,19 +359,21 @@ __device__ __forceinline__ void act_pick(const Lanes& A, uint32_t hw) {
     }
   }
   if (best >= 0) {
-    const uint64_t v = (uint64_t)A((uint32_t)best, AP_TTS);
-    if (!((uint32_t)v & bbit)) A((uint32_t)best, AP_TTS) = (int64_t)(v | bbit);
+    const uint64_t m = (uint64_t)S.ld((uint32_t)best, AP_META);
+    const uint64_t b = (uint64_t)bbit << META_TTS_SHIFT;
+    if (!(m & b)) S.st((uint32_t)best, AP_META, (int64_t)(m | b));
   }
 }
 
 // user timer pick (timerBuilder.go:171-184,233-247): head by (ExpiryTime, StartedID)
-__device__ __forceinline__ void tim_pick(const Lanes& T, uint32_t hw) {
+template <class T>
+__device__ __forceinline__ void tim_pick(const T& S, uint32_t hw) {
   int best = -1;
   int64_t be = 0, bs = 0;
   for (uint32_t j = 0; j < hw; j++) {
-    const int64_t sid = T(j, TP_SID);
+    const int64_t sid = S.ld(j, TP_SID);
     if (sid == DEAD_KEY) continue;
-    const int64_t ex = T(j, TP_EXPIRY);
+    const int64_t ex = S.ld(j, TP_EXPIRY);
     if (best < 0 || ex < be || (ex == be && sid < bs)) {
       best = (int)j;
       be = ex;
@@ -240,78 +381,84 @@ __device__ __forceinline__ void tim_pick(const Lanes& T, uint32_t hw) {
     }
   }
   if (best >= 0) {
-    const uint64_t v = (uint64_t)T((uint32_t)best, TP_TID_TASK);
+    const uint64_t v = (uint64_t)S.ld((uint32_t)best, TP_TID_TASK);
     if ((v >> 32) != CDR_TIMER_TASK_STATUS_CREATED)
-      T((uint32_t)best, TP_TID_TASK) = (int64_t)((v & 0xFFFFFFFFull) | ((uint64_t)CDR_TIMER_TASK_STATUS_CREATED << 32));
+      S.st((uint32_t)best, TP_TID_TASK,
+           (int64_t)((v & 0xFFFFFFFFull) | ((uint64_t)CDR_TIMER_TASK_STATUS_CREATED << 32)));
   }
-}
-
-// ============================================================== replay kernel
-namespace {
-
-// one event's columns (cdr.h "sliced layout")
-struct Ev {
-  uint32_t tf, h;
-  int32_t n;
-  int64_t id, ver, ts, task, key, aux;
-};
-
-__device__ __forceinline__ Ev load_ev(const cdr_slices& S, uint64_t i) {
-  Ev e;
-  e.tf = S.type_flags[i];
-  e.id = S.event_id[i];
-  e.ver = S.version[i];
-  e.ts = S.timestamp[i];
-  e.task = S.task_id[i];
-  e.key = S.key[i];
-  e.aux = S.aux[i];
-  e.h = S.h[i];
-  e.n = S.n[i];
-  return e;
 }
 
 }  // namespace
 
-__global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_out O) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t s = g >> 6;
+// ============================================================== replay kernel
+// LDS = true: slices whose working slots fit (act_slots <= la, tim_slots <= lt);
+// LDS = false: the rest, with working slots in the global scratch.
+template <bool LDS>
+__global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu(CDR_WPE, 8))) void k_replay(
+    cdr_dev_batch B, cdr_out O, uint32_t la, uint32_t lt) {
+  const uint32_t s = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
   if (s >= B.ev.n_slices) return;
-  const int32_t w = B.ev.lane_wf[g];
+  const uint32_t act_cap = B.ev.slice_act_slots[s], tim_cap = B.ev.slice_tim_slots[s];
+  if ((act_cap <= la && tim_cap <= lt) != LDS) return;
+  const int32_t w = B.ev.lane_wf[(uint64_t)s * CDR_SLICE_WIDTH + lane];
   if (w < 0) return;
-  const cdr_wf_desc& D = B.wfs[w];
-  const cdr_wf_caps& CP = B.caps[w];
+  // per-workflow descriptor, capacities and output records, re-read where used
+#define D (late(B.wfs)[w])
+#define CP (late(B.caps)[w])
+#define X (late(O.exec) + w)
+#define RS (late(O.repl) + w)
   const uint32_t len = (uint32_t)D.ev_len;
   const uint32_t builder = D.builder;
-  const uint64_t base = B.ev.slice_row0[s] * CDR_SLICE_WIDTH + (g & 63);
   const uint32_t EU = B.empty_uuid;
   const bool isRS = builder == CDR_BUILDER_2DC;
   const bool isVH = builder == CDR_BUILDER_NDC;
 
-  cdr_activity_info* act = O.act + CP.act_off;
-  cdr_timer_info* tim = O.timer + CP.timer_off;
-  cdr_child_info* chi = O.child + CP.child_off;
-  cdr_cancel_info* can = O.cancel + CP.cancel_off;
-  cdr_signal_info* sig = O.signal + CP.signal_off;
-  cdr_vh_item* vh = O.vh + CP.vh_off;
-  cdr_reset_point* rp = O.rp + CP.rp_off;
-  cdr_kv* sa = O.sa + CP.sa_off;
-  cdr_exec_info* X = O.exec + w;
-  cdr_repl_state* RS = O.repl + w;
-  const uint32_t chi_cap = CP.child_cap, can_cap = CP.cancel_cap, sig_cap = CP.signal_cap, vh_cap = CP.vh_cap,
-                 rp_cap = CP.rp_cap, sa_cap = CP.sa_cap;
-  // working slots of pending activities / user timers (lane-interleaved scratch)
-  const uint32_t act_cap = B.ev.slice_act_slots[s], tim_cap = B.ev.slice_tim_slots[s];
-  uint64_t* const lane_scratch = B.scratch + B.ev.slice_scratch_off[s] + (g & 63);
-  __shared__ uint64_t lds_ws[LDS_WORDS];
-  const Lanes A{lane_scratch, lds_ws + threadIdx.x, CDR_ACT_PLANES};
-  const Lanes T{lane_scratch + (uint64_t)act_cap * CDR_ACT_PLANES * CDR_SLICE_WIDTH,
-                lds_ws + CDR_LDS_SLOTS * CDR_ACT_PLANES * 256 + threadIdx.x, CDR_TIM_PLANES};
+  // per-slice column descriptors (wave-uniform)
+  const uint64_t row0 = B.ev.slice_row0[s];
+  const uint32_t srows = B.ev.slice_len[s];
+  Cols C;
+  C.tf = slice_rsrc(B.ev.type_flags, row0, srows, 4);
+  C.id = slice_rsrc(B.ev.event_id, row0, srows, 8);
+  C.ver = slice_rsrc(B.ev.version, row0, srows, 8);
+  C.ts = slice_rsrc(B.ev.timestamp, row0, srows, 8);
+  C.key = slice_rsrc(B.ev.key, row0, srows, 8);
+  C.aux = slice_rsrc(B.ev.aux, row0, srows, 8);
+  C.h = slice_rsrc(B.ev.h, row0, srows, 4);
+  C.n = slice_rsrc(B.ev.n, row0, srows, 4);
+
+#define chi (late(O.child) + CP.child_off)
+#define can (late(O.cancel) + CP.cancel_off)
+#define sig (late(O.signal) + CP.signal_off)
+#define vh (late(O.vh) + CP.vh_off)
+#define rp (late(O.rp) + CP.rp_off)
+#define sa (late(O.sa) + CP.sa_off)
+#define chi_cap (CP.child_cap)
+#define can_cap (CP.cancel_cap)
+#define sig_cap (CP.signal_cap)
+#define vh_cap (CP.vh_cap)
+#define rp_cap (CP.rp_cap)
+#define sa_cap (CP.sa_cap)
+
+  // working slots of pending activities / user timers
+  typedef typename std::conditional<LDS, LdsSlots<CDR_ACT_PLANES>, GlbSlots<CDR_ACT_PLANES>>::type ASlots;
+  typedef typename std::conditional<LDS, LdsSlots<CDR_TIM_PLANES>, GlbSlots<CDR_TIM_PLANES>>::type TSlots;
+  ASlots A;
+  TSlots T;
+  if constexpr (LDS) {
+    A.l = lane;
+    T.l = la * CDR_ACT_PLANES * CDR_SLICE_WIDTH + lane;
+  } else {
+    GAS uint64_t* g = (GAS uint64_t*)(B.scratch + B.ev.slice_scratch_off[s] + lane);
+    A.g = g;
+    T.g = g + (uint64_t)act_cap * CDR_ACT_PLANES * CDR_SLICE_WIDTH;
+  }
   uint32_t cks_ok = 0;  // a binary checksum known to be in AutoResetPoints
 
   // ---- ExecutionInfo fields that later events change (registers); the fields only
   // WorkflowExecutionStarted writes go straight to the output record.
   uint32_t x_flags = 0;
-  int64_t x_completion_batch = 0, x_last_first = 0, x_last_task = 0, x_next_event = CDR_FIRST_EVENT_ID,
+  int64_t x_completion_batch = 0, x_next_event = CDR_FIRST_EVENT_ID,
           x_last_processed = CDR_EMPTY_EVENT_ID;
   int32_t x_dt_timeout_value = 0, x_state = CDR_STATE_CREATED, x_close = CDR_CLOSE_NONE, x_signals = 0;
   // decision (decisionInfo, mutableStateDecisionTaskManager.go:677-690)
@@ -321,7 +468,9 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
   int32_t dto = 0;
   // versions
   int64_t curv = D.failover_version;  // NDC currentVersion
-  int64_t rs_cur = curv, rs_start = curv, rs_lwv = CDR_EMPTY_VERSION, rs_lwid = CDR_EMPTY_EVENT_ID;
+  // 2DC ReplicationState: CurrentVersion and LastWrite{Version,EventID} always end as
+  // the last applied event's (prev_ver / prev_id); StartVersion is written through at
+  // WorkflowExecutionStarted; only the LastReplicationInfo mask stays in a register
   uint32_t rs_mask = 0;
   int64_t vh_last_id = 0, vh_last_ver = 0;  // the last VH item lives in registers
   uint32_t n_vh = 0;
@@ -344,30 +493,28 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
     stop_at_call_end = true; \
   } while (0)
 
-  // software pipeline of the column loads (CDR_PF: 1 = next event issued at the top
-  // of the iteration, 2 = at the bottom, 3 = two events ahead)
-#if CDR_PF == 3
-  Ev nxt = len ? load_ev(B.ev, base) : Ev{};
-  Ev nxt2 = len > 1 ? load_ev(B.ev, base + CDR_SLICE_WIDTH) : Ev{};
+  // ---- software pipeline: operands CDR_DEPTH events ahead, types two further ahead
+#if CDR_DEPTH == 2
+  Ev q0 = load_ops(C, 0, len, lane, load_tf(C, 0, len, lane));
+  Ev q1 = load_ops(C, 1, len, lane, load_tf(C, 1, len, lane));
+  uint32_t t2 = load_tf(C, 2, len, lane), t3 = load_tf(C, 3, len, lane);
 #else
-  Ev nxt = len ? load_ev(B.ev, base) : Ev{};
+  Ev q0 = load_ops(C, 0, len, lane, load_tf(C, 0, len, lane));
+  uint32_t t1 = load_tf(C, 1, len, lane), t2 = load_tf(C, 2, len, lane);
 #endif
-  for (uint32_t k = 0; k < len;
-#if CDR_PF == 2
-       nxt = (k + 1 < len) ? load_ev(B.ev, base + (uint64_t)(k + 1) * CDR_SLICE_WIDTH) : nxt, k++
+  for (uint32_t k = 0; k < len; k++) {
+    const Ev e = q0;
+#if CDR_DEPTH == 2
+    q0 = q1;
+    const uint32_t t4 = load_tf(C, k + 4, len, lane);
+    q1 = load_ops(C, k + 2, len, lane, t2);
+    t2 = t3;
+    t3 = t4;
 #else
-       k++
-#endif
-  ) {
-#if CDR_PF == 3
-    const Ev e = nxt;
-    nxt = nxt2;
-    if (k + 2 < len) nxt2 = load_ev(B.ev, base + (uint64_t)(k + 2) * CDR_SLICE_WIDTH);
-#elif CDR_PF == 2
-    const Ev e = nxt;
-#else
-    const Ev e = nxt;
-    if (k + 1 < len) nxt = load_ev(B.ev, base + (uint64_t)(k + 1) * CDR_SLICE_WIDTH);
+    const uint32_t t3 = load_tf(C, k + 3, len, lane);
+    q0 = load_ops(C, k + 1, len, lane, t1);
+    t1 = t2;
+    t2 = t3;
 #endif
     const uint32_t type = e.tf & 0xFFu;
     if ((e.tf & CDR_SEF_BATCH_FIRST) || k == 0) {
@@ -375,8 +522,6 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         // ---- end of the previous call: stateBuilder.go:603-604, plus the replication
         // state whose source is the call's last event (mutableStateBuilder.go:561-581)
         if (isRS) {
-          rs_lwv = prev_ver;
-          rs_lwid = prev_id;
           const int src = cluster_for_version(B.cluster, prev_ver);
           if (src < 0) {  // the panic fires at the call's first event, before anything else
             err = CDR_P_UNKNOWN_CLUSTER;
@@ -389,7 +534,6 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
           }
         }
         if (err != CDR_OK) break;
-        x_last_first = call_first_id;
         x_next_event = prev_id + 1;
         call_idx++;
       }
@@ -401,9 +545,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
     if (stop_at_call_end) continue;  // rest of a failed call: only its last event matters (2DC)
 
     // ---- version prelude (stateBuilder.go:134-154)
-    if (isRS) {
-      rs_cur = e.ver;  // UpdateReplicationStateVersion(v, true)
-    } else if (isVH) {
+    if (isVH) {  // (2DC: UpdateReplicationStateVersion(v, true) leaves CurrentVersion = e.ver)
       if (x_state == CDR_STATE_CREATED || x_state == CDR_STATE_RUNNING) curv = e.ver;  // UpdateCurrentVersion
       // NewVersionHistoryItem + AddOrUpdateItem (versionHistory.go:31-42,203-236)
       if (e.id < 0 || (e.ver < 0 && e.ver != CDR_EMPTY_VERSION)) {
@@ -423,17 +565,17 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
           FAIL(CDR_E_BAD_INPUT);
           continue;
         }
-        if (n_vh) vh[n_vh - 1] = cdr_vh_item{vh_last_id, vh_last_ver};  // close the previous item
+        if (n_vh) gput(vh + (n_vh - 1), cdr_vh_item{vh_last_id, vh_last_ver});  // close the previous item
         n_vh++;
         vh_last_ver = e.ver;
       }
       vh_last_id = e.id;
     }
-    x_last_task = e.task;  // :155
+    // LastEventTaskID (:155) is read once after the loop (last applied event)
 
     switch (type) {
       case CDR_EV_WF_STARTED: {  // stateBuilder.go:158-184 -> mutableStateBuilder.go:1639-1716
-        const cdr_attr_wf_started* a = reinterpret_cast<const cdr_attr_wf_started*>(B.ev.arena + (uint64_t)e.aux);
+        const GAS cdr_attr_wf_started* a = (const GAS cdr_attr_wf_started*)(B.ev.arena + (uint64_t)e.aux);
         const uint32_t af = a->flags;
         if ((af & CDR_SF_HAS_PARENT_DOMAIN) && (af & CDR_SF_PARENT_DOMAIN_MISSING)) {
           FAIL(CDR_E_DOMAIN_NOT_FOUND);
@@ -458,7 +600,6 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         x_state = CDR_STATE_CREATED;
         x_close = CDR_CLOSE_NONE;
         x_last_processed = CDR_EMPTY_EVENT_ID;
-        x_last_first = e.id;
         dv = CDR_EMPTY_VERSION;
         dsched = CDR_EMPTY_EVENT_ID;
         dstart = CDR_EMPTY_EVENT_ID;
@@ -504,13 +645,13 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
           const int64_t expiring = e.ts + (int64_t)D.retention_days * 24ll * 3600ll * NS_PER_S;
           const uint32_t crun = a->continued_run_id, off = a->reset_points_off, cnt = a->reset_points_len;
           for (uint32_t q = 0; q < cnt && q < rp_cap; q++) {
-            cdr_reset_point p = B.rps[off + q];
+            cdr_reset_point p = gget((const GAS cdr_reset_point*)B.rps + (off + q));
             const uint32_t run = (p.flags & CDR_RP_HAS_RUN_ID) ? p.run_id : 0u;
             if (run == crun) {
               p.flags |= CDR_RP_HAS_EXPIRING;
               p.expiring_time_nano = expiring;
             }
-            rp[n_rp++] = p;
+            gput(rp + n_rp++, p);
           }
         }
         if (af & CDR_SF_HAS_MEMO) {
@@ -522,7 +663,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         if (af & CDR_SF_HAS_SEARCH_ATTR) {
           n_sa = 0;
           const uint32_t off = a->search_attr_off, cnt = a->search_attr_len;
-          for (uint32_t q = 0; q < cnt && q < sa_cap; q++) sa[n_sa++] = B.kvs[off + q];
+          for (uint32_t q = 0; q < cnt && q < sa_cap; q++) gput(sa + n_sa++, gget((const GAS cdr_kv*)B.kvs + (off + q)));
           if (n_sa) x_flags |= CDR_XI_HAS_SEARCH_ATTR;
           else x_flags &= ~CDR_XI_HAS_SEARCH_ATTR;
         }
@@ -534,7 +675,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         X->branch_id_lo = lo;
         X->branch_id_hi = hi;
         x_flags |= isVH ? CDR_XI_VH_BRANCH : CDR_XI_HAS_BRANCH;
-        if (isRS) rs_start = e.ver;  // :182-184
+        if (isRS) RS->start_version = e.ver;  // :182-184
         break;
       }
       case CDR_EV_DT_SCHEDULED:  // :186-200 -> mutableStateDecisionTaskManager.go:143-167
@@ -574,7 +715,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         if (cks && cks != cks_ok) {  // addBinaryCheckSumIfNotExists (mutableStateBuilder.go:1798-1842)
           bool exists = false;
           for (uint32_t q = 0; q < n_rp; q++) {
-            const cdr_reset_point& p = rp[q];
+            const cdr_reset_point p = gget(rp + q);
             exists |= ((p.flags & CDR_RP_HAS_CHECKSUM) ? p.binary_checksum : 0u) == cks;
           }
           if (!exists) {
@@ -583,7 +724,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
               break;
             }
             const bool resettable = live_chi == 0 && live_can == 0 && live_sig == 0;
-            cdr_reset_point& p = rp[n_rp++];
+            cdr_reset_point p;
             p.binary_checksum = cks;
             p.run_id = D.run_id;
             p.first_decision_completed_id = e.id;
@@ -592,6 +733,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
             p.flags = CDR_RP_HAS_CHECKSUM | CDR_RP_HAS_RUN_ID | CDR_RP_HAS_FIRST_DC_ID | CDR_RP_HAS_CREATED |
                       CDR_RP_HAS_RESETTABLE | (resettable ? CDR_RP_RESETTABLE : 0u);
             p._pad = 0;
+            gput(rp + n_rp++, p);
             x_flags |= CDR_XI_HAS_RESET_POINTS;
           }
           cks_ok = cks;  // the list only grows until the next WorkflowExecutionStarted
@@ -611,7 +753,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         dorig_ts = 0;
         dsc_ts = inc ? B.now_ns : 0;
         if (datt != 0) {  // transient decision: no decision is pending here by construction
-          dv = isRS ? rs_cur : (isVH ? curv : CDR_EMPTY_VERSION);
+          dv = isRS ? e.ver : (isVH ? curv : CDR_EMPTY_VERSION);
           dsched = x_next_event;  // NextEventID as of the call's start
           dto = x_dt_timeout_value;
           dsc_ts = B.now_ns;
@@ -619,16 +761,15 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         break;
       }
       case CDR_EV_AT_SCHEDULED: {  // :259-269 -> mutableStateBuilder.go:1982-2028
-        const cdr_attr_at_scheduled* a = reinterpret_cast<const cdr_attr_at_scheduled*>(B.ev.arena + (uint64_t)e.aux);
         const uint32_t aid = (uint32_t)e.key;
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++) {
-          if (A(j, AP_SID) == DEAD_KEY) {
+          if (A.ld(j, AP_SID) == DEAD_KEY) {
             if (slot < 0) slot = (int)j;
           } else {
-            const uint64_t m = (uint64_t)A(j, AP_META);
-            if ((uint32_t)m == aid && ((m >> 32) & AF_AIDMAP))  // byActivityID[aid] is overwritten
-              A(j, AP_META) = (int64_t)(m & ~((uint64_t)AF_AIDMAP << 32));
+            const uint64_t m = (uint64_t)A.ld(j, AP_META);
+            if ((uint32_t)m == aid && (m & META_FLAG(AF_AIDMAP)))  // byActivityID[aid] is overwritten
+              A.st(j, AP_META, (int64_t)(m & ~META_FLAG(AF_AIDMAP)));
           }
         }
         if (slot < 0) {
@@ -639,46 +780,40 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
           slot = (int)hw_act++;
         }
         const uint32_t j = (uint32_t)slot;
-        const int32_t s2c = a->s2c_s, xs = a->retry_expiration_s;
-        const bool retry = (a->flags & CDR_AF_HAS_RETRY) != 0;
-        const int64_t exp = e.ts + (int64_t)((retry && xs > s2c) ? xs : s2c) * NS_PER_S;
-        const int64_t t_s2c = e.ts + (int64_t)s2c * NS_PER_S;
-        A(j, AP_SID) = e.id;
-        A(j, AP_META) = (int64_t)(aid | ((uint64_t)AF_AIDMAP << 32));
-        A(j, AP_TTS) = CDR_TIMER_TASK_STATUS_NONE;
-        A(j, AP_VER) = e.ver;
-        A(j, AP_TS2C) = exp < t_s2c ? exp : t_s2c;
-        A(j, AP_TALT) = e.ts + (int64_t)a->s2s_s * NS_PER_S;
-        A(j, AP_THB) = T_NONE;
-        A(j, AP_STARTED_ID) = CDR_EMPTY_EVENT_ID;
-        A(j, AP_STARTED_TIME) = 0;
-        A(j, AP_CANCEL_ID) = CDR_EMPTY_EVENT_ID;
-        A(j, AP_AREC) = e.aux;
-        A(j, AP_SCHED_TIME) = e.ts;
-        A(j, AP_BATCH) = call_first_id;
-        A(j, AP_EXP) = exp;
-        A(j, AP_STC_HB) = (int64_t)((uint32_t)a->stc_s | ((uint64_t)(uint32_t)a->hb_s << 32));
+        const int32_t s2c = (int32_t)e.h, s2s = e.n;
+        A.st(j, AP_SID, e.id);
+        A.st(j, AP_TS2C, e.ts + (int64_t)s2c * NS_PER_S);
+        A.st(j, AP_TALT, e.ts + (int64_t)s2s * NS_PER_S);
+        A.st(j, AP_THB, T_NONE);
+        A.st(j, AP_META, (int64_t)(aid | META_FLAG(AF_AIDMAP)));
+        A.st(j, AP_VER, e.ver);
+        A.st(j, AP_STARTED_ID, CDR_EMPTY_EVENT_ID);
+        A.st(j, AP_STARTED_TIME, 0);
+        A.st(j, AP_CANCEL_ID, CDR_EMPTY_EVENT_ID);
+        A.st(j, AP_ROWS, (int64_t)(k | ((uint64_t)call_first_k << 32)));
+        A.st(j, AP_STC_HB, (int64_t)(((uint64_t)e.key >> 32) | ((uint64_t)e.aux & 0xFFFFFFFF00000000ull)));
+        A.st(j, AP_REQ, 0);
         act_pick(A, hw_act);
         break;
       }
       case CDR_EV_AT_STARTED: {  // :271-278 -> :2083-2098
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++)
-          if (A(j, AP_SID) == e.key) slot = (int)j;
+          if (A.ld(j, AP_SID) == e.key) slot = (int)j;
         if (slot < 0) {
           FAIL(CDR_P_ACTIVITY_STARTED_NIL);  // nil deref in Go
           break;
         }
         const uint32_t j = (uint32_t)slot;
-        const uint64_t th = (uint64_t)A(j, AP_STC_HB);
+        const uint64_t th = (uint64_t)A.ld(j, AP_STC_HB);
         const int32_t stc = (int32_t)(uint32_t)th, hb = (int32_t)(uint32_t)(th >> 32);
-        A(j, AP_VER) = e.ver;
-        A(j, AP_STARTED_ID) = e.id;
-        A(j, AP_TTS) = (int64_t)(((uint64_t)(uint32_t)A(j, AP_TTS)) | ((uint64_t)e.h << 32));
-        A(j, AP_STARTED_TIME) = e.ts;  // LastHeartBeatUpdatedTime = StartedTime
-        A(j, AP_META) = (int64_t)((uint64_t)A(j, AP_META) | ((uint64_t)AF_STARTED << 32));
-        A(j, AP_TALT) = e.ts + (int64_t)stc * NS_PER_S;
-        A(j, AP_THB) = hb > 0 ? e.ts + (int64_t)hb * NS_PER_S : T_NONE;
+        A.st(j, AP_VER, e.ver);
+        A.st(j, AP_STARTED_ID, e.id);
+        A.st(j, AP_REQ, (int64_t)e.h);
+        A.st(j, AP_STARTED_TIME, e.ts);  // LastHeartBeatUpdatedTime = StartedTime
+        A.st(j, AP_META, (int64_t)((uint64_t)A.ld(j, AP_META) | META_FLAG(AF_STARTED)));
+        A.st(j, AP_TALT, e.ts + (int64_t)stc * NS_PER_S);
+        A.st(j, AP_THB, hb > 0 ? e.ts + (int64_t)hb * NS_PER_S : T_NONE);
         act_pick(A, hw_act);
         break;
       }
@@ -688,22 +823,22 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
       case CDR_EV_AT_CANCELED: {
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++)
-          if (A(j, AP_SID) == e.key) slot = (int)j;
+          if (A.ld(j, AP_SID) == e.key) slot = (int)j;
         if (slot < 0) {
           FAIL(CDR_E_ACTIVITY_NOT_FOUND);
           break;
         }
-        const uint64_t m = (uint64_t)A((uint32_t)slot, AP_META);
+        const uint64_t m = (uint64_t)A.ld((uint32_t)slot, AP_META);
         const uint32_t aid = (uint32_t)m;
-        A((uint32_t)slot, AP_SID) = DEAD_KEY;
-        A((uint32_t)slot, AP_META) = (int64_t)(m & ~((uint64_t)AF_AIDMAP << 32));
-        bool found = ((m >> 32) & AF_AIDMAP) != 0;
+        A.st((uint32_t)slot, AP_SID, DEAD_KEY);
+        A.st((uint32_t)slot, AP_META, (int64_t)(m & ~META_FLAG(AF_AIDMAP)));
+        bool found = (m & META_FLAG(AF_AIDMAP)) != 0;
         if (!found)
           for (uint32_t j = 0; j < hw_act; j++) {
-            if (A(j, AP_SID) == DEAD_KEY) continue;
-            const uint64_t mj = (uint64_t)A(j, AP_META);
-            if ((uint32_t)mj == aid && ((mj >> 32) & AF_AIDMAP)) {
-              A(j, AP_META) = (int64_t)(mj & ~((uint64_t)AF_AIDMAP << 32));
+            if (A.ld(j, AP_SID) == DEAD_KEY) continue;
+            const uint64_t mj = (uint64_t)A.ld(j, AP_META);
+            if ((uint32_t)mj == aid && (mj & META_FLAG(AF_AIDMAP))) {
+              A.st(j, AP_META, (int64_t)(mj & ~META_FLAG(AF_AIDMAP)));
               found = true;
             }
           }
@@ -718,27 +853,27 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         const uint32_t aid = (uint32_t)e.key;
         int slot = -1;
         for (uint32_t j = 0; j < hw_act; j++) {
-          if (A(j, AP_SID) == DEAD_KEY) continue;
-          const uint64_t mj = (uint64_t)A(j, AP_META);
-          if ((uint32_t)mj == aid && ((mj >> 32) & AF_AIDMAP)) slot = (int)j;
+          if (A.ld(j, AP_SID) == DEAD_KEY) continue;
+          const uint64_t mj = (uint64_t)A.ld(j, AP_META);
+          if ((uint32_t)mj == aid && (mj & META_FLAG(AF_AIDMAP))) slot = (int)j;
         }
         if (slot < 0) {
           FAIL(CDR_E_MISSING_ACTIVITY_INFO);
           break;
         }
         const uint32_t j = (uint32_t)slot;
-        A(j, AP_VER) = e.ver;
-        A(j, AP_META) = (int64_t)((uint64_t)A(j, AP_META) | ((uint64_t)AF_CANCEL << 32));
-        A(j, AP_CANCEL_ID) = e.id;
+        A.st(j, AP_VER, e.ver);
+        A.st(j, AP_META, (int64_t)((uint64_t)A.ld(j, AP_META) | META_FLAG(AF_CANCEL)));
+        A.st(j, AP_CANCEL_ID, e.id);
         break;
       }
       case CDR_EV_TIMER_STARTED: {  // :324-332 -> :2877-2900
         const uint32_t tid = (uint32_t)e.key;
         int slot = -1, free_slot = -1;
         for (uint32_t j = 0; j < hw_tim; j++) {
-          if (T(j, TP_SID) == DEAD_KEY) {
+          if (T.ld(j, TP_SID) == DEAD_KEY) {
             if (free_slot < 0) free_slot = (int)j;
-          } else if ((uint32_t)T(j, TP_TID_TASK) == tid) {
+          } else if ((uint32_t)T.ld(j, TP_TID_TASK) == tid) {
             slot = (int)j;
           }
         }
@@ -751,10 +886,10 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
           slot = (int)hw_tim++;
         }
         const uint32_t j = (uint32_t)slot;
-        T(j, TP_SID) = e.id;
-        T(j, TP_TID_TASK) = (int64_t)tid;  // TaskID = TimerTaskStatusNone
-        T(j, TP_EXPIRY) = e.ts + e.aux * NS_PER_S;
-        T(j, TP_VER) = e.ver;
+        T.st(j, TP_SID, e.id);
+        T.st(j, TP_TID_TASK, (int64_t)tid);  // TaskID = TimerTaskStatusNone
+        T.st(j, TP_EXPIRY, e.ts + e.aux * NS_PER_S);
+        T.st(j, TP_VER, e.ver);
         tim_pick(T, hw_tim);
         break;
       }
@@ -762,7 +897,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
       case CDR_EV_TIMER_CANCELED: {  // :343-350
         const uint32_t tid = (uint32_t)e.key;
         for (uint32_t j = 0; j < hw_tim; j++)
-          if (T(j, TP_SID) != DEAD_KEY && (uint32_t)T(j, TP_TID_TASK) == tid) T(j, TP_SID) = DEAD_KEY;
+          if (T.ld(j, TP_SID) != DEAD_KEY && (uint32_t)T.ld(j, TP_TID_TASK) == tid) T.st(j, TP_SID, DEAD_KEY);
         tim_pick(T, hw_tim);
         break;
       }
@@ -772,7 +907,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
           FAIL(CDR_E_BAD_INPUT);
           break;
         }
-        cdr_child_info& c = chi[slot];
+        cdr_child_info c;
         c.version = e.ver;
         c.initiated_id = e.id;
         c.initiated_event_batch_id = call_first_id;
@@ -787,6 +922,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         c.workflow_type = (uint32_t)e.aux;
         c.parent_close_policy = e.n;
         c._pad = 0;
+        gput(chi + slot, c);
         live_chi++;
         if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
         break;
@@ -820,7 +956,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
           FAIL(CDR_E_BAD_INPUT);
           break;
         }
-        cdr_cancel_info& c = can[slot];
+        cdr_cancel_info c;
         c.version = e.ver;
         c.initiated_event_batch_id = call_first_id;
         c.initiated_id = e.id;
@@ -828,6 +964,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         cdr_uuid(B.uuid_seed, D.wf_key, CDR_UUID_CANCEL_REQ, e.id, &lo, &hi);
         c.cancel_request_lo = lo;
         c.cancel_request_hi = hi;
+        gput(can + slot, c);
         live_can++;
         if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
         break;
@@ -847,7 +984,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
           FAIL(CDR_E_BAD_INPUT);
           break;
         }
-        cdr_signal_info& c = sig[slot];
+        cdr_signal_info c;
         c.version = e.ver;
         c.initiated_event_batch_id = call_first_id;
         c.initiated_id = e.id;
@@ -859,6 +996,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         c.input = (uint32_t)((uint64_t)e.aux >> 32);
         c.control = (uint32_t)e.aux;
         c._pad = 0;
+        gput(sig + slot, c);
         live_sig++;
         if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
         break;
@@ -905,20 +1043,20 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         const uint64_t off = (uint64_t)e.aux;
         const uint32_t cnt = e.h;
         for (uint32_t q = 0; q < cnt; q++) {
-          const cdr_kv kv = B.kvs[off + q];
+          const cdr_kv kv = gget((const GAS cdr_kv*)B.kvs + (off + q));
           bool found = false;
           for (uint32_t j = 0; j < n_sa; j++)
             if (sa[j].key == kv.key) {
               sa[j].value = kv.value;
               found = true;
             }
-          if (!found && n_sa < sa_cap) sa[n_sa++] = kv;
+          if (!found && n_sa < sa_cap) gput(sa + n_sa++, kv);
         }
         x_flags |= CDR_XI_HAS_SEARCH_ATTR;
         break;
       }
       case CDR_EV_WF_CONTINUED_AS_NEW: {  // :537-595
-        if (D.newrun < 0 || call_idx != D.newrun_call || B.wfs[D.newrun].ev_len == 0) {
+        if (D.newrun < 0 || call_idx != D.newrun_call || late(B.wfs)[D.newrun].ev_len == 0) {
           FAIL(CDR_E_NEWRUN_HISTORY_EMPTY);
           break;
         }
@@ -941,8 +1079,6 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
   // ---- end of the last call
   if (len > 0 && (err == CDR_OK || stop_at_call_end)) {
     if (isRS) {
-      rs_lwv = prev_ver;
-      rs_lwid = prev_id;
       const int src = cluster_for_version(B.cluster, prev_ver);
       if (src < 0) {
         err = CDR_P_UNKNOWN_CLUSTER;
@@ -954,10 +1090,7 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
         rs_mask |= 1u << src;
       }
     }
-    if (err == CDR_OK) {
-      x_last_first = call_first_id;
-      x_next_event = prev_id + 1;
-    }
+    if (err == CDR_OK) x_next_event = prev_id + 1;
   }
   if (err == CDR_OK && D.parent < 0 && D.expected_next_event_id != 0 && x_next_event != D.expected_next_event_id) {
     err = CDR_E_REBUILD_NEXT_EVENT_ID;  // nDCStateRebuilder.go:139-143
@@ -981,62 +1114,73 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
   r.n_vh = n_vh;
   r.n_reset_points = n_rp;
   r.n_search_attr = n_sa;
+  const uint64_t lane_base = (row0 * CDR_SLICE_WIDTH) + lane;  // element of row 0 of this lane
   if (err == CDR_OK) {
-    // emit the live working slots as persisted rows (k_tables orders them by key)
+    // emit the live working slots as persisted rows (k_tables orders them by key);
+    // fields the loop did not carry are re-read from the scheduling event's row
+    GAS cdr_activity_info* act = (GAS cdr_activity_info*)(O.act + CP.act_off);
+    GAS cdr_timer_info* tim = (GAS cdr_timer_info*)(O.timer + CP.timer_off);
     uint32_t n = 0;
     for (uint32_t j = 0; j < hw_act; j++) {
-      const int64_t sid = A(j, AP_SID);
+      const int64_t sid = A.ld(j, AP_SID);
       if (sid == DEAD_KEY) continue;
-      const cdr_attr_at_scheduled* a = reinterpret_cast<const cdr_attr_at_scheduled*>(B.ev.arena + (uint64_t)A(j, AP_AREC));
-      const uint64_t m = (uint64_t)A(j, AP_META), tts = (uint64_t)A(j, AP_TTS);
-      const uint32_t fl = (uint32_t)(m >> 32);
+      const uint64_t rows = (uint64_t)A.ld(j, AP_ROWS);
+      const uint64_t i_s = lane_base + (uint64_t)(uint32_t)rows * CDR_SLICE_WIDTH;
+      const uint64_t i_b = lane_base + (rows >> 32) * CDR_SLICE_WIDTH;
+      const int64_t sched_ts = ((const GAS int64_t*)B.ev.timestamp)[i_s];
+      const uint32_t arec = (uint32_t)((const GAS uint64_t*)B.ev.aux)[i_s];
+      const GAS cdr_attr_at_scheduled* a = (const GAS cdr_attr_at_scheduled*)(B.ev.arena + arec);
+      const uint64_t m = (uint64_t)A.ld(j, AP_META);
       const bool retry = (a->flags & CDR_AF_HAS_RETRY) != 0;
-      cdr_activity_info& o = act[n++];
-      o.version = A(j, AP_VER);
+      const int32_t s2c = a->s2c_s, xs = a->retry_expiration_s;
+      cdr_activity_info o;
+      o.version = A.ld(j, AP_VER);
       o.schedule_id = sid;
-      o.scheduled_event_batch_id = A(j, AP_BATCH);
-      o.scheduled_time = A(j, AP_SCHED_TIME);
-      o.started_id = A(j, AP_STARTED_ID);
-      o.started_time = A(j, AP_STARTED_TIME);
+      o.scheduled_event_batch_id = ((const GAS int64_t*)B.ev.event_id)[i_b];
+      o.scheduled_time = sched_ts;
+      o.started_id = A.ld(j, AP_STARTED_ID);
+      o.started_time = A.ld(j, AP_STARTED_TIME);
       o.last_heartbeat_time = o.started_time;
-      o.expiration_time = A(j, AP_EXP);
-      o.cancel_request_id = A(j, AP_CANCEL_ID);
+      o.expiration_time = sched_ts + (int64_t)((retry && xs > s2c) ? xs : s2c) * NS_PER_S;
+      o.cancel_request_id = A.ld(j, AP_CANCEL_ID);
       o.activity_id = (uint32_t)m;
-      o.request_id = (uint32_t)(tts >> 32);
+      o.request_id = (uint32_t)A.ld(j, AP_REQ);
       o.task_list = a->task_list;
       o.nonretriable = retry ? a->nonretriable : 0u;
       o.s2s = a->s2s_s;
-      o.s2c = a->s2c_s;
+      o.s2c = s2c;
       o.stc = a->stc_s;
       o.hb = a->hb_s;
-      o.timer_task_status = (int32_t)(uint32_t)tts;
+      o.timer_task_status = (int32_t)((m >> META_TTS_SHIFT) & 0xFFu);
       o.attempt = 0;
       o.initial_interval = retry ? a->retry_initial_s : 0;
       o.maximum_interval = retry ? a->retry_max_interval_s : 0;
       o.maximum_attempts = retry ? a->retry_max_attempts : 0;
-      o.flags = (retry ? CDR_AI_HAS_RETRY : 0u) | ((fl & AF_CANCEL) ? CDR_AI_CANCEL_REQUESTED : 0u) |
-                ((fl & AF_STARTED) ? CDR_AI_STARTED_TIME_SET : 0u);
+      o.flags = (retry ? CDR_AI_HAS_RETRY : 0u) | ((m & META_FLAG(AF_CANCEL)) ? CDR_AI_CANCEL_REQUESTED : 0u) |
+                ((m & META_FLAG(AF_STARTED)) ? CDR_AI_STARTED_TIME_SET : 0u);
       o.backoff_coefficient = retry ? a->backoff_coefficient : 0.0;
+      gput(act + n++, o);
     }
     r.n_activity = n;
     n = 0;
     for (uint32_t j = 0; j < hw_tim; j++) {
-      const int64_t sid = T(j, TP_SID);
+      const int64_t sid = T.ld(j, TP_SID);
       if (sid == DEAD_KEY) continue;
-      const uint64_t tt = (uint64_t)T(j, TP_TID_TASK);
-      cdr_timer_info& o = tim[n++];
-      o.version = T(j, TP_VER);
+      const uint64_t tt = (uint64_t)T.ld(j, TP_TID_TASK);
+      cdr_timer_info o;
+      o.version = T.ld(j, TP_VER);
       o.started_id = sid;
-      o.expiry_time = T(j, TP_EXPIRY);
+      o.expiry_time = T.ld(j, TP_EXPIRY);
       o.task_id = (int64_t)(tt >> 32);
       o.timer_id = (uint32_t)tt;
       o._pad = 0;
+      gput(tim + n++, o);
     }
     r.n_timer = n;
   }
-  O.result[w] = r;
+  gput((GAS cdr_wf_result*)O.result + w, r);
   if (err != CDR_OK) return;
-  if (n_vh) vh[n_vh - 1] = cdr_vh_item{vh_last_id, vh_last_ver};
+  if (n_vh) gput(vh + (n_vh - 1), cdr_vh_item{vh_last_id, vh_last_ver});
   if (!(x_flags & CDR_XI_STARTED)) {  // no WorkflowExecutionStarted: its fields keep their zero values
     X->domain_id = X->workflow_id = X->run_id = X->create_request_id = 0;
     X->parent_domain_id = X->parent_workflow_id = X->parent_run_id = X->task_list = 0;
@@ -1055,8 +1199,10 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
   X->decision_timeout_value = x_dt_timeout_value;
   X->state = x_state;
   X->close_status = x_close;
-  X->last_first_event_id = x_last_first;
-  X->last_event_task_id = x_last_task;
+  X->last_first_event_id = call_first_id;  // stateBuilder.go:603 of the last call
+  // LastEventTaskID (stateBuilder.go:155): every applied event sets it, so an OK
+  // workflow ends with its last event's task id
+  X->last_event_task_id = ((const GAS int64_t*)B.ev.task_id)[lane_base + (uint64_t)(len - 1) * CDR_SLICE_WIDTH];
   X->next_event_id = x_next_event;
   X->last_processed_event = x_last_processed;
   X->signal_count = x_signals;
@@ -1072,10 +1218,10 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
   X->reset_points_len = n_rp;
   X->search_attr_len = n_sa;
   if (isRS) {
-    RS->current_version = rs_cur;
-    RS->start_version = rs_start;
-    RS->last_write_version = rs_lwv;
-    RS->last_write_event_id = rs_lwid;
+    RS->current_version = prev_ver;
+    if (!(x_flags & CDR_XI_STARTED)) RS->start_version = D.failover_version;
+    RS->last_write_version = prev_ver;
+    RS->last_write_event_id = prev_id;
     for (int c = 0; c < CDR_MAX_CLUSTERS; c++)
       if (!(rs_mask & (1u << c))) {
         RS->lri_version[c] = 0;
@@ -1084,23 +1230,37 @@ __global__ __launch_bounds__(256, CDR_MINW) void k_replay(cdr_dev_batch B, cdr_o
     RS->lri_mask = rs_mask;
     RS->present = 1;
   } else {
-    *RS = cdr_repl_state{};
+    gput(RS, cdr_repl_state{});
   }
 }
 
+#undef D
+#undef CP
+#undef X
+#undef RS
+#undef chi
+#undef can
+#undef sig
+#undef vh
+#undef rp
+#undef sa
+#undef chi_cap
+#undef can_cap
+#undef sig_cap
+#undef vh_cap
+#undef rp_cap
+#undef sa_cap
+
 // Per-workflow table epilogue: move live rows to the front in key order (the
-// canonical order of the Go maps' keys), drop kernel-private flags, sort the
-// SearchAttributes map by key, and turn high-water marks into live counts.
+// canonical order of the Go maps' keys), sort the SearchAttributes map by key, and
+// turn high-water marks into live counts.
 __global__ __launch_bounds__(256) void k_tables(cdr_dev_batch B, cdr_out O) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= B.n_wfs) return;
   cdr_wf_result& r = O.result[w];
   if (r.code != CDR_OK) return;
   const cdr_wf_caps& cp = B.caps[w];
-  cdr_activity_info* act = O.act + cp.act_off;
-  const uint32_t na = compact_sorted(act, r.n_activity, ActKey{});
-  for (uint32_t j = 0; j < na; j++) act[j].flags &= ~AI_IN_AID_MAP;
-  r.n_activity = na;
+  r.n_activity = compact_sorted(O.act + cp.act_off, r.n_activity, ActKey{});
   r.n_timer = compact_sorted(O.timer + cp.timer_off, r.n_timer, TimerKey{});
   r.n_child = compact_sorted(O.child + cp.child_off, r.n_child, ChildKey{});
   r.n_cancel = compact_sorted(O.cancel + cp.cancel_off, r.n_cancel, CancelKey{});
@@ -1193,11 +1353,19 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   if (!c || !in || !out) return CDR_API_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipSetDevice(c->device));
-  const uint32_t threads = in->ev.n_slices * CDR_SLICE_WIDTH;
-  const uint32_t blocks = (threads + 255) / 256;
+  // LDS budget: up to CDR_LDS_ACT_MAX activity and CDR_LDS_TIM_MAX timer slots per
+  // lane; slices that need more replay in the scratch-slot launch
+  const uint32_t la = in->max_act_slots < CDR_LDS_ACT_MAX ? in->max_act_slots : CDR_LDS_ACT_MAX;
+  const uint32_t lt = in->max_tim_slots < CDR_LDS_TIM_MAX ? in->max_tim_slots : CDR_LDS_TIM_MAX;
+  const size_t lds = (size_t)(la * CDR_ACT_PLANES + lt * CDR_TIM_PLANES) * CDR_SLICE_WIDTH * sizeof(uint64_t);
+  const bool spill = in->max_act_slots > la || in->max_tim_slots > lt;
+  const uint32_t blocks = in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
-  if (blocks) hipLaunchKernelGGL(k_replay, dim3(blocks), dim3(256), 0, st, *in, *out);
+  if (blocks) hipLaunchKernelGGL(k_replay<true>, dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, *in, *out, la, lt);
+  HIPCHK(hipGetLastError());
+  if (blocks && spill)
+    hipLaunchKernelGGL(k_replay<false>, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, *in, *out, la, lt);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used + 1] : c->ev[1], st));
   if (ring) {
@@ -1226,10 +1394,6 @@ int cdr_last_kernel_ms(cdr_ctx* c, float* replay_ms, float* finalize_ms) {
   if (finalize_ms) *finalize_ms = b;
   return CDR_API_OK;
 }
-
-}  // extern "C"
-
-extern "C" {
 
 // Start recording the replay kernel of the next `max_launches` launches with HIP
 // events on their launch stream (bench.py's in-process kernel timing).

@@ -845,7 +845,7 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
     }
     ent += m;
   }
-  if (ab > o->arena_words) return CDR_API_EINVAL;
+  if (ab > o->arena_words || ab >= (1ull << 32)) return CDR_API_EINVAL;  // u32 arena offsets (cdr.h)
   uint32_t ns = 0;
   uint64_t rows = 0;
   int rc = cdr_plan_slices(lens.data(), ent, const_cast<int32_t*>(o->lane_wf), const_cast<uint32_t*>(o->slice_len),

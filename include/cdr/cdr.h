@@ -45,7 +45,30 @@ extern "C" {
 /* Sliced event layout ("SELL-64"): workflows are grouped 64 to a slice (one lane
  * each, slices sorted by length); event k of lane L of slice s lives at element
  * (slice_row0[s] + k) * 64 + L of every column, so a wavefront that walks its 64
- * histories in lockstep reads each column fully coalesced. */
+ * histories in lockstep reads each column fully coalesced.  The kernel reads only
+ * the columns an event's type needs (replay.hip: NEED_*).
+ *
+ * Operand columns per type (all others 0):
+ *   WorkflowExecutionStarted  aux = arena word offset of cdr_attr_wf_started
+ *   DecisionTaskScheduled     aux = attempt, n = StartToCloseTimeoutSeconds
+ *   DecisionTaskStarted       key = scheduledEventId, h = requestId
+ *   DecisionTaskCompleted     key = scheduledEventId, aux = startedEventId, h = binaryChecksum
+ *   DecisionTaskTimedOut      n = timeoutType
+ *   ActivityTaskScheduled     key = activityId | (u32)StartToClose << 32, h = (u32)ScheduleToClose,
+ *                             n = ScheduleToStart, aux = arena word offset (< 2^32) of
+ *                             cdr_attr_at_scheduled | (u32)Heartbeat << 32
+ *   ActivityTask{Started,Completed,Failed,TimedOut,Canceled}  key = scheduledEventId
+ *                             (Started: h = requestId)
+ *   ActivityTaskCancelRequested / RequestCancelActivityTaskFailed  key = activityId
+ *   Timer{Started,Fired,Canceled}, CancelTimerFailed  key = timerId (Started: aux = startToFireSeconds)
+ *   StartChildWorkflowExecutionInitiated  key = domain, aux = workflowType, h = workflowId,
+ *                             n = parentClosePolicy
+ *   SignalExternalWorkflowExecutionInitiated  key = domain, aux = input << 32 | control, h = signalName
+ *   RequestCancelExternalWorkflowExecutionInitiated  key = domain
+ *   ChildWorkflowExecutionStarted  key = initiatedEventId, h = runId
+ *   other child / external closes  key = initiatedEventId
+ *   UpsertWorkflowSearchAttributes  aux = kv offset, h = kv count
+ *   WorkflowExecutionContinuedAsNew  h = newExecutionRunId */
 typedef struct cdr_slices {
   uint32_t n_slices, _pad;
   uint64_t n_rows;        /* sum of slice_len */
@@ -71,7 +94,7 @@ typedef struct cdr_slices {
   const uint32_t* slice_tim_slots;   /* [n_slices] user-timer working slots per lane */
 } cdr_slices;
 
-#define CDR_ACT_PLANES 15 /* words per activity working slot (replay.hip) */
+#define CDR_ACT_PLANES 12 /* words per activity working slot (replay.hip) */
 #define CDR_TIM_PLANES 4  /* words per user-timer working slot */
 
 #define CDR_SEF_BATCH_FIRST (1u << 8)
@@ -87,6 +110,9 @@ typedef struct cdr_dev_batch {
   const cdr_reset_point* rps;
   uint32_t n_wfs;
   uint32_t empty_uuid; /* handle of "emptyUuid" (mutableStateBuilder.go:42) */
+  /* max over slices of slice_act_slots / slice_tim_slots (cdr_plan_scratch): the
+   * launcher keeps up to this many working slots per lane in LDS (0 = all in scratch) */
+  uint32_t max_act_slots, max_tim_slots;
   cdr_cluster_meta cluster;
   int64_t now_ns;
   uint64_t uuid_seed;

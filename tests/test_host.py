@@ -93,8 +93,14 @@ def test_pack_round_trip():
             assert (cols["event_id"][j], cols["version"][j], cols["timestamp"][j], cols["task_id"][j]) == (
                 e.event_id, e.version, e.timestamp, e.task_id)
             if e.type == abi.EV["ActivityTaskScheduled"]:
-                rec = abi.AttrATSched.from_buffer_copy(arena[cols["aux"][j]:cols["aux"][j] + 7].tobytes())
-                assert bytes(rec) == bytes(e.a.at_sched) and cols["key"][j] == e.a.at_sched.activity_id
+                a = e.a.at_sched
+                off = int(cols["aux"][j]) & 0xFFFFFFFF
+                rec = abi.AttrATSched.from_buffer_copy(arena[off:off + 7].tobytes())
+                assert bytes(rec) == bytes(a)
+                assert int(cols["key"][j]) & 0xFFFFFFFF == a.activity_id
+                assert (int(cols["key"][j]) >> 32) & 0xFFFFFFFF == a.stc_s & 0xFFFFFFFF
+                assert (int(cols["aux"][j]) >> 32) & 0xFFFFFFFF == a.hb_s & 0xFFFFFFFF
+                assert cols["h"][j] == a.s2c_s & 0xFFFFFFFF and cols["n"][j] == a.s2s_s
             elif e.type == abi.EV["ActivityTaskStarted"]:
                 assert cols["key"][j] == e.a.at.scheduled_event_id and cols["h"][j] == e.a.at.request_id
             elif e.type == abi.EV["TimerStarted"]:
