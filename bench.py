@@ -87,10 +87,7 @@ class DeviceBatch:
         info = abi.CdrSynthPlanInfo()
         assert L.cdr_synth_sliced_plan(C.byref(p), C.byref(info)) == 0
         self.info = info
-        n = info.n_rows * 64
-        cols = {"type_flags": np.uint32, "event_id": np.int64, "version": np.int64, "timestamp": np.int64,
-                "task_id": np.int64, "key": np.int64, "aux": np.int64, "h": np.uint32, "n": np.int32}
-        self.h_cols = {k: np.empty(n, dt) for k, dt in cols.items()}
+        self.h_slab = np.empty(info.n_rows * 64 * abi.EL_BYTES, np.uint8)
         self.h_lane = np.empty(info.n_slices * 64, np.int32)
         self.h_slen = np.empty(info.n_slices, np.uint32)
         self.h_row0 = np.empty(info.n_slices, np.uint64)
@@ -105,8 +102,7 @@ class DeviceBatch:
         s = abi.CdrSlices(n_slices=info.n_slices, n_rows=info.n_rows, arena_words=info.arena_words)
         s.slice_row0, s.slice_len, s.lane_wf = self.h_row0.ctypes.data, self.h_slen.ctypes.data, \
             self.h_lane.ctypes.data
-        for k, v in self.h_cols.items():
-            setattr(s, k, v.ctypes.data)
+        s.slab = self.h_slab.ctypes.data
         s.arena = self.h_arena.ctypes.data
         s.slice_scratch_off, s.slice_act_slots, s.slice_tim_slots = (
             self.h_sc_off.ctypes.data, self.h_sc_act.ctypes.data, self.h_sc_tim.ctypes.data)
@@ -133,8 +129,7 @@ class DeviceBatch:
         db = abi.CdrDevBatch()
         db.ev.n_slices, db.ev.n_rows, db.ev.arena_words = info.n_slices, info.n_rows, info.arena_words
         db.ev.slice_row0, db.ev.slice_len, db.ev.lane_wf = up(self.h_row0), up(self.h_slen), up(self.h_lane)
-        for k, v in self.h_cols.items():
-            setattr(db.ev, k, up(v))
+        db.ev.slab = up(self.h_slab)
         db.ev.arena = up(self.h_arena)
         db.ev.slice_scratch_off = up(self.h_sc_off)
         db.ev.slice_act_slots = up(self.h_sc_act)
@@ -172,8 +167,8 @@ class DeviceBatch:
         self.out = out
         torch.cuda.synchronize()
         self.h2d_s = time.perf_counter() - t0
-        self.in_bytes = sum(v.nbytes for v in self.h_cols.values()) + self.h_arena.nbytes
-        types = self.h_cols["type_flags"] & 0xFF
+        self.in_bytes = self.h_slab.nbytes + self.h_arena.nbytes
+        types = abi.slab_columns(self.h_slab, self.h_row0, self.h_slen, ("type_flags",))["type_flags"] & 0xFF
         self.type_counts = np.bincount(types, minlength=256)
         self.n_events = int(self.type_counts[:abi.EV["UpsertWorkflowSearchAttributes"] + 1].sum())
 

@@ -178,8 +178,32 @@ CdrOut = _S("cdr_out", [(n, C.c_void_p) for n in (
     "result", "exec", "repl", "vh", "act", "timer", "child", "cancel", "signal", "rp", "sa")])
 CdrSlices = _S("cdr_slices", [
     ("n_slices", u32), ("_pad", u32), ("n_rows", u64), ("arena_words", u64)] + [(n, C.c_void_p) for n in (
-        "slice_row0", "slice_len", "lane_wf", "type_flags", "event_id", "version", "timestamp", "task_id", "key",
-        "aux", "h", "n", "arena", "slice_scratch_off", "slice_act_slots", "slice_tim_slots")])
+        "slice_row0", "slice_len", "lane_wf", "slab", "arena", "slice_scratch_off", "slice_act_slots",
+        "slice_tim_slots")])
+
+# slice-major slab of event columns (cdr.h enum cdr_col): name, dtype, in order
+SLAB_COLS = (("event_id", np.int64), ("version", np.int64), ("timestamp", np.int64), ("task_id", np.int64),
+             ("key", np.int64), ("aux", np.int64), ("type_flags", np.uint32), ("h", np.uint32), ("n", np.int32))
+EL_BYTES = sum(np.dtype(t).itemsize for _, t in SLAB_COLS)  # CDR_EL_BYTES
+SEF_BATCH_FIRST, SEF_DOMAIN_MISSING = 1 << 8, 1 << 9
+
+
+def slab_columns(slab, row0, slen, cols=None):
+    """Columns of a slice-major slab (uint8 array) in global element order: element
+    (row0[s] + k) * 64 + lane of the result is event k of lane `lane` of slice s."""
+    slab = np.asarray(slab).view(np.uint8)
+    want = [c for c in SLAB_COLS if cols is None or c[0] in cols]
+    out = {name: [] for name, _ in want}
+    for r0, ln in zip(np.asarray(row0, np.uint64).tolist(), np.asarray(slen, np.uint32).tolist()):
+        E = int(ln) * SLICE_WIDTH
+        base = int(r0) * SLICE_WIDTH * EL_BYTES
+        off = 0
+        for name, dt in SLAB_COLS:
+            size = np.dtype(dt).itemsize
+            if name in out:
+                out[name].append(slab[base + off * E: base + (off + size) * E].view(dt))
+            off += size
+    return {k: (np.concatenate(v) if v else np.zeros(0, dict(SLAB_COLS)[k])) for k, v in out.items()}
 CdrDevBatch = _S("cdr_dev_batch", [
     ("ev", CdrSlices), ("scratch", C.c_void_p), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
     ("n_wfs", u32), ("empty_uuid", u32), ("max_act_slots", u32), ("max_tim_slots", u32),

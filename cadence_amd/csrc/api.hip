@@ -185,9 +185,7 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   if (rc) return rc;
   const uint64_t ne = rows * CDR_SLICE_WIDTH;
   const uint64_t aw = cdr_plan_arena_words(b);
-  std::vector<uint32_t> tf(ne), hh(ne);
-  std::vector<int64_t> eid(ne), ver(ne), ts(ne), task(ne), key(ne), aux(ne);
-  std::vector<int32_t> nn(ne);
+  std::vector<uint8_t> slab(ne * CDR_EL_BYTES);
   std::vector<uint64_t> arena(aw ? aw : 1);
   cdr_slices hs{};
   hs.n_slices = ns;
@@ -196,15 +194,7 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   hs.slice_row0 = row0.data();
   hs.slice_len = slen.data();
   hs.lane_wf = lane.data();
-  hs.type_flags = tf.data();
-  hs.event_id = eid.data();
-  hs.version = ver.data();
-  hs.timestamp = ts.data();
-  hs.task_id = task.data();
-  hs.key = key.data();
-  hs.aux = aux.data();
-  hs.h = hh.data();
-  hs.n = nn.data();
+  hs.slab = slab.data();
   hs.arena = arena.data();
   rc = cdr_pack_slices(b, &hs, 0);
   if (rc) return rc;
@@ -235,15 +225,7 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   db.ev.slice_row0 = (const uint64_t*)up(row0.data(), ns * 8ull);
   db.ev.slice_len = (const uint32_t*)up(slen.data(), ns * 4ull);
   db.ev.lane_wf = (const int32_t*)up(lane.data(), lane.size() * 4ull);
-  db.ev.type_flags = (const uint32_t*)up(tf.data(), ne * 4);
-  db.ev.event_id = (const int64_t*)up(eid.data(), ne * 8);
-  db.ev.version = (const int64_t*)up(ver.data(), ne * 8);
-  db.ev.timestamp = (const int64_t*)up(ts.data(), ne * 8);
-  db.ev.task_id = (const int64_t*)up(task.data(), ne * 8);
-  db.ev.key = (const int64_t*)up(key.data(), ne * 8);
-  db.ev.aux = (const int64_t*)up(aux.data(), ne * 8);
-  db.ev.h = (const uint32_t*)up(hh.data(), ne * 4);
-  db.ev.n = (const int32_t*)up(nn.data(), ne * 4);
+  db.ev.slab = (const uint8_t*)up(slab.data(), slab.size());
   db.ev.arena = (const uint64_t*)up(arena.data(), arena.size() * 8);
   std::vector<uint64_t> sc_off(ns);
   std::vector<uint32_t> sc_act(ns), sc_tim(ns);

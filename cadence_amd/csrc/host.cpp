@@ -128,18 +128,20 @@ void caps_one(const cdr_event* ev, uint64_t n, cdr_wf_caps* out) {
 
 void pack_lane(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t len, uint32_t l, uint64_t apos,
                const cdr_slices* o) {
-  uint32_t* tf = const_cast<uint32_t*>(o->type_flags);
-  int64_t* eid = const_cast<int64_t*>(o->event_id);
-  int64_t* ver = const_cast<int64_t*>(o->version);
-  int64_t* ts = const_cast<int64_t*>(o->timestamp);
-  int64_t* task = const_cast<int64_t*>(o->task_id);
-  int64_t* key = const_cast<int64_t*>(o->key);
-  int64_t* aux = const_cast<int64_t*>(o->aux);
-  uint32_t* hh = const_cast<uint32_t*>(o->h);
-  int32_t* nn = const_cast<int32_t*>(o->n);
+  uint8_t* blk = const_cast<uint8_t*>(o->slab) + row0 * CDR_SLICE_WIDTH * CDR_EL_BYTES;
+  const uint64_t E = (uint64_t)len * CDR_SLICE_WIDTH;
+  int64_t* eid = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_EVENT_ID, E));
+  int64_t* ver = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_VERSION, E));
+  int64_t* ts = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_TIMESTAMP, E));
+  int64_t* task = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_TASK_ID, E));
+  int64_t* key = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_KEY, E));
+  int64_t* aux = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_AUX, E));
+  uint32_t* tf = reinterpret_cast<uint32_t*>(blk + cdr_col_off(CDR_COL_TYPE_FLAGS, E));
+  uint32_t* hh = reinterpret_cast<uint32_t*>(blk + cdr_col_off(CDR_COL_H, E));
+  int32_t* nn = reinterpret_cast<int32_t*>(blk + cdr_col_off(CDR_COL_N, E));
   uint64_t* arena = const_cast<uint64_t*>(o->arena);
   for (uint32_t k = 0; k < len; k++) {
-    const uint64_t i = (row0 + k) * CDR_SLICE_WIDTH + l;
+    const uint64_t i = (uint64_t)k * CDR_SLICE_WIDTH + l;
     if (k >= n_ev) {
       tf[i] = CDR_EV_PAD;
       eid[i] = ver[i] = ts[i] = task[i] = key[i] = aux[i] = 0;
@@ -252,7 +254,7 @@ void pack_lane(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t len, 
       default:
         break;
     }
-    tf[i] = (e.type & 0xFFu) | flags;
+    tf[i] = cdr_type_flags(e.type, flags);
     eid[i] = e.event_id;
     ver[i] = e.version;
     ts[i] = e.timestamp;

@@ -40,7 +40,7 @@
 #include "cdr/cdr.h"
 
 #ifndef CDR_DEPTH
-#define CDR_DEPTH 2 /* events whose operand loads are in flight beyond the one processed */
+#define CDR_DEPTH 1 /* events whose operand loads are in flight beyond the one processed */
 #endif
 #ifndef CDR_TYPED
 #define CDR_TYPED 1 /* 1: read only the operand columns the event's type needs */
@@ -88,7 +88,8 @@ __device__ __forceinline__ bool transition_ok(int cur, int cur_close, int st, in
 }
 
 // ClusterNameForFailoverVersion (common/cluster/metadata.go:187-203): -1 = no owner
-__device__ __forceinline__ int cluster_for_version(const cdr_cluster_meta& m, int64_t v) {
+template <class M>  // cdr_cluster_meta in any address space
+__device__ __forceinline__ int cluster_for_version(const M& m, int64_t v) {
   if (v == CDR_EMPTY_VERSION) return m.current_cluster;
   int64_t init = v % m.failover_version_increment;
   int r = -1;
@@ -197,45 +198,28 @@ __device__ __forceinline__ int alloc_initiated(const GAS Row* rows, uint32_t& hw
 }
 
 // ---------------------------------------------------------------- event columns
-// Which operand columns each event type reads (bit = cdr_event_type).  Every type
-// reads type_flags, event_id and version (prelude, stateBuilder.go:134-155).
-#define TB(t) (1ull << (t))
-constexpr uint64_t NEED_TS = TB(CDR_EV_WF_STARTED) | TB(CDR_EV_DT_SCHEDULED) | TB(CDR_EV_DT_STARTED) |
-                             TB(CDR_EV_AT_SCHEDULED) | TB(CDR_EV_AT_STARTED) | TB(CDR_EV_TIMER_STARTED);
-constexpr uint64_t NEED_KEY =
-    TB(CDR_EV_DT_STARTED) | TB(CDR_EV_AT_SCHEDULED) | TB(CDR_EV_AT_STARTED) | TB(CDR_EV_AT_COMPLETED) |
-    TB(CDR_EV_AT_FAILED) | TB(CDR_EV_AT_TIMED_OUT) | TB(CDR_EV_AT_CANCELED) | TB(CDR_EV_AT_CANCEL_REQUESTED) |
-    TB(CDR_EV_TIMER_STARTED) | TB(CDR_EV_TIMER_FIRED) | TB(CDR_EV_TIMER_CANCELED) | TB(CDR_EV_CHILD_INITIATED) |
-    TB(CDR_EV_CHILD_STARTED) | TB(CDR_EV_CHILD_START_FAILED) | TB(CDR_EV_CHILD_COMPLETED) |
-    TB(CDR_EV_CHILD_FAILED) | TB(CDR_EV_CHILD_CANCELED) | TB(CDR_EV_CHILD_TIMED_OUT) |
-    TB(CDR_EV_CHILD_TERMINATED) | TB(CDR_EV_RCE_FAILED) | TB(CDR_EV_EXT_CANCEL_REQUESTED) | TB(CDR_EV_SE_FAILED) |
-    TB(CDR_EV_EXT_SIGNALED);
-constexpr uint64_t NEED_AUX = TB(CDR_EV_WF_STARTED) | TB(CDR_EV_DT_SCHEDULED) | TB(CDR_EV_DT_COMPLETED) |
-                              TB(CDR_EV_AT_SCHEDULED) | TB(CDR_EV_TIMER_STARTED) | TB(CDR_EV_CHILD_INITIATED) |
-                              TB(CDR_EV_SE_INITIATED) | TB(CDR_EV_UPSERT_SA);
-constexpr uint64_t NEED_H = TB(CDR_EV_DT_STARTED) | TB(CDR_EV_DT_COMPLETED) | TB(CDR_EV_AT_SCHEDULED) |
-                            TB(CDR_EV_AT_STARTED) | TB(CDR_EV_CHILD_INITIATED) | TB(CDR_EV_CHILD_STARTED) |
-                            TB(CDR_EV_SE_INITIATED) | TB(CDR_EV_UPSERT_SA);
-constexpr uint64_t NEED_N =
-    TB(CDR_EV_DT_SCHEDULED) | TB(CDR_EV_DT_TIMED_OUT) | TB(CDR_EV_AT_SCHEDULED) | TB(CDR_EV_CHILD_INITIATED);
-#undef TB
-
-__device__ __forceinline__ bool needs(uint64_t mask, uint32_t t) { return t < 64 && ((mask >> t) & 1ull); }
-
+// One buffer descriptor per slice (the slice's block of the slab, cdr.h); a column
+// is selected by its uniform start offset (soffset), an element by the lane's byte
+// offset (voffset).  Columns an event's type does not read get bit 31 set in the
+// voffset: past the block, the load returns 0 without touching memory.
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
-struct Cols {  // buffer descriptors of one slice's columns
-  rsrc_t tf, id, ver, ts, key, aux, h, n;
-};
-__device__ __forceinline__ rsrc_t slice_rsrc(const void* col, uint64_t row0, uint32_t rows, uint32_t esz) {
-  const char* p = (const char*)col + row0 * CDR_SLICE_WIDTH * esz;
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(rows * CDR_SLICE_WIDTH * esz), 0x00020000);
-}
-__device__ __forceinline__ int64_t bld64(rsrc_t r, uint32_t off) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+#define OOB_BIT 0x80000000u
+__device__ __forceinline__ int64_t bld64(rsrc_t r, uint32_t voff, uint32_t soff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
   return (int64_t)(((uint64_t)v[1] << 32) | (uint64_t)v[0]);
 }
-__device__ __forceinline__ uint32_t bld32(rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+__device__ __forceinline__ uint32_t bld32(rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+struct Slice {
+  rsrc_t r;
+  uint32_t elems;  // slice_len * 64
+  __device__ __forceinline__ uint32_t col(int c) const { return (uint32_t)cdr_col_off(c, elems); }
+};
+// voffset of element (k, lane) in an 8-byte column (4-byte columns: half of it);
+// OOB_BIT when k is past the lane's history
+__device__ __forceinline__ uint32_t el8(uint32_t k, uint32_t len, uint32_t lane) {
+  return k < len ? (k * CDR_SLICE_WIDTH + lane) * 8u : OOB_BIT;
 }
 
 // one event's operands (cdr.h "operand columns per type"); task_id is read once,
@@ -245,32 +229,31 @@ struct Ev {
   int32_t n;
   int64_t id, ver, ts, key, aux;
 };
-
-__device__ __forceinline__ uint32_t load_tf(const Cols& C, uint32_t k, uint32_t len, uint32_t lane) {
-  return bld32(C.tf, k < len ? (k * CDR_SLICE_WIDTH + lane) * 4u : OOB);
+__device__ __forceinline__ uint32_t load_tf(const Slice& S, uint32_t o8) {
+  return bld32(S.r, (o8 >> 1) | (o8 & OOB_BIT), S.col(CDR_COL_TYPE_FLAGS));
 }
-__device__ __forceinline__ Ev load_ops(const Cols& C, uint32_t k, uint32_t len, uint32_t lane, uint32_t tf) {
-  const bool in = k < len;
-  const uint32_t t = tf & 0xFFu;
-  const uint32_t o4 = in ? (k * CDR_SLICE_WIDTH + lane) * 4u : OOB;
-  const uint32_t o8 = in ? (k * CDR_SLICE_WIDTH + lane) * 8u : OOB;
+// need bit b of tf (CDR_SEF_NEED_*) clear -> OOB_BIT
+__device__ __forceinline__ uint32_t gate(uint32_t off, uint32_t tf, uint32_t bit) {
+  return off | ((tf & bit) ? 0u : OOB_BIT);
+}
+__device__ __forceinline__ Ev load_ops(const Slice& S, uint32_t o8, uint32_t tf) {
+  const uint32_t o4 = (o8 >> 1) | (o8 & OOB_BIT);
   Ev e;
   e.tf = tf;
-  e.id = bld64(C.id, o8);
-  e.ver = bld64(C.ver, o8);
+  e.id = bld64(S.r, o8, S.col(CDR_COL_EVENT_ID));
+  e.ver = bld64(S.r, o8, S.col(CDR_COL_VERSION));
 #if CDR_TYPED
-  e.ts = bld64(C.ts, needs(NEED_TS, t) ? o8 : OOB);
-  e.key = bld64(C.key, needs(NEED_KEY, t) ? o8 : OOB);
-  e.aux = bld64(C.aux, needs(NEED_AUX, t) ? o8 : OOB);
-  e.h = bld32(C.h, needs(NEED_H, t) ? o4 : OOB);
-  e.n = (int32_t)bld32(C.n, needs(NEED_N, t) ? o4 : OOB);
+  e.ts = bld64(S.r, gate(o8, tf, CDR_SEF_NEED_TS), S.col(CDR_COL_TIMESTAMP));
+  e.key = bld64(S.r, gate(o8, tf, CDR_SEF_NEED_KEY), S.col(CDR_COL_KEY));
+  e.aux = bld64(S.r, gate(o8, tf, CDR_SEF_NEED_AUX), S.col(CDR_COL_AUX));
+  e.h = bld32(S.r, gate(o4, tf, CDR_SEF_NEED_H), S.col(CDR_COL_H));
+  e.n = (int32_t)bld32(S.r, gate(o4, tf, CDR_SEF_NEED_N), S.col(CDR_COL_N));
 #else
-  (void)t;
-  e.ts = bld64(C.ts, o8);
-  e.key = bld64(C.key, o8);
-  e.aux = bld64(C.aux, o8);
-  e.h = bld32(C.h, o4);
-  e.n = (int32_t)bld32(C.n, o4);
+  e.ts = bld64(S.r, o8, S.col(CDR_COL_TIMESTAMP));
+  e.key = bld64(S.r, o8, S.col(CDR_COL_KEY));
+  e.aux = bld64(S.r, o8, S.col(CDR_COL_AUX));
+  e.h = bld32(S.r, o4, S.col(CDR_COL_H));
+  e.n = (int32_t)bld32(S.r, o4, S.col(CDR_COL_N));
 #endif
   return e;
 }
@@ -391,54 +374,73 @@ __device__ __forceinline__ void tim_pick(const T& S, uint32_t hw) {
 }  // namespace
 
 // ============================================================== replay kernel
+// Launch parameters.  The kernel reads them through the kernarg segment pointer made
+// opaque at each use (KA()): every field is a fresh scalar load where it is needed,
+// so rarely used parameters (table bases, cluster map, uuid seed ...) do not occupy
+// SGPRs across the replay loop.
+struct cdr_launch {
+  cdr_dev_batch B;
+  cdr_out O;
+  uint32_t la, lt;  // activity / user-timer working slots per lane held in LDS
+};
+#define AS4 __attribute__((address_space(4)))
+__device__ __forceinline__ const AS4 cdr_launch* KA() {
+  const AS4 cdr_launch* p = (const AS4 cdr_launch*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+template <class T>
+__device__ __forceinline__ GAS T* gp(T* p) {
+  return (GAS T*)p;
+}
+template <class T>
+__device__ __forceinline__ const GAS T* gp(const T* p) {
+  return (const GAS T*)p;
+}
+
 // LDS = true: slices whose working slots fit (act_slots <= la, tim_slots <= lt);
 // LDS = false: the rest, with working slots in the global scratch.
 template <bool LDS>
 __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu(CDR_WPE, 8))) void k_replay(
-    cdr_dev_batch B, cdr_out O, uint32_t la, uint32_t lt) {
+    cdr_launch L) {
+  (void)L;  // read through KA()
   const uint32_t s = blockIdx.x;
   const uint32_t lane = threadIdx.x;
-  if (s >= B.ev.n_slices) return;
-  const uint32_t act_cap = B.ev.slice_act_slots[s], tim_cap = B.ev.slice_tim_slots[s];
+  if (s >= KA()->B.ev.n_slices) return;
+  // slice scalars (readfirstlane makes their uniformity visible, so the descriptor
+  // lives in SGPRs and no buffer load needs a waterfall loop)
+  const uint32_t act_cap = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_act_slots[s]);
+  const uint32_t tim_cap = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_tim_slots[s]);
+  const uint32_t la = KA()->la, lt = KA()->lt;
   if ((act_cap <= la && tim_cap <= lt) != LDS) return;
-  const int32_t w = B.ev.lane_wf[(uint64_t)s * CDR_SLICE_WIDTH + lane];
+  const uint64_t row0_ = KA()->B.ev.slice_row0[s];
+  const uint64_t row0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(row0_ >> 32)) << 32) |
+                        __builtin_amdgcn_readfirstlane((uint32_t)row0_);
+  Slice S;
+  S.elems = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_len[s]) * CDR_SLICE_WIDTH;
+  S.r = __builtin_amdgcn_make_buffer_rsrc((void*)(KA()->B.ev.slab + row0 * CDR_SLICE_WIDTH * CDR_EL_BYTES), (short)0,
+                                          (int)(S.elems * CDR_EL_BYTES), 0x00020000);
+  const int32_t w = KA()->B.ev.lane_wf[(uint64_t)s * CDR_SLICE_WIDTH + lane];
   if (w < 0) return;
+
   // per-workflow descriptor, capacities and output records, re-read where used
-#define D (late(B.wfs)[w])
-#define CP (late(B.caps)[w])
-#define X (late(O.exec) + w)
-#define RS (late(O.repl) + w)
+#define B_ (KA()->B)
+#define O_ (KA()->O)
+#define D (gp(B_.wfs)[w])
+#define CP (gp(B_.caps)[w])
+#define X (gp(O_.exec) + w)
+#define RS (gp(O_.repl) + w)
+#define chi (gp(O_.child) + CP.child_off)
+#define can (gp(O_.cancel) + CP.cancel_off)
+#define sig (gp(O_.signal) + CP.signal_off)
+#define vh (gp(O_.vh) + CP.vh_off)
+#define rp (gp(O_.rp) + CP.rp_off)
+#define sa (gp(O_.sa) + CP.sa_off)
   const uint32_t len = (uint32_t)D.ev_len;
   const uint32_t builder = D.builder;
-  const uint32_t EU = B.empty_uuid;
+  const uint32_t EU = B_.empty_uuid;
   const bool isRS = builder == CDR_BUILDER_2DC;
   const bool isVH = builder == CDR_BUILDER_NDC;
-
-  // per-slice column descriptors (wave-uniform)
-  const uint64_t row0 = B.ev.slice_row0[s];
-  const uint32_t srows = B.ev.slice_len[s];
-  Cols C;
-  C.tf = slice_rsrc(B.ev.type_flags, row0, srows, 4);
-  C.id = slice_rsrc(B.ev.event_id, row0, srows, 8);
-  C.ver = slice_rsrc(B.ev.version, row0, srows, 8);
-  C.ts = slice_rsrc(B.ev.timestamp, row0, srows, 8);
-  C.key = slice_rsrc(B.ev.key, row0, srows, 8);
-  C.aux = slice_rsrc(B.ev.aux, row0, srows, 8);
-  C.h = slice_rsrc(B.ev.h, row0, srows, 4);
-  C.n = slice_rsrc(B.ev.n, row0, srows, 4);
-
-#define chi (late(O.child) + CP.child_off)
-#define can (late(O.cancel) + CP.cancel_off)
-#define sig (late(O.signal) + CP.signal_off)
-#define vh (late(O.vh) + CP.vh_off)
-#define rp (late(O.rp) + CP.rp_off)
-#define sa (late(O.sa) + CP.sa_off)
-#define chi_cap (CP.child_cap)
-#define can_cap (CP.cancel_cap)
-#define sig_cap (CP.signal_cap)
-#define vh_cap (CP.vh_cap)
-#define rp_cap (CP.rp_cap)
-#define sa_cap (CP.sa_cap)
 
   // working slots of pending activities / user timers
   typedef typename std::conditional<LDS, LdsSlots<CDR_ACT_PLANES>, GlbSlots<CDR_ACT_PLANES>>::type ASlots;
@@ -449,7 +451,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     A.l = lane;
     T.l = la * CDR_ACT_PLANES * CDR_SLICE_WIDTH + lane;
   } else {
-    GAS uint64_t* g = (GAS uint64_t*)(B.scratch + B.ev.slice_scratch_off[s] + lane);
+    GAS uint64_t* g = gp(B_.scratch + B_.ev.slice_scratch_off[s] + lane);
     A.g = g;
     T.g = g + (uint64_t)act_cap * CDR_ACT_PLANES * CDR_SLICE_WIDTH;
   }
@@ -458,8 +460,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   // ---- ExecutionInfo fields that later events change (registers); the fields only
   // WorkflowExecutionStarted writes go straight to the output record.
   uint32_t x_flags = 0;
-  int64_t x_completion_batch = 0, x_next_event = CDR_FIRST_EVENT_ID,
-          x_last_processed = CDR_EMPTY_EVENT_ID;
+  int64_t x_completion_batch = 0, x_next_event = CDR_FIRST_EVENT_ID, x_last_processed = CDR_EMPTY_EVENT_ID;
   int32_t x_dt_timeout_value = 0, x_state = CDR_STATE_CREATED, x_close = CDR_CLOSE_NONE, x_signals = 0;
   // decision (decisionInfo, mutableStateDecisionTaskManager.go:677-690)
   int64_t dv = CDR_EMPTY_VERSION, dsched = CDR_EMPTY_EVENT_ID, dstart = CDR_EMPTY_EVENT_ID, datt = 0, dst_ts = 0,
@@ -493,26 +494,28 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     stop_at_call_end = true; \
   } while (0)
 
-  // ---- software pipeline: operands CDR_DEPTH events ahead, types two further ahead
+  // ---- software pipeline: operands of event k+CDR_DEPTH and the type of event
+  // k+CDR_DEPTH+2 are issued while event k is processed
+  uint32_t o8 = el8(0, len, lane);  // voffset of event k
 #if CDR_DEPTH == 2
-  Ev q0 = load_ops(C, 0, len, lane, load_tf(C, 0, len, lane));
-  Ev q1 = load_ops(C, 1, len, lane, load_tf(C, 1, len, lane));
-  uint32_t t2 = load_tf(C, 2, len, lane), t3 = load_tf(C, 3, len, lane);
+  Ev q0 = load_ops(S, o8, load_tf(S, o8));
+  Ev q1 = load_ops(S, el8(1, len, lane), load_tf(S, el8(1, len, lane)));
+  uint32_t t2 = load_tf(S, el8(2, len, lane)), t3 = load_tf(S, el8(3, len, lane));
 #else
-  Ev q0 = load_ops(C, 0, len, lane, load_tf(C, 0, len, lane));
-  uint32_t t1 = load_tf(C, 1, len, lane), t2 = load_tf(C, 2, len, lane);
+  Ev q0 = load_ops(S, o8, load_tf(S, o8));
+  uint32_t t1 = load_tf(S, el8(1, len, lane)), t2 = load_tf(S, el8(2, len, lane));
 #endif
   for (uint32_t k = 0; k < len; k++) {
     const Ev e = q0;
 #if CDR_DEPTH == 2
     q0 = q1;
-    const uint32_t t4 = load_tf(C, k + 4, len, lane);
-    q1 = load_ops(C, k + 2, len, lane, t2);
+    const uint32_t t4 = load_tf(S, el8(k + 4, len, lane));
+    q1 = load_ops(S, el8(k + 2, len, lane), t2);
     t2 = t3;
     t3 = t4;
 #else
-    const uint32_t t3 = load_tf(C, k + 3, len, lane);
-    q0 = load_ops(C, k + 1, len, lane, t1);
+    const uint32_t t3 = load_tf(S, el8(k + 3, len, lane));
+    q0 = load_ops(S, el8(k + 1, len, lane), t1);
     t1 = t2;
     t2 = t3;
 #endif
@@ -522,12 +525,12 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
         // ---- end of the previous call: stateBuilder.go:603-604, plus the replication
         // state whose source is the call's last event (mutableStateBuilder.go:561-581)
         if (isRS) {
-          const int src = cluster_for_version(B.cluster, prev_ver);
+          const int src = cluster_for_version(B_.cluster, prev_ver);
           if (src < 0) {  // the panic fires at the call's first event, before anything else
             err = CDR_P_UNKNOWN_CLUSTER;
             err_id = call_first_id;
             err_k = call_first_k;
-          } else if (src != B.cluster.current_cluster) {
+          } else if (src != B_.cluster.current_cluster) {
             RS->lri_version[src] = prev_ver;
             RS->lri_last_event_id[src] = prev_id;
             rs_mask |= 1u << src;
@@ -544,8 +547,9 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     prev_ver = e.ver;
     if (stop_at_call_end) continue;  // rest of a failed call: only its last event matters (2DC)
 
-    // ---- version prelude (stateBuilder.go:134-154)
-    if (isVH) {  // (2DC: UpdateReplicationStateVersion(v, true) leaves CurrentVersion = e.ver)
+    // ---- version prelude (stateBuilder.go:134-154); 2DC: UpdateReplicationStateVersion
+    // (v, true) leaves CurrentVersion = e.ver, read back from prev_ver at the end
+    if (isVH) {
       if (x_state == CDR_STATE_CREATED || x_state == CDR_STATE_RUNNING) curv = e.ver;  // UpdateCurrentVersion
       // NewVersionHistoryItem + AddOrUpdateItem (versionHistory.go:31-42,203-236)
       if (e.id < 0 || (e.ver < 0 && e.ver != CDR_EMPTY_VERSION)) {
@@ -561,7 +565,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
         continue;
       }
       if (n_vh == 0 || e.ver > vh_last_ver) {
-        if (n_vh >= vh_cap) {
+        if (n_vh >= CP.vh_cap) {
           FAIL(CDR_E_BAD_INPUT);
           continue;
         }
@@ -573,518 +577,528 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     }
     // LastEventTaskID (:155) is read once after the loop (last applied event)
 
-    switch (type) {
-      case CDR_EV_WF_STARTED: {  // stateBuilder.go:158-184 -> mutableStateBuilder.go:1639-1716
-        const GAS cdr_attr_wf_started* a = (const GAS cdr_attr_wf_started*)(B.ev.arena + (uint64_t)e.aux);
-        const uint32_t af = a->flags;
-        if ((af & CDR_SF_HAS_PARENT_DOMAIN) && (af & CDR_SF_PARENT_DOMAIN_MISSING)) {
-          FAIL(CDR_E_DOMAIN_NOT_FOUND);
-          break;
-        }
-        if (!transition_ok(x_state, x_close, CDR_STATE_CREATED, CDR_CLOSE_NONE)) {
-          FAIL(CDR_E_INVALID_STATE_TRANSITION);
-          break;
-        }
-        const bool first = !(x_flags & CDR_XI_STARTED);  // fields absent from a first Started stay zero
-        X->domain_id = D.domain_id;
-        X->workflow_id = D.workflow_id;
-        X->run_id = D.run_id;
-        X->create_request_id = D.request_id;
-        X->task_list = a->task_list;
-        X->workflow_type = a->workflow_type;
-        X->workflow_timeout = a->exec_timeout_s;
-        X->cron_schedule = a->cron_schedule;
-        X->attempt = a->attempt;
-        X->initiated_id = (af & CDR_SF_HAS_PARENT_INITIATED) ? a->parent_initiated_id : CDR_EMPTY_EVENT_ID;
-        x_dt_timeout_value = a->task_timeout_s;
-        x_state = CDR_STATE_CREATED;
-        x_close = CDR_CLOSE_NONE;
-        x_last_processed = CDR_EMPTY_EVENT_ID;
-        dv = CDR_EMPTY_VERSION;
-        dsched = CDR_EMPTY_EVENT_ID;
-        dstart = CDR_EMPTY_EVENT_ID;
-        dreq = EU;
-        dto = 0;
-        if (af & CDR_SF_HAS_PARENT_DOMAIN) X->parent_domain_id = a->parent_domain_id;
-        else if (first) X->parent_domain_id = 0;
-        if (af & CDR_SF_HAS_PARENT_EXEC) {
-          X->parent_workflow_id = a->parent_workflow_id;
-          X->parent_run_id = a->parent_run_id;
-        } else if (first) {
-          X->parent_workflow_id = 0;
-          X->parent_run_id = 0;
-        }
-        if (a->expiration_ts != 0) {
-          X->expiration_time = a->expiration_ts;
-          x_flags |= CDR_XI_HAS_EXPIRATION;
-        } else if (first) {
-          X->expiration_time = 0;
-        }
-        if (af & CDR_SF_HAS_RETRY) {
-          x_flags |= CDR_XI_HAS_RETRY;
-          X->backoff_coefficient = a->backoff_coefficient;
-          X->expiration_seconds = a->retry_expiration_s;
-          X->initial_interval = a->retry_initial_s;
-          X->maximum_attempts = a->retry_max_attempts;
-          X->maximum_interval = a->retry_max_interval_s;
-          X->nonretriable = a->nonretriable;
-        } else if (first) {
-          X->backoff_coefficient = 0.0;
-          X->expiration_seconds = 0;
-          X->initial_interval = 0;
-          X->maximum_attempts = 0;
-          X->maximum_interval = 0;
-          X->nonretriable = 0;
-        }
-        // rolloverAutoResetPointsWithExpiringTime (:3184-3205)
-        n_rp = 0;
-        cks_ok = 0;
-        x_flags &= ~CDR_XI_HAS_RESET_POINTS;
-        if (af & CDR_SF_HAS_RESET_POINTS) {
-          x_flags |= CDR_XI_HAS_RESET_POINTS;
-          const int64_t expiring = e.ts + (int64_t)D.retention_days * 24ll * 3600ll * NS_PER_S;
-          const uint32_t crun = a->continued_run_id, off = a->reset_points_off, cnt = a->reset_points_len;
-          for (uint32_t q = 0; q < cnt && q < rp_cap; q++) {
-            cdr_reset_point p = gget((const GAS cdr_reset_point*)B.rps + (off + q));
-            const uint32_t run = (p.flags & CDR_RP_HAS_RUN_ID) ? p.run_id : 0u;
-            if (run == crun) {
-              p.flags |= CDR_RP_HAS_EXPIRING;
-              p.expiring_time_nano = expiring;
+    // ---- dispatch (stateBuilder.go:157-600): one pass per distinct event type in
+    // the wave, each with a wave-uniform type, so the switch is a scalar branch tree
+    // and a pass executes only its own case
+    for (bool todo = true; todo;) {
+      const uint32_t ut = __builtin_amdgcn_readfirstlane(type);
+      if (type != ut) continue;
+      todo = false;
+      switch (ut) {
+        case CDR_EV_WF_STARTED: {  // stateBuilder.go:158-184 -> mutableStateBuilder.go:1639-1716
+          const GAS cdr_attr_wf_started* a = gp((const cdr_attr_wf_started*)(B_.ev.arena + (uint64_t)e.aux));
+          const uint32_t af = a->flags;
+          if ((af & CDR_SF_HAS_PARENT_DOMAIN) && (af & CDR_SF_PARENT_DOMAIN_MISSING)) {
+            FAIL(CDR_E_DOMAIN_NOT_FOUND);
+            break;
+          }
+          if (!transition_ok(x_state, x_close, CDR_STATE_CREATED, CDR_CLOSE_NONE)) {
+            FAIL(CDR_E_INVALID_STATE_TRANSITION);
+            break;
+          }
+          const bool first = !(x_flags & CDR_XI_STARTED);  // fields absent from a first Started stay zero
+          X->domain_id = D.domain_id;
+          X->workflow_id = D.workflow_id;
+          X->run_id = D.run_id;
+          X->create_request_id = D.request_id;
+          X->task_list = a->task_list;
+          X->workflow_type = a->workflow_type;
+          X->workflow_timeout = a->exec_timeout_s;
+          X->cron_schedule = a->cron_schedule;
+          X->attempt = a->attempt;
+          X->initiated_id = (af & CDR_SF_HAS_PARENT_INITIATED) ? a->parent_initiated_id : CDR_EMPTY_EVENT_ID;
+          x_dt_timeout_value = a->task_timeout_s;
+          x_state = CDR_STATE_CREATED;
+          x_close = CDR_CLOSE_NONE;
+          x_last_processed = CDR_EMPTY_EVENT_ID;
+          dv = CDR_EMPTY_VERSION;
+          dsched = CDR_EMPTY_EVENT_ID;
+          dstart = CDR_EMPTY_EVENT_ID;
+          dreq = EU;
+          dto = 0;
+          if (af & CDR_SF_HAS_PARENT_DOMAIN) X->parent_domain_id = a->parent_domain_id;
+          else if (first) X->parent_domain_id = 0;
+          if (af & CDR_SF_HAS_PARENT_EXEC) {
+            X->parent_workflow_id = a->parent_workflow_id;
+            X->parent_run_id = a->parent_run_id;
+          } else if (first) {
+            X->parent_workflow_id = 0;
+            X->parent_run_id = 0;
+          }
+          if (a->expiration_ts != 0) {
+            X->expiration_time = a->expiration_ts;
+            x_flags |= CDR_XI_HAS_EXPIRATION;
+          } else if (first) {
+            X->expiration_time = 0;
+          }
+          if (af & CDR_SF_HAS_RETRY) {
+            x_flags |= CDR_XI_HAS_RETRY;
+            X->backoff_coefficient = a->backoff_coefficient;
+            X->expiration_seconds = a->retry_expiration_s;
+            X->initial_interval = a->retry_initial_s;
+            X->maximum_attempts = a->retry_max_attempts;
+            X->maximum_interval = a->retry_max_interval_s;
+            X->nonretriable = a->nonretriable;
+          } else if (first) {
+            X->backoff_coefficient = 0.0;
+            X->expiration_seconds = 0;
+            X->initial_interval = 0;
+            X->maximum_attempts = 0;
+            X->maximum_interval = 0;
+            X->nonretriable = 0;
+          }
+          // rolloverAutoResetPointsWithExpiringTime (:3184-3205)
+          n_rp = 0;
+          cks_ok = 0;
+          x_flags &= ~CDR_XI_HAS_RESET_POINTS;
+          if (af & CDR_SF_HAS_RESET_POINTS) {
+            x_flags |= CDR_XI_HAS_RESET_POINTS;
+            const int64_t expiring = e.ts + (int64_t)D.retention_days * 24ll * 3600ll * NS_PER_S;
+            const uint32_t crun = a->continued_run_id, off = a->reset_points_off, cnt = a->reset_points_len;
+            for (uint32_t q = 0; q < cnt && q < CP.rp_cap; q++) {
+              cdr_reset_point p = gget(gp(B_.rps) + (off + q));
+              const uint32_t run = (p.flags & CDR_RP_HAS_RUN_ID) ? p.run_id : 0u;
+              if (run == crun) {
+                p.flags |= CDR_RP_HAS_EXPIRING;
+                p.expiring_time_nano = expiring;
+              }
+              gput(rp + n_rp++, p);
             }
-            gput(rp + n_rp++, p);
           }
-        }
-        if (af & CDR_SF_HAS_MEMO) {
-          x_flags |= CDR_XI_HAS_MEMO;
-          X->memo = a->memo;
-        } else if (first) {
-          X->memo = 0;
-        }
-        if (af & CDR_SF_HAS_SEARCH_ATTR) {
-          n_sa = 0;
-          const uint32_t off = a->search_attr_off, cnt = a->search_attr_len;
-          for (uint32_t q = 0; q < cnt && q < sa_cap; q++) gput(sa + n_sa++, gget((const GAS cdr_kv*)B.kvs + (off + q)));
-          if (n_sa) x_flags |= CDR_XI_HAS_SEARCH_ATTR;
-          else x_flags &= ~CDR_XI_HAS_SEARCH_ATTR;
-        }
-        x_flags |= CDR_XI_STARTED;
-        // SetHistoryTree (:313-339): branch token on ExecutionInfo, or on the VH for NDC
-        uint64_t lo, hi;
-        cdr_uuid(B.uuid_seed, D.wf_key, CDR_UUID_BRANCH, e.id, &lo, &hi);
-        X->branch_tree_id = D.run_id;
-        X->branch_id_lo = lo;
-        X->branch_id_hi = hi;
-        x_flags |= isVH ? CDR_XI_VH_BRANCH : CDR_XI_HAS_BRANCH;
-        if (isRS) RS->start_version = e.ver;  // :182-184
-        break;
-      }
-      case CDR_EV_DT_SCHEDULED:  // :186-200 -> mutableStateDecisionTaskManager.go:143-167
-        dv = e.ver;
-        dsched = e.id;
-        dstart = CDR_EMPTY_EVENT_ID;
-        dreq = EU;
-        dto = e.n;
-        datt = e.aux;
-        dsc_ts = e.ts;
-        dst_ts = 0;
-        dorig_ts = e.ts;
-        break;
-      case CDR_EV_DT_STARTED:  // :202-213 -> :200-253
-        if (e.key != dsched) {
-          FAIL(CDR_E_DECISION_NOT_FOUND);
+          if (af & CDR_SF_HAS_MEMO) {
+            x_flags |= CDR_XI_HAS_MEMO;
+            X->memo = a->memo;
+          } else if (first) {
+            X->memo = 0;
+          }
+          if (af & CDR_SF_HAS_SEARCH_ATTR) {
+            n_sa = 0;
+            const uint32_t off = a->search_attr_off, cnt = a->search_attr_len;
+            for (uint32_t q = 0; q < cnt && q < CP.sa_cap; q++) gput(sa + n_sa++, gget(gp(B_.kvs) + (off + q)));
+            if (n_sa) x_flags |= CDR_XI_HAS_SEARCH_ATTR;
+            else x_flags &= ~CDR_XI_HAS_SEARCH_ATTR;
+          }
+          x_flags |= CDR_XI_STARTED;
+          // SetHistoryTree (:313-339): branch token on ExecutionInfo, or on the VH for NDC
+          uint64_t lo, hi;
+          cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_BRANCH, e.id, &lo, &hi);
+          X->branch_tree_id = D.run_id;
+          X->branch_id_lo = lo;
+          X->branch_id_hi = hi;
+          x_flags |= isVH ? CDR_XI_VH_BRANCH : CDR_XI_HAS_BRANCH;
+          if (isRS) RS->start_version = e.ver;  // :182-184
           break;
         }
-        if (x_state == CDR_STATE_CREATED) x_state = CDR_STATE_RUNNING;  // always accepted (:56-60)
-        dv = e.ver;
-        dstart = e.id;
-        dreq = e.h;
-        datt = 0;
-        dst_ts = e.ts;
-        break;
-      case CDR_EV_DT_COMPLETED: {  // :215-219 -> :255-262,659-674,789-800
-        dv = CDR_EMPTY_VERSION;
-        dsched = CDR_EMPTY_EVENT_ID;
-        dstart = CDR_EMPTY_EVENT_ID;
-        dreq = EU;
-        dto = 0;
-        datt = 0;
-        dst_ts = 0;
-        dsc_ts = 0;  // OriginalScheduledTimestamp kept
-        x_last_processed = e.aux;
-        const uint32_t cks = e.h;
-        if (cks && cks != cks_ok) {  // addBinaryCheckSumIfNotExists (mutableStateBuilder.go:1798-1842)
-          bool exists = false;
-          for (uint32_t q = 0; q < n_rp; q++) {
-            const cdr_reset_point p = gget(rp + q);
-            exists |= ((p.flags & CDR_RP_HAS_CHECKSUM) ? p.binary_checksum : 0u) == cks;
+        case CDR_EV_DT_SCHEDULED:  // :186-200 -> mutableStateDecisionTaskManager.go:143-167
+          dv = e.ver;
+          dsched = e.id;
+          dstart = CDR_EMPTY_EVENT_ID;
+          dreq = EU;
+          dto = e.n;
+          datt = e.aux;
+          dsc_ts = e.ts;
+          dst_ts = 0;
+          dorig_ts = e.ts;
+          break;
+        case CDR_EV_DT_STARTED:  // :202-213 -> :200-253
+          if (e.key != dsched) {
+            FAIL(CDR_E_DECISION_NOT_FOUND);
+            break;
           }
-          if (!exists) {
-            if (n_rp >= rp_cap) {
+          if (x_state == CDR_STATE_CREATED) x_state = CDR_STATE_RUNNING;  // always accepted (:56-60)
+          dv = e.ver;
+          dstart = e.id;
+          dreq = e.h;
+          datt = 0;
+          dst_ts = e.ts;
+          break;
+        case CDR_EV_DT_COMPLETED: {  // :215-219 -> :255-262,659-674,789-800
+          dv = CDR_EMPTY_VERSION;
+          dsched = CDR_EMPTY_EVENT_ID;
+          dstart = CDR_EMPTY_EVENT_ID;
+          dreq = EU;
+          dto = 0;
+          datt = 0;
+          dst_ts = 0;
+          dsc_ts = 0;  // OriginalScheduledTimestamp kept
+          x_last_processed = e.aux;
+          const uint32_t cks = e.h;
+          if (cks && cks != cks_ok) {  // addBinaryCheckSumIfNotExists (mutableStateBuilder.go:1798-1842)
+            bool exists = false;
+            for (uint32_t q = 0; q < n_rp; q++) {
+              const cdr_reset_point p = gget(rp + q);
+              exists |= ((p.flags & CDR_RP_HAS_CHECKSUM) ? p.binary_checksum : 0u) == cks;
+            }
+            if (!exists) {
+              if (n_rp >= CP.rp_cap) {
+                FAIL(CDR_E_BAD_INPUT);
+                break;
+              }
+              const bool resettable = live_chi == 0 && live_can == 0 && live_sig == 0;
+              cdr_reset_point p;
+              p.binary_checksum = cks;
+              p.run_id = D.run_id;
+              p.first_decision_completed_id = e.id;
+              p.created_time_nano = B_.now_ns;
+              p.expiring_time_nano = 0;
+              p.flags = CDR_RP_HAS_CHECKSUM | CDR_RP_HAS_RUN_ID | CDR_RP_HAS_FIRST_DC_ID | CDR_RP_HAS_CREATED |
+                        CDR_RP_HAS_RESETTABLE | (resettable ? CDR_RP_RESETTABLE : 0u);
+              p._pad = 0;
+              gput(rp + n_rp++, p);
+              x_flags |= CDR_XI_HAS_RESET_POINTS;
+            }
+            cks_ok = cks;  // the list only grows until the next WorkflowExecutionStarted
+          }
+          break;
+        }
+        case CDR_EV_DT_TIMED_OUT:  // :221-239 -> FailDecision :635-656 + transient :169-198
+        case CDR_EV_DT_FAILED: {   // :241-257
+          const bool inc = type == CDR_EV_DT_FAILED || e.n != CDR_TIMEOUT_SCHEDULE_TO_START;
+          const int64_t now = B_.now_ns;
+          datt = inc ? datt + 1 : 0;
+          dv = CDR_EMPTY_VERSION;
+          dsched = CDR_EMPTY_EVENT_ID;
+          dstart = CDR_EMPTY_EVENT_ID;
+          dreq = EU;
+          dto = 0;
+          dst_ts = 0;
+          dorig_ts = 0;
+          dsc_ts = inc ? now : 0;
+          if (datt != 0) {  // transient decision: no decision is pending here by construction
+            dv = isRS ? e.ver : (isVH ? curv : CDR_EMPTY_VERSION);
+            dsched = x_next_event;  // NextEventID as of the call's start
+            dto = x_dt_timeout_value;
+            dsc_ts = now;
+          }
+          break;
+        }
+        case CDR_EV_AT_SCHEDULED: {  // :259-269 -> mutableStateBuilder.go:1982-2028
+          const uint32_t aid = (uint32_t)e.key;
+          int slot = -1;
+          for (uint32_t j = 0; j < hw_act; j++) {
+            if (A.ld(j, AP_SID) == DEAD_KEY) {
+              if (slot < 0) slot = (int)j;
+            } else {
+              const uint64_t m = (uint64_t)A.ld(j, AP_META);
+              if ((uint32_t)m == aid && (m & META_FLAG(AF_AIDMAP)))  // byActivityID[aid] is overwritten
+                A.st(j, AP_META, (int64_t)(m & ~META_FLAG(AF_AIDMAP)));
+            }
+          }
+          if (slot < 0) {
+            if (hw_act >= act_cap) {
               FAIL(CDR_E_BAD_INPUT);
               break;
             }
-            const bool resettable = live_chi == 0 && live_can == 0 && live_sig == 0;
-            cdr_reset_point p;
-            p.binary_checksum = cks;
-            p.run_id = D.run_id;
-            p.first_decision_completed_id = e.id;
-            p.created_time_nano = B.now_ns;
-            p.expiring_time_nano = 0;
-            p.flags = CDR_RP_HAS_CHECKSUM | CDR_RP_HAS_RUN_ID | CDR_RP_HAS_FIRST_DC_ID | CDR_RP_HAS_CREATED |
-                      CDR_RP_HAS_RESETTABLE | (resettable ? CDR_RP_RESETTABLE : 0u);
-            p._pad = 0;
-            gput(rp + n_rp++, p);
-            x_flags |= CDR_XI_HAS_RESET_POINTS;
+            slot = (int)hw_act++;
           }
-          cks_ok = cks;  // the list only grows until the next WorkflowExecutionStarted
+          const uint32_t j = (uint32_t)slot;
+          const int32_t s2c = (int32_t)e.h, s2s = e.n;
+          A.st(j, AP_SID, e.id);
+          A.st(j, AP_TS2C, e.ts + (int64_t)s2c * NS_PER_S);
+          A.st(j, AP_TALT, e.ts + (int64_t)s2s * NS_PER_S);
+          A.st(j, AP_THB, T_NONE);
+          A.st(j, AP_META, (int64_t)(aid | META_FLAG(AF_AIDMAP)));
+          A.st(j, AP_VER, e.ver);
+          A.st(j, AP_STARTED_ID, CDR_EMPTY_EVENT_ID);
+          A.st(j, AP_STARTED_TIME, 0);
+          A.st(j, AP_CANCEL_ID, CDR_EMPTY_EVENT_ID);
+          A.st(j, AP_ROWS, (int64_t)(k | ((uint64_t)call_first_k << 32)));
+          A.st(j, AP_STC_HB, (int64_t)(((uint64_t)e.key >> 32) | ((uint64_t)e.aux & 0xFFFFFFFF00000000ull)));
+          A.st(j, AP_REQ, 0);
+          act_pick(A, hw_act);
+          break;
         }
-        break;
-      }
-      case CDR_EV_DT_TIMED_OUT:  // :221-239 -> FailDecision :635-656 + transient :169-198
-      case CDR_EV_DT_FAILED: {   // :241-257
-        const bool inc = type == CDR_EV_DT_FAILED || e.n != CDR_TIMEOUT_SCHEDULE_TO_START;
-        datt = inc ? datt + 1 : 0;
-        dv = CDR_EMPTY_VERSION;
-        dsched = CDR_EMPTY_EVENT_ID;
-        dstart = CDR_EMPTY_EVENT_ID;
-        dreq = EU;
-        dto = 0;
-        dst_ts = 0;
-        dorig_ts = 0;
-        dsc_ts = inc ? B.now_ns : 0;
-        if (datt != 0) {  // transient decision: no decision is pending here by construction
-          dv = isRS ? e.ver : (isVH ? curv : CDR_EMPTY_VERSION);
-          dsched = x_next_event;  // NextEventID as of the call's start
-          dto = x_dt_timeout_value;
-          dsc_ts = B.now_ns;
-        }
-        break;
-      }
-      case CDR_EV_AT_SCHEDULED: {  // :259-269 -> mutableStateBuilder.go:1982-2028
-        const uint32_t aid = (uint32_t)e.key;
-        int slot = -1;
-        for (uint32_t j = 0; j < hw_act; j++) {
-          if (A.ld(j, AP_SID) == DEAD_KEY) {
-            if (slot < 0) slot = (int)j;
-          } else {
-            const uint64_t m = (uint64_t)A.ld(j, AP_META);
-            if ((uint32_t)m == aid && (m & META_FLAG(AF_AIDMAP)))  // byActivityID[aid] is overwritten
-              A.st(j, AP_META, (int64_t)(m & ~META_FLAG(AF_AIDMAP)));
-          }
-        }
-        if (slot < 0) {
-          if (hw_act >= act_cap) {
-            FAIL(CDR_E_BAD_INPUT);
+        case CDR_EV_AT_STARTED: {  // :271-278 -> :2083-2098
+          int slot = -1;
+          for (uint32_t j = 0; j < hw_act; j++)
+            if (A.ld(j, AP_SID) == e.key) slot = (int)j;
+          if (slot < 0) {
+            FAIL(CDR_P_ACTIVITY_STARTED_NIL);  // nil deref in Go
             break;
           }
-          slot = (int)hw_act++;
-        }
-        const uint32_t j = (uint32_t)slot;
-        const int32_t s2c = (int32_t)e.h, s2s = e.n;
-        A.st(j, AP_SID, e.id);
-        A.st(j, AP_TS2C, e.ts + (int64_t)s2c * NS_PER_S);
-        A.st(j, AP_TALT, e.ts + (int64_t)s2s * NS_PER_S);
-        A.st(j, AP_THB, T_NONE);
-        A.st(j, AP_META, (int64_t)(aid | META_FLAG(AF_AIDMAP)));
-        A.st(j, AP_VER, e.ver);
-        A.st(j, AP_STARTED_ID, CDR_EMPTY_EVENT_ID);
-        A.st(j, AP_STARTED_TIME, 0);
-        A.st(j, AP_CANCEL_ID, CDR_EMPTY_EVENT_ID);
-        A.st(j, AP_ROWS, (int64_t)(k | ((uint64_t)call_first_k << 32)));
-        A.st(j, AP_STC_HB, (int64_t)(((uint64_t)e.key >> 32) | ((uint64_t)e.aux & 0xFFFFFFFF00000000ull)));
-        A.st(j, AP_REQ, 0);
-        act_pick(A, hw_act);
-        break;
-      }
-      case CDR_EV_AT_STARTED: {  // :271-278 -> :2083-2098
-        int slot = -1;
-        for (uint32_t j = 0; j < hw_act; j++)
-          if (A.ld(j, AP_SID) == e.key) slot = (int)j;
-        if (slot < 0) {
-          FAIL(CDR_P_ACTIVITY_STARTED_NIL);  // nil deref in Go
+          const uint32_t j = (uint32_t)slot;
+          const uint64_t th = (uint64_t)A.ld(j, AP_STC_HB);
+          const int32_t stc = (int32_t)(uint32_t)th, hb = (int32_t)(uint32_t)(th >> 32);
+          A.st(j, AP_VER, e.ver);
+          A.st(j, AP_STARTED_ID, e.id);
+          A.st(j, AP_REQ, (int64_t)e.h);
+          A.st(j, AP_STARTED_TIME, e.ts);  // LastHeartBeatUpdatedTime = StartedTime
+          A.st(j, AP_META, (int64_t)((uint64_t)A.ld(j, AP_META) | META_FLAG(AF_STARTED)));
+          A.st(j, AP_TALT, e.ts + (int64_t)stc * NS_PER_S);
+          A.st(j, AP_THB, hb > 0 ? e.ts + (int64_t)hb * NS_PER_S : T_NONE);
+          act_pick(A, hw_act);
           break;
         }
-        const uint32_t j = (uint32_t)slot;
-        const uint64_t th = (uint64_t)A.ld(j, AP_STC_HB);
-        const int32_t stc = (int32_t)(uint32_t)th, hb = (int32_t)(uint32_t)(th >> 32);
-        A.st(j, AP_VER, e.ver);
-        A.st(j, AP_STARTED_ID, e.id);
-        A.st(j, AP_REQ, (int64_t)e.h);
-        A.st(j, AP_STARTED_TIME, e.ts);  // LastHeartBeatUpdatedTime = StartedTime
-        A.st(j, AP_META, (int64_t)((uint64_t)A.ld(j, AP_META) | META_FLAG(AF_STARTED)));
-        A.st(j, AP_TALT, e.ts + (int64_t)stc * NS_PER_S);
-        A.st(j, AP_THB, hb > 0 ? e.ts + (int64_t)hb * NS_PER_S : T_NONE);
-        act_pick(A, hw_act);
-        break;
-      }
-      case CDR_EV_AT_COMPLETED:  // :280-305,312-319 -> DeleteActivity :1247-1269
-      case CDR_EV_AT_FAILED:
-      case CDR_EV_AT_TIMED_OUT:
-      case CDR_EV_AT_CANCELED: {
-        int slot = -1;
-        for (uint32_t j = 0; j < hw_act; j++)
-          if (A.ld(j, AP_SID) == e.key) slot = (int)j;
-        if (slot < 0) {
-          FAIL(CDR_E_ACTIVITY_NOT_FOUND);
+        case CDR_EV_AT_COMPLETED:  // :280-305,312-319 -> DeleteActivity :1247-1269
+        case CDR_EV_AT_FAILED:
+        case CDR_EV_AT_TIMED_OUT:
+        case CDR_EV_AT_CANCELED: {
+          int slot = -1;
+          for (uint32_t j = 0; j < hw_act; j++)
+            if (A.ld(j, AP_SID) == e.key) slot = (int)j;
+          if (slot < 0) {
+            FAIL(CDR_E_ACTIVITY_NOT_FOUND);
+            break;
+          }
+          const uint64_t m = (uint64_t)A.ld((uint32_t)slot, AP_META);
+          const uint32_t aid = (uint32_t)m;
+          A.st((uint32_t)slot, AP_SID, DEAD_KEY);
+          A.st((uint32_t)slot, AP_META, (int64_t)(m & ~META_FLAG(AF_AIDMAP)));
+          bool found = (m & META_FLAG(AF_AIDMAP)) != 0;
+          if (!found)
+            for (uint32_t j = 0; j < hw_act; j++) {
+              if (A.ld(j, AP_SID) == DEAD_KEY) continue;
+              const uint64_t mj = (uint64_t)A.ld(j, AP_META);
+              if ((uint32_t)mj == aid && (mj & META_FLAG(AF_AIDMAP))) {
+                A.st(j, AP_META, (int64_t)(mj & ~META_FLAG(AF_AIDMAP)));
+                found = true;
+              }
+            }
+          if (!found) {
+            FAIL(CDR_E_ACTIVITY_ID_NOT_FOUND);
+            break;
+          }
+          act_pick(A, hw_act);
           break;
         }
-        const uint64_t m = (uint64_t)A.ld((uint32_t)slot, AP_META);
-        const uint32_t aid = (uint32_t)m;
-        A.st((uint32_t)slot, AP_SID, DEAD_KEY);
-        A.st((uint32_t)slot, AP_META, (int64_t)(m & ~META_FLAG(AF_AIDMAP)));
-        bool found = (m & META_FLAG(AF_AIDMAP)) != 0;
-        if (!found)
+        case CDR_EV_AT_CANCEL_REQUESTED: {  // :307-310 -> :2264-2285
+          const uint32_t aid = (uint32_t)e.key;
+          int slot = -1;
           for (uint32_t j = 0; j < hw_act; j++) {
             if (A.ld(j, AP_SID) == DEAD_KEY) continue;
             const uint64_t mj = (uint64_t)A.ld(j, AP_META);
-            if ((uint32_t)mj == aid && (mj & META_FLAG(AF_AIDMAP))) {
-              A.st(j, AP_META, (int64_t)(mj & ~META_FLAG(AF_AIDMAP)));
-              found = true;
+            if ((uint32_t)mj == aid && (mj & META_FLAG(AF_AIDMAP))) slot = (int)j;
+          }
+          if (slot < 0) {
+            FAIL(CDR_E_MISSING_ACTIVITY_INFO);
+            break;
+          }
+          const uint32_t j = (uint32_t)slot;
+          A.st(j, AP_VER, e.ver);
+          A.st(j, AP_META, (int64_t)((uint64_t)A.ld(j, AP_META) | META_FLAG(AF_CANCEL)));
+          A.st(j, AP_CANCEL_ID, e.id);
+          break;
+        }
+        case CDR_EV_TIMER_STARTED: {  // :324-332 -> :2877-2900
+          const uint32_t tid = (uint32_t)e.key;
+          int slot = -1, free_slot = -1;
+          for (uint32_t j = 0; j < hw_tim; j++) {
+            if (T.ld(j, TP_SID) == DEAD_KEY) {
+              if (free_slot < 0) free_slot = (int)j;
+            } else if ((uint32_t)T.ld(j, TP_TID_TASK) == tid) {
+              slot = (int)j;
             }
           }
-        if (!found) {
-          FAIL(CDR_E_ACTIVITY_ID_NOT_FOUND);
-          break;
-        }
-        act_pick(A, hw_act);
-        break;
-      }
-      case CDR_EV_AT_CANCEL_REQUESTED: {  // :307-310 -> :2264-2285
-        const uint32_t aid = (uint32_t)e.key;
-        int slot = -1;
-        for (uint32_t j = 0; j < hw_act; j++) {
-          if (A.ld(j, AP_SID) == DEAD_KEY) continue;
-          const uint64_t mj = (uint64_t)A.ld(j, AP_META);
-          if ((uint32_t)mj == aid && (mj & META_FLAG(AF_AIDMAP))) slot = (int)j;
-        }
-        if (slot < 0) {
-          FAIL(CDR_E_MISSING_ACTIVITY_INFO);
-          break;
-        }
-        const uint32_t j = (uint32_t)slot;
-        A.st(j, AP_VER, e.ver);
-        A.st(j, AP_META, (int64_t)((uint64_t)A.ld(j, AP_META) | META_FLAG(AF_CANCEL)));
-        A.st(j, AP_CANCEL_ID, e.id);
-        break;
-      }
-      case CDR_EV_TIMER_STARTED: {  // :324-332 -> :2877-2900
-        const uint32_t tid = (uint32_t)e.key;
-        int slot = -1, free_slot = -1;
-        for (uint32_t j = 0; j < hw_tim; j++) {
-          if (T.ld(j, TP_SID) == DEAD_KEY) {
-            if (free_slot < 0) free_slot = (int)j;
-          } else if ((uint32_t)T.ld(j, TP_TID_TASK) == tid) {
-            slot = (int)j;
+          if (slot < 0) slot = free_slot;
+          if (slot < 0) {
+            if (hw_tim >= tim_cap) {
+              FAIL(CDR_E_BAD_INPUT);
+              break;
+            }
+            slot = (int)hw_tim++;
           }
+          const uint32_t j = (uint32_t)slot;
+          T.st(j, TP_SID, e.id);
+          T.st(j, TP_TID_TASK, (int64_t)tid);  // TaskID = TimerTaskStatusNone
+          T.st(j, TP_EXPIRY, e.ts + e.aux * NS_PER_S);
+          T.st(j, TP_VER, e.ver);
+          tim_pick(T, hw_tim);
+          break;
         }
-        if (slot < 0) slot = free_slot;
-        if (slot < 0) {
-          if (hw_tim >= tim_cap) {
+        case CDR_EV_TIMER_FIRED:       // :334-341
+        case CDR_EV_TIMER_CANCELED: {  // :343-350
+          const uint32_t tid = (uint32_t)e.key;
+          for (uint32_t j = 0; j < hw_tim; j++)
+            if (T.ld(j, TP_SID) != DEAD_KEY && (uint32_t)T.ld(j, TP_TID_TASK) == tid) T.st(j, TP_SID, DEAD_KEY);
+          tim_pick(T, hw_tim);
+          break;
+        }
+        case CDR_EV_CHILD_INITIATED: {  // :355-371 -> :3256-3280
+          const int slot = alloc_initiated(chi, hw_chi, CP.child_cap);
+          if (slot < 0) {
             FAIL(CDR_E_BAD_INPUT);
             break;
           }
-          slot = (int)hw_tim++;
-        }
-        const uint32_t j = (uint32_t)slot;
-        T.st(j, TP_SID, e.id);
-        T.st(j, TP_TID_TASK, (int64_t)tid);  // TaskID = TimerTaskStatusNone
-        T.st(j, TP_EXPIRY, e.ts + e.aux * NS_PER_S);
-        T.st(j, TP_VER, e.ver);
-        tim_pick(T, hw_tim);
-        break;
-      }
-      case CDR_EV_TIMER_FIRED:       // :334-341
-      case CDR_EV_TIMER_CANCELED: {  // :343-350
-        const uint32_t tid = (uint32_t)e.key;
-        for (uint32_t j = 0; j < hw_tim; j++)
-          if (T.ld(j, TP_SID) != DEAD_KEY && (uint32_t)T.ld(j, TP_TID_TASK) == tid) T.st(j, TP_SID, DEAD_KEY);
-        tim_pick(T, hw_tim);
-        break;
-      }
-      case CDR_EV_CHILD_INITIATED: {  // :355-371 -> :3256-3280
-        const int slot = alloc_initiated(chi, hw_chi, chi_cap);
-        if (slot < 0) {
-          FAIL(CDR_E_BAD_INPUT);
+          cdr_child_info c;
+          c.version = e.ver;
+          c.initiated_id = e.id;
+          c.initiated_event_batch_id = call_first_id;
+          c.started_id = CDR_EMPTY_EVENT_ID;
+          uint64_t lo, hi;
+          cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_CHILD_REQ, e.id, &lo, &hi);
+          c.create_request_lo = lo;
+          c.create_request_hi = hi;
+          c.started_workflow_id = e.h;
+          c.started_run_id = 0;
+          c.domain_name = (uint32_t)e.key;
+          c.workflow_type = (uint32_t)e.aux;
+          c.parent_close_policy = e.n;
+          c._pad = 0;
+          gput(chi + slot, c);
+          live_chi++;
+          if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
           break;
         }
-        cdr_child_info c;
-        c.version = e.ver;
-        c.initiated_id = e.id;
-        c.initiated_event_batch_id = call_first_id;
-        c.started_id = CDR_EMPTY_EVENT_ID;
-        uint64_t lo, hi;
-        cdr_uuid(B.uuid_seed, D.wf_key, CDR_UUID_CHILD_REQ, e.id, &lo, &hi);
-        c.create_request_lo = lo;
-        c.create_request_hi = hi;
-        c.started_workflow_id = e.h;
-        c.started_run_id = 0;
-        c.domain_name = (uint32_t)e.key;
-        c.workflow_type = (uint32_t)e.aux;
-        c.parent_close_policy = e.n;
-        c._pad = 0;
-        gput(chi + slot, c);
-        live_chi++;
-        if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
-        break;
-      }
-      case CDR_EV_CHILD_STARTED: {  // :378-381 -> :3312-3325
-        const int slot = find_initiated(chi, hw_chi, e.key);
-        if (slot < 0) {
-          FAIL(CDR_P_CHILD_STARTED_NIL);
+        case CDR_EV_CHILD_STARTED: {  // :378-381 -> :3312-3325
+          const int slot = find_initiated(chi, hw_chi, e.key);
+          if (slot < 0) {
+            FAIL(CDR_P_CHILD_STARTED_NIL);
+            break;
+          }
+          chi[slot].started_id = e.id;
+          chi[slot].started_run_id = e.h;
           break;
         }
-        chi[slot].started_id = e.id;
-        chi[slot].started_run_id = e.h;
-        break;
-      }
-      case CDR_EV_CHILD_START_FAILED:
-      case CDR_EV_CHILD_COMPLETED:
-      case CDR_EV_CHILD_FAILED:
-      case CDR_EV_CHILD_CANCELED:
-      case CDR_EV_CHILD_TIMED_OUT:
-      case CDR_EV_CHILD_TERMINATED: {  // DeletePendingChildExecution :1138-1144
-        const int slot = find_initiated(chi, hw_chi, e.key);
-        if (slot >= 0) {
-          chi[slot].initiated_id = DEAD_KEY;
-          live_chi--;
-        }
-        break;
-      }
-      case CDR_EV_RCE_INITIATED: {  // :408-427 -> :2577-2596
-        const int slot = alloc_initiated(can, hw_can, can_cap);
-        if (slot < 0) {
-          FAIL(CDR_E_BAD_INPUT);
+        case CDR_EV_CHILD_START_FAILED:
+        case CDR_EV_CHILD_COMPLETED:
+        case CDR_EV_CHILD_FAILED:
+        case CDR_EV_CHILD_CANCELED:
+        case CDR_EV_CHILD_TIMED_OUT:
+        case CDR_EV_CHILD_TERMINATED: {  // DeletePendingChildExecution :1138-1144
+          const int slot = find_initiated(chi, hw_chi, e.key);
+          if (slot >= 0) {
+            chi[slot].initiated_id = DEAD_KEY;
+            live_chi--;
+          }
           break;
         }
-        cdr_cancel_info c;
-        c.version = e.ver;
-        c.initiated_event_batch_id = call_first_id;
-        c.initiated_id = e.id;
-        uint64_t lo, hi;
-        cdr_uuid(B.uuid_seed, D.wf_key, CDR_UUID_CANCEL_REQ, e.id, &lo, &hi);
-        c.cancel_request_lo = lo;
-        c.cancel_request_hi = hi;
-        gput(can + slot, c);
-        live_can++;
-        if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
-        break;
-      }
-      case CDR_EV_RCE_FAILED:
-      case CDR_EV_EXT_CANCEL_REQUESTED: {  // DeletePendingRequestCancel :1147-1153
-        const int slot = find_initiated(can, hw_can, e.key);
-        if (slot >= 0) {
-          can[slot].initiated_id = DEAD_KEY;
-          live_can--;
-        }
-        break;
-      }
-      case CDR_EV_SE_INITIATED: {  // :439-458 -> :2701-2723
-        const int slot = alloc_initiated(sig, hw_sig, sig_cap);
-        if (slot < 0) {
-          FAIL(CDR_E_BAD_INPUT);
+        case CDR_EV_RCE_INITIATED: {  // :408-427 -> :2577-2596
+          const int slot = alloc_initiated(can, hw_can, CP.cancel_cap);
+          if (slot < 0) {
+            FAIL(CDR_E_BAD_INPUT);
+            break;
+          }
+          cdr_cancel_info c;
+          c.version = e.ver;
+          c.initiated_event_batch_id = call_first_id;
+          c.initiated_id = e.id;
+          uint64_t lo, hi;
+          cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_CANCEL_REQ, e.id, &lo, &hi);
+          c.cancel_request_lo = lo;
+          c.cancel_request_hi = hi;
+          gput(can + slot, c);
+          live_can++;
+          if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
           break;
         }
-        cdr_signal_info c;
-        c.version = e.ver;
-        c.initiated_event_batch_id = call_first_id;
-        c.initiated_id = e.id;
-        uint64_t lo, hi;
-        cdr_uuid(B.uuid_seed, D.wf_key, CDR_UUID_SIGNAL_REQ, e.id, &lo, &hi);
-        c.signal_request_lo = lo;
-        c.signal_request_hi = hi;
-        c.signal_name = e.h;
-        c.input = (uint32_t)((uint64_t)e.aux >> 32);
-        c.control = (uint32_t)e.aux;
-        c._pad = 0;
-        gput(sig + slot, c);
-        live_sig++;
-        if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
-        break;
-      }
-      case CDR_EV_SE_FAILED:
-      case CDR_EV_EXT_SIGNALED: {  // DeletePendingSignal :1156-1162
-        const int slot = find_initiated(sig, hw_sig, e.key);
-        if (slot >= 0) {
-          sig[slot].initiated_id = DEAD_KEY;
-          live_sig--;
+        case CDR_EV_RCE_FAILED:
+        case CDR_EV_EXT_CANCEL_REQUESTED: {  // DeletePendingRequestCancel :1147-1153
+          const int slot = find_initiated(can, hw_can, e.key);
+          if (slot >= 0) {
+            can[slot].initiated_id = DEAD_KEY;
+            live_can--;
+          }
+          break;
         }
-        break;
-      }
-      case CDR_EV_AT_REQ_CANCEL_FAILED:
-      case CDR_EV_CANCEL_TIMER_FAILED:
-      case CDR_EV_MARKER_RECORDED:
-        break;
-      case CDR_EV_WF_SIGNALED:  // :473-476
-        x_signals++;
-        break;
-      case CDR_EV_WF_CANCEL_REQUESTED:  // :478-481
-        x_flags |= CDR_XI_CANCEL_REQUESTED;
-        break;
-      case CDR_EV_WF_COMPLETED:
-      case CDR_EV_WF_FAILED:
-      case CDR_EV_WF_TIMED_OUT:
-      case CDR_EV_WF_CANCELED:
-      case CDR_EV_WF_TERMINATED: {  // :483-531
-        const int cs = type == CDR_EV_WF_COMPLETED   ? CDR_CLOSE_COMPLETED
-                       : type == CDR_EV_WF_FAILED    ? CDR_CLOSE_FAILED
-                       : type == CDR_EV_WF_TIMED_OUT ? CDR_CLOSE_TIMED_OUT
-                       : type == CDR_EV_WF_CANCELED  ? CDR_CLOSE_CANCELED
+        case CDR_EV_SE_INITIATED: {  // :439-458 -> :2701-2723
+          const int slot = alloc_initiated(sig, hw_sig, CP.signal_cap);
+          if (slot < 0) {
+            FAIL(CDR_E_BAD_INPUT);
+            break;
+          }
+          cdr_signal_info c;
+          c.version = e.ver;
+          c.initiated_event_batch_id = call_first_id;
+          c.initiated_id = e.id;
+          uint64_t lo, hi;
+          cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_SIGNAL_REQ, e.id, &lo, &hi);
+          c.signal_request_lo = lo;
+          c.signal_request_hi = hi;
+          c.signal_name = e.h;
+          c.input = (uint32_t)((uint64_t)e.aux >> 32);
+          c.control = (uint32_t)e.aux;
+          c._pad = 0;
+          gput(sig + slot, c);
+          live_sig++;
+          if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
+          break;
+        }
+        case CDR_EV_SE_FAILED:
+        case CDR_EV_EXT_SIGNALED: {  // DeletePendingSignal :1156-1162
+          const int slot = find_initiated(sig, hw_sig, e.key);
+          if (slot >= 0) {
+            sig[slot].initiated_id = DEAD_KEY;
+            live_sig--;
+          }
+          break;
+        }
+        case CDR_EV_AT_REQ_CANCEL_FAILED:
+        case CDR_EV_CANCEL_TIMER_FAILED:
+        case CDR_EV_MARKER_RECORDED:
+          break;
+        case CDR_EV_WF_SIGNALED:  // :473-476
+          x_signals++;
+          break;
+        case CDR_EV_WF_CANCEL_REQUESTED:  // :478-481
+          x_flags |= CDR_XI_CANCEL_REQUESTED;
+          break;
+        case CDR_EV_WF_COMPLETED:
+        case CDR_EV_WF_FAILED:
+        case CDR_EV_WF_TIMED_OUT:
+        case CDR_EV_WF_CANCELED:
+        case CDR_EV_WF_TERMINATED: {  // :483-531
+          const int cs = ut == CDR_EV_WF_COMPLETED   ? CDR_CLOSE_COMPLETED
+                         : ut == CDR_EV_WF_FAILED    ? CDR_CLOSE_FAILED
+                         : ut == CDR_EV_WF_TIMED_OUT ? CDR_CLOSE_TIMED_OUT
+                         : ut == CDR_EV_WF_CANCELED  ? CDR_CLOSE_CANCELED
                                                      : CDR_CLOSE_TERMINATED;
-        if (!transition_ok(x_state, x_close, CDR_STATE_COMPLETED, cs)) {
-          FAIL(CDR_E_INVALID_STATE_TRANSITION);
+          if (!transition_ok(x_state, x_close, CDR_STATE_COMPLETED, cs)) {
+            FAIL(CDR_E_INVALID_STATE_TRANSITION);
+            break;
+          }
+          x_state = CDR_STATE_COMPLETED;
+          x_close = cs;
+          x_completion_batch = call_first_id;
           break;
         }
-        x_state = CDR_STATE_COMPLETED;
-        x_close = cs;
-        x_completion_batch = call_first_id;
-        break;
-      }
-      case CDR_EV_UPSERT_SA: {  // :533-535 -> :2746-2768
-        const uint64_t off = (uint64_t)e.aux;
-        const uint32_t cnt = e.h;
-        for (uint32_t q = 0; q < cnt; q++) {
-          const cdr_kv kv = gget((const GAS cdr_kv*)B.kvs + (off + q));
-          bool found = false;
-          for (uint32_t j = 0; j < n_sa; j++)
-            if (sa[j].key == kv.key) {
-              sa[j].value = kv.value;
-              found = true;
-            }
-          if (!found && n_sa < sa_cap) gput(sa + n_sa++, kv);
-        }
-        x_flags |= CDR_XI_HAS_SEARCH_ATTR;
-        break;
-      }
-      case CDR_EV_WF_CONTINUED_AS_NEW: {  // :537-595
-        if (D.newrun < 0 || call_idx != D.newrun_call || late(B.wfs)[D.newrun].ev_len == 0) {
-          FAIL(CDR_E_NEWRUN_HISTORY_EMPTY);
+        case CDR_EV_UPSERT_SA: {  // :533-535 -> :2746-2768
+          const uint64_t off = (uint64_t)e.aux;
+          const uint32_t cnt = e.h;
+          for (uint32_t q = 0; q < cnt; q++) {
+            const cdr_kv kv = gget(gp(B_.kvs) + (off + q));
+            bool found = false;
+            for (uint32_t j = 0; j < n_sa; j++)
+              if (sa[j].key == kv.key) {
+                sa[j].value = kv.value;
+                found = true;
+              }
+            if (!found && n_sa < CP.sa_cap) gput(sa + n_sa++, kv);
+          }
+          x_flags |= CDR_XI_HAS_SEARCH_ATTR;
           break;
         }
-        newrun_applied = true;  // the new run replays in its own lane; k_finalize joins
-        if (!transition_ok(x_state, x_close, CDR_STATE_COMPLETED, CDR_CLOSE_CONTINUED_AS_NEW)) {
-          FAIL(CDR_E_INVALID_STATE_TRANSITION);
+        case CDR_EV_WF_CONTINUED_AS_NEW: {  // :537-595
+          const int32_t nr = D.newrun;
+          if (nr < 0 || call_idx != D.newrun_call || gp(B_.wfs)[nr].ev_len == 0) {
+            FAIL(CDR_E_NEWRUN_HISTORY_EMPTY);
+            break;
+          }
+          newrun_applied = true;  // the new run replays in its own lane; k_finalize joins
+          if (!transition_ok(x_state, x_close, CDR_STATE_COMPLETED, CDR_CLOSE_CONTINUED_AS_NEW)) {
+            FAIL(CDR_E_INVALID_STATE_TRANSITION);
+            break;
+          }
+          x_state = CDR_STATE_COMPLETED;
+          x_close = CDR_CLOSE_CONTINUED_AS_NEW;
+          x_completion_batch = call_first_id;
           break;
         }
-        x_state = CDR_STATE_COMPLETED;
-        x_close = CDR_CLOSE_CONTINUED_AS_NEW;
-        x_completion_batch = call_first_id;
-        break;
+        default:
+          FAIL(CDR_E_UNKNOWN_EVENT_TYPE);  // :597-599
+          break;
       }
-      default:
-        FAIL(CDR_E_UNKNOWN_EVENT_TYPE);  // :597-599
-        break;
     }
   }
 #undef FAIL
   // ---- end of the last call
   if (len > 0 && (err == CDR_OK || stop_at_call_end)) {
     if (isRS) {
-      const int src = cluster_for_version(B.cluster, prev_ver);
+      const int src = cluster_for_version(B_.cluster, prev_ver);
       if (src < 0) {
         err = CDR_P_UNKNOWN_CLUSTER;
         err_id = call_first_id;
         err_k = call_first_k;
-      } else if (src != B.cluster.current_cluster && err == CDR_OK) {
+      } else if (src != B_.cluster.current_cluster && err == CDR_OK) {
         RS->lri_version[src] = prev_ver;
         RS->lri_last_event_id[src] = prev_id;
         rs_mask |= 1u << src;
@@ -1114,29 +1128,27 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   r.n_vh = n_vh;
   r.n_reset_points = n_rp;
   r.n_search_attr = n_sa;
-  const uint64_t lane_base = (row0 * CDR_SLICE_WIDTH) + lane;  // element of row 0 of this lane
   if (err == CDR_OK) {
     // emit the live working slots as persisted rows (k_tables orders them by key);
     // fields the loop did not carry are re-read from the scheduling event's row
-    GAS cdr_activity_info* act = (GAS cdr_activity_info*)(O.act + CP.act_off);
-    GAS cdr_timer_info* tim = (GAS cdr_timer_info*)(O.timer + CP.timer_off);
+    GAS cdr_activity_info* act = gp(O_.act) + CP.act_off;
+    GAS cdr_timer_info* tim = gp(O_.timer) + CP.timer_off;
     uint32_t n = 0;
     for (uint32_t j = 0; j < hw_act; j++) {
       const int64_t sid = A.ld(j, AP_SID);
       if (sid == DEAD_KEY) continue;
       const uint64_t rows = (uint64_t)A.ld(j, AP_ROWS);
-      const uint64_t i_s = lane_base + (uint64_t)(uint32_t)rows * CDR_SLICE_WIDTH;
-      const uint64_t i_b = lane_base + (rows >> 32) * CDR_SLICE_WIDTH;
-      const int64_t sched_ts = ((const GAS int64_t*)B.ev.timestamp)[i_s];
-      const uint32_t arec = (uint32_t)((const GAS uint64_t*)B.ev.aux)[i_s];
-      const GAS cdr_attr_at_scheduled* a = (const GAS cdr_attr_at_scheduled*)(B.ev.arena + arec);
+      const uint32_t o_s = el8((uint32_t)rows, len, lane), o_b = el8((uint32_t)(rows >> 32), len, lane);
+      const int64_t sched_ts = bld64(S.r, o_s, S.col(CDR_COL_TIMESTAMP));
+      const uint32_t arec = (uint32_t)bld64(S.r, o_s, S.col(CDR_COL_AUX));
+      const GAS cdr_attr_at_scheduled* a = gp((const cdr_attr_at_scheduled*)(B_.ev.arena + arec));
       const uint64_t m = (uint64_t)A.ld(j, AP_META);
       const bool retry = (a->flags & CDR_AF_HAS_RETRY) != 0;
       const int32_t s2c = a->s2c_s, xs = a->retry_expiration_s;
       cdr_activity_info o;
       o.version = A.ld(j, AP_VER);
       o.schedule_id = sid;
-      o.scheduled_event_batch_id = ((const GAS int64_t*)B.ev.event_id)[i_b];
+      o.scheduled_event_batch_id = bld64(S.r, o_b, S.col(CDR_COL_EVENT_ID));
       o.scheduled_time = sched_ts;
       o.started_id = A.ld(j, AP_STARTED_ID);
       o.started_time = A.ld(j, AP_STARTED_TIME);
@@ -1178,7 +1190,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     }
     r.n_timer = n;
   }
-  gput((GAS cdr_wf_result*)O.result + w, r);
+  gput(gp(O_.result) + w, r);
   if (err != CDR_OK) return;
   if (n_vh) gput(vh + (n_vh - 1), cdr_vh_item{vh_last_id, vh_last_ver});
   if (!(x_flags & CDR_XI_STARTED)) {  // no WorkflowExecutionStarted: its fields keep their zero values
@@ -1202,7 +1214,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   X->last_first_event_id = call_first_id;  // stateBuilder.go:603 of the last call
   // LastEventTaskID (stateBuilder.go:155): every applied event sets it, so an OK
   // workflow ends with its last event's task id
-  X->last_event_task_id = ((const GAS int64_t*)B.ev.task_id)[lane_base + (uint64_t)(len - 1) * CDR_SLICE_WIDTH];
+  X->last_event_task_id = bld64(S.r, el8(len - 1, len, lane), S.col(CDR_COL_TASK_ID));
   X->next_event_id = x_next_event;
   X->last_processed_event = x_last_processed;
   X->signal_count = x_signals;
@@ -1232,8 +1244,6 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   } else {
     gput(RS, cdr_repl_state{});
   }
-}
-
 #undef D
 #undef CP
 #undef X
@@ -1244,12 +1254,9 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
 #undef vh
 #undef rp
 #undef sa
-#undef chi_cap
-#undef can_cap
-#undef sig_cap
-#undef vh_cap
-#undef rp_cap
-#undef sa_cap
+#undef B_
+#undef O_
+}
 
 // Per-workflow table epilogue: move live rows to the front in key order (the
 // canonical order of the Go maps' keys), sort the SearchAttributes map by key, and
@@ -1362,10 +1369,10 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const uint32_t blocks = in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
-  if (blocks) hipLaunchKernelGGL(k_replay<true>, dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, *in, *out, la, lt);
+  cdr_launch L{*in, *out, la, lt};
+  if (blocks) hipLaunchKernelGGL(k_replay<true>, dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, L);
   HIPCHK(hipGetLastError());
-  if (blocks && spill)
-    hipLaunchKernelGGL(k_replay<false>, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, *in, *out, la, lt);
+  if (blocks && spill) hipLaunchKernelGGL(k_replay<false>, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used + 1] : c->ev[1], st));
   if (ring) {

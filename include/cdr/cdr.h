@@ -42,11 +42,14 @@ extern "C" {
 
 #define CDR_SLICE_WIDTH 64 /* workflows per slice = one wavefront */
 
-/* Sliced event layout ("SELL-64"): workflows are grouped 64 to a slice (one lane
- * each, slices sorted by length); event k of lane L of slice s lives at element
- * (slice_row0[s] + k) * 64 + L of every column, so a wavefront that walks its 64
- * histories in lockstep reads each column fully coalesced.  The kernel reads only
- * the columns an event's type needs (replay.hip: NEED_*).
+/* Sliced event layout ("SELL-64" in a slice-major slab): workflows are grouped 64
+ * to a slice (one lane each, slices sorted by length).  Slice s owns one contiguous
+ * block of the slab, starting at byte slice_row0[s] * 64 * CDR_EL_BYTES, that holds
+ * its E = slice_len[s] * 64 elements column after column (cdr_col_off below).  Event
+ * k of lane L is element k * 64 + L of every column of its slice, so a wavefront
+ * that walks its 64 histories in lockstep reads each column fully coalesced, and
+ * one buffer descriptor per slice addresses every column.  The kernel reads only
+ * the operand columns an event's type needs (CDR_SEF_NEED_* bits of type_flags).
  *
  * Operand columns per type (all others 0):
  *   WorkflowExecutionStarted  aux = arena word offset of cdr_attr_wf_started
@@ -69,23 +72,33 @@ extern "C" {
  *   other child / external closes  key = initiatedEventId
  *   UpsertWorkflowSearchAttributes  aux = kv offset, h = kv count
  *   WorkflowExecutionContinuedAsNew  h = newExecutionRunId */
+enum cdr_col {
+  CDR_COL_EVENT_ID = 0, /* i64 */
+  CDR_COL_VERSION,      /* i64 */
+  CDR_COL_TIMESTAMP,    /* i64 */
+  CDR_COL_TASK_ID,      /* i64 */
+  CDR_COL_KEY,          /* i64 entity key: scheduled/initiated event id, activity/timer handle ... */
+  CDR_COL_AUX,          /* i64 second operand or arena word offset (type-dependent) */
+  CDR_COL_TYPE_FLAGS,   /* u32 bits 0-7 cdr_event_type, 8+ CDR_SEF_* */
+  CDR_COL_H,            /* u32 string handle operand (type-dependent) */
+  CDR_COL_N,            /* i32 small integer operand (type-dependent) */
+  CDR_NUM_COLS
+};
+#define CDR_EL_BYTES 60u /* bytes of one (row, lane) element over all columns */
+/* element size and byte offset (within a slice block of `elems` elements) of a column */
+CDR_HD uint32_t cdr_col_size(int c) { return c < CDR_COL_TYPE_FLAGS ? 8u : 4u; }
+CDR_HD uint64_t cdr_col_off(int c, uint64_t elems) {
+  return elems * (c <= CDR_COL_TYPE_FLAGS ? 8u * (uint32_t)c : 48u + 4u * (uint32_t)(c - CDR_COL_TYPE_FLAGS));
+}
+
 typedef struct cdr_slices {
   uint32_t n_slices, _pad;
   uint64_t n_rows;        /* sum of slice_len */
   uint64_t arena_words;   /* 8-byte words of attribute records */
-  const uint64_t* slice_row0; /* [n_slices] */
+  const uint64_t* slice_row0; /* [n_slices] prefix sum of slice_len */
   const uint32_t* slice_len;  /* [n_slices] */
   const int32_t* lane_wf;     /* [n_slices*64] workflow index, -1 = empty lane */
-  /* event columns, [n_rows*64] each */
-  const uint32_t* type_flags; /* bits 0-7 cdr_event_type, 8+ CDR_SEF_* */
-  const int64_t* event_id;
-  const int64_t* version;
-  const int64_t* timestamp;
-  const int64_t* task_id;
-  const int64_t* key; /* entity key: scheduled/initiated event id, activity/timer handle ... */
-  const int64_t* aux; /* second operand or arena word offset (type-dependent) */
-  const uint32_t* h;  /* string handle operand (type-dependent) */
-  const int32_t* n;   /* small integer operand (type-dependent) */
+  const uint8_t* slab;        /* n_rows * 64 * CDR_EL_BYTES bytes of event columns */
   const uint64_t* arena; /* WorkflowExecutionStarted / ActivityTaskScheduled attribute records */
   /* working-state scratch of each slice (cdr_plan_scratch): pending activities and
    * user timers are kept lane-interleaved ("plane j*P+p, lane L") while they are live */
@@ -99,6 +112,48 @@ typedef struct cdr_slices {
 
 #define CDR_SEF_BATCH_FIRST (1u << 8)
 #define CDR_SEF_DOMAIN_MISSING (1u << 9)
+/* operand columns the event's type reads (set by the packer from CDR_NEED_*) */
+#define CDR_SEF_NEED_TS (1u << 16)
+#define CDR_SEF_NEED_KEY (1u << 17)
+#define CDR_SEF_NEED_AUX (1u << 18)
+#define CDR_SEF_NEED_H (1u << 19)
+#define CDR_SEF_NEED_N (1u << 20)
+/* per-column sets of event types (bit = cdr_event_type) that read it; every type
+ * reads type_flags, event_id and version (stateBuilder.go:134-155) */
+#define CDR_TB(t) (1ull << (t))
+#define CDR_NEED_TS                                                                                  \
+  (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_DT_SCHEDULED) | CDR_TB(CDR_EV_DT_STARTED) |              \
+   CDR_TB(CDR_EV_AT_SCHEDULED) | CDR_TB(CDR_EV_AT_STARTED) | CDR_TB(CDR_EV_TIMER_STARTED))
+#define CDR_NEED_KEY                                                                                 \
+  (CDR_TB(CDR_EV_DT_STARTED) | CDR_TB(CDR_EV_AT_SCHEDULED) | CDR_TB(CDR_EV_AT_STARTED) |              \
+   CDR_TB(CDR_EV_AT_COMPLETED) | CDR_TB(CDR_EV_AT_FAILED) | CDR_TB(CDR_EV_AT_TIMED_OUT) |              \
+   CDR_TB(CDR_EV_AT_CANCELED) | CDR_TB(CDR_EV_AT_CANCEL_REQUESTED) | CDR_TB(CDR_EV_TIMER_STARTED) |    \
+   CDR_TB(CDR_EV_TIMER_FIRED) | CDR_TB(CDR_EV_TIMER_CANCELED) | CDR_TB(CDR_EV_CHILD_INITIATED) |       \
+   CDR_TB(CDR_EV_CHILD_STARTED) | CDR_TB(CDR_EV_CHILD_START_FAILED) | CDR_TB(CDR_EV_CHILD_COMPLETED) | \
+   CDR_TB(CDR_EV_CHILD_FAILED) | CDR_TB(CDR_EV_CHILD_CANCELED) | CDR_TB(CDR_EV_CHILD_TIMED_OUT) |      \
+   CDR_TB(CDR_EV_CHILD_TERMINATED) | CDR_TB(CDR_EV_RCE_FAILED) | CDR_TB(CDR_EV_EXT_CANCEL_REQUESTED) | \
+   CDR_TB(CDR_EV_SE_FAILED) | CDR_TB(CDR_EV_EXT_SIGNALED))
+#define CDR_NEED_AUX                                                                                 \
+  (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_DT_SCHEDULED) | CDR_TB(CDR_EV_DT_COMPLETED) |            \
+   CDR_TB(CDR_EV_AT_SCHEDULED) | CDR_TB(CDR_EV_TIMER_STARTED) | CDR_TB(CDR_EV_CHILD_INITIATED) |       \
+   CDR_TB(CDR_EV_SE_INITIATED) | CDR_TB(CDR_EV_UPSERT_SA))
+#define CDR_NEED_H                                                                                   \
+  (CDR_TB(CDR_EV_DT_STARTED) | CDR_TB(CDR_EV_DT_COMPLETED) | CDR_TB(CDR_EV_AT_SCHEDULED) |            \
+   CDR_TB(CDR_EV_AT_STARTED) | CDR_TB(CDR_EV_CHILD_INITIATED) | CDR_TB(CDR_EV_CHILD_STARTED) |        \
+   CDR_TB(CDR_EV_SE_INITIATED) | CDR_TB(CDR_EV_UPSERT_SA))
+#define CDR_NEED_N \
+  (CDR_TB(CDR_EV_DT_SCHEDULED) | CDR_TB(CDR_EV_DT_TIMED_OUT) | CDR_TB(CDR_EV_AT_SCHEDULED) | CDR_TB(CDR_EV_CHILD_INITIATED))
+/* type_flags word of an event: type, flags and its column-need bits */
+CDR_HD uint32_t cdr_type_flags(uint32_t type, uint32_t flags) {
+  uint32_t tf = (type & 0xFFu) | flags;
+  if (type < 64) {
+    const uint64_t b = 1ull << type;
+    tf |= ((CDR_NEED_TS & b) ? CDR_SEF_NEED_TS : 0u) | ((CDR_NEED_KEY & b) ? CDR_SEF_NEED_KEY : 0u) |
+          ((CDR_NEED_AUX & b) ? CDR_SEF_NEED_AUX : 0u) | ((CDR_NEED_H & b) ? CDR_SEF_NEED_H : 0u) |
+          ((CDR_NEED_N & b) ? CDR_SEF_NEED_N : 0u);
+  }
+  return tf;
+}
 
 /* everything the device needs for one replay launch (all pointers device memory) */
 typedef struct cdr_dev_batch {

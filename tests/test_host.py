@@ -18,6 +18,7 @@ def _declared():
     for h in ("cdr.h", "synth.h"):
         src = open(os.path.join(ROOT, "include", "cdr", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"CDR_HD [^(]*\(", "", src)  # header-inline helpers are not exports
         names |= set(re.findall(r"\b(cdr_[a-z0-9_]+)\s*\(", src))
     return names
 
@@ -65,18 +66,16 @@ def test_pack_round_trip():
     row0 = np.zeros(ns.value, np.uint64)
     L.cdr_plan_slices(b.wfs, b.n_wfs, lane.ctypes.data, slen.ctypes.data, row0.ctypes.data, C.byref(ns),
                       C.byref(rows))
-    cols = {k: np.zeros(n, dt) for k, dt in (("type_flags", np.uint32), ("event_id", np.int64),
-                                             ("version", np.int64), ("timestamp", np.int64),
-                                             ("task_id", np.int64), ("key", np.int64), ("aux", np.int64),
-                                             ("h", np.uint32), ("n", np.int32))}
+    slab = np.zeros(n * abi.EL_BYTES, np.uint8)
     aw = L.cdr_plan_arena_words(C.byref(b.cstruct()))
     arena = np.zeros(max(1, aw), np.uint64)
     s = abi.CdrSlices(n_slices=ns.value, n_rows=rows.value, arena_words=aw)
     s.slice_row0, s.slice_len, s.lane_wf = row0.ctypes.data, slen.ctypes.data, lane.ctypes.data
-    for k, v in cols.items():
-        setattr(s, k, v.ctypes.data)
+    s.slab = slab.ctypes.data
     s.arena = arena.ctypes.data
     assert L.cdr_pack_slices(C.byref(b.cstruct()), C.byref(s), 2) == 0
+    cols = abi.slab_columns(slab, row0, slen)
+    assert all(len(v) == n for v in cols.values())
     for i, w in enumerate(lane):
         sl, l = divmod(i, 64)
         if w < 0:
@@ -89,7 +88,12 @@ def test_pack_round_trip():
                 continue
             e = b.events[d.ev_off + k]
             assert cols["type_flags"][j] & 0xFF == e.type
-            assert bool(cols["type_flags"][j] & (1 << 8)) == bool(e.flags & 1 or k == 0)
+            assert bool(cols["type_flags"][j] & abi.SEF_BATCH_FIRST) == bool(e.flags & 1 or k == 0)
+            need = (int(cols["type_flags"][j]) >> 16) & 0x1F  # CDR_SEF_NEED_{TS,KEY,AUX,H,N}
+            if e.type == abi.EV["ActivityTaskScheduled"]:
+                assert need == 0x1F
+            elif e.type == abi.EV["ActivityTaskCompleted"]:
+                assert need == 0x02
             assert (cols["event_id"][j], cols["version"][j], cols["timestamp"][j], cols["task_id"][j]) == (
                 e.event_id, e.version, e.timestamp, e.task_id)
             if e.type == abi.EV["ActivityTaskScheduled"]:
