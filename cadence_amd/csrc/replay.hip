@@ -48,6 +48,9 @@
 #ifndef CDR_WPE
 #define CDR_WPE 3 /* waves per SIMD the register allocator must leave room for */
 #endif
+#ifndef CDR_EXP
+#define CDR_EXP 0 /* cost-breakdown experiments only (tools/build_variants.sh); 0 = product */
+#endif
 #ifndef CDR_LDS_ACT_MAX
 #define CDR_LDS_ACT_MAX 1 /* activity working slots per lane kept in LDS */
 #endif
@@ -371,6 +374,61 @@ __device__ __forceinline__ void tim_pick(const T& S, uint32_t hw) {
   }
 }
 
+// Predicated forms of the picks for the replay loop: the slot scan runs to the
+// slice's uniform slot count `cap` (slots past the lane's high-water mark `hw` are
+// ignored), state is carried in selects, and only the final status-bit store is
+// lane-masked.  `on` = the lane's event asked for a pick.
+template <class A>
+__device__ __forceinline__ void act_pick_p(const A& S, uint32_t hw, uint32_t cap, bool on) {
+  int best = -1;
+  int64_t bt = 0, bs = 0;
+  int bo = 0;
+  uint32_t bbit = 0;
+  uint64_t bm = 0;
+  for (uint32_t j = 0; j < cap; j++) {
+    const int64_t sid = S.ld(j, AP_SID);
+    const uint64_t meta = (uint64_t)S.ld(j, AP_META);
+    const int64_t t0 = S.ld(j, AP_TS2C), ta = S.ld(j, AP_TALT), th = S.ld(j, AP_THB);
+    // append order breaks ties within an activity: S2C, then STC/S2S, then HB
+    const bool pa = ta < t0;
+    const int64_t t1 = pa ? ta : t0;
+    const bool ph = th < t1;
+    const int64_t t = ph ? th : t1;
+    const int o = ph ? 2 : (pa ? 1 : 0);
+    const uint32_t bit = ph ? CDR_TTS_HEARTBEAT
+                            : (pa ? ((meta & META_FLAG(AF_STARTED)) ? CDR_TTS_START_TO_CLOSE : CDR_TTS_SCHEDULE_TO_START)
+                                  : CDR_TTS_SCHEDULE_TO_CLOSE);
+    const bool better = on && j < hw && sid != DEAD_KEY &&
+                        (best < 0 || t < bt || (t == bt && (sid < bs || (sid == bs && o < bo))));
+    best = better ? (int)j : best;
+    bt = better ? t : bt;
+    bs = better ? sid : bs;
+    bo = better ? o : bo;
+    bbit = better ? bit : bbit;
+    bm = better ? meta : bm;
+  }
+  const uint64_t b = (uint64_t)bbit << META_TTS_SHIFT;
+  if (best >= 0 && !(bm & b)) S.st((uint32_t)best, AP_META, (int64_t)(bm | b));
+}
+template <class T>
+__device__ __forceinline__ void tim_pick_p(const T& S, uint32_t hw, uint32_t cap, bool on) {
+  int best = -1;
+  int64_t be = 0, bs = 0;
+  uint64_t bv = 0;
+  for (uint32_t j = 0; j < cap; j++) {
+    const int64_t sid = S.ld(j, TP_SID);
+    const int64_t ex = S.ld(j, TP_EXPIRY);
+    const uint64_t v = (uint64_t)S.ld(j, TP_TID_TASK);
+    const bool better = on && j < hw && sid != DEAD_KEY && (best < 0 || ex < be || (ex == be && sid < bs));
+    best = better ? (int)j : best;
+    be = better ? ex : be;
+    bs = better ? sid : bs;
+    bv = better ? v : bv;
+  }
+  if (best >= 0 && (bv >> 32) != CDR_TIMER_TASK_STATUS_CREATED)
+    S.st((uint32_t)best, TP_TID_TASK, (int64_t)((bv & 0xFFFFFFFFull) | ((uint64_t)CDR_TIMER_TASK_STATUS_CREATED << 32)));
+}
+
 }  // namespace
 
 // ============================================================== replay kernel
@@ -496,16 +554,33 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
 
   // ---- software pipeline: operands of event k+CDR_DEPTH and the type of event
   // k+CDR_DEPTH+2 are issued while event k is processed
-  uint32_t o8 = el8(0, len, lane);  // voffset of event k
 #if CDR_DEPTH == 2
-  Ev q0 = load_ops(S, o8, load_tf(S, o8));
+  Ev q0 = load_ops(S, el8(0, len, lane), load_tf(S, el8(0, len, lane)));
   Ev q1 = load_ops(S, el8(1, len, lane), load_tf(S, el8(1, len, lane)));
   uint32_t t2 = load_tf(S, el8(2, len, lane)), t3 = load_tf(S, el8(3, len, lane));
 #else
-  Ev q0 = load_ops(S, o8, load_tf(S, o8));
+  Ev q0 = load_ops(S, el8(0, len, lane), load_tf(S, el8(0, len, lane)));
   uint32_t t1 = load_tf(S, el8(1, len, lane)), t2 = load_tf(S, el8(2, len, lane));
 #endif
-  for (uint32_t k = 0; k < len; k++) {
+  const uint32_t vh_cap = CP.vh_cap;
+  bool done = len == 0;  // the lane stopped (end of a failed call) or ran out of events
+
+  // Control flow below is wave-uniform (the step loop runs to the slice length, the
+  // dispatch loop over the event types present in the wave); per-lane effects on the
+  // register state are selects and only memory side effects are lane-masked.  This
+  // keeps the compiler from structurising a divergent CFG around ~80 live registers.
+#define SEL(c, a, b) ((c) ? (a) : (b))
+#define PFAIL(cond, code)               \
+  do {                                  \
+    const bool f_ = (cond);             \
+    err = SEL(f_, (int32_t)(code), err); \
+    err_id = SEL(f_, e.id, err_id);     \
+    err_k = SEL(f_, k, err_k);          \
+    stop_at_call_end |= f_;             \
+  } while (0)
+  const uint32_t srows = S.elems / CDR_SLICE_WIDTH;
+  for (uint32_t k = 0; k < srows; k++) {
+    if (__builtin_amdgcn_ballot_w64(!done) == 0) break;  // every lane finished
     const Ev e = q0;
 #if CDR_DEPTH == 2
     q0 = q1;
@@ -519,221 +594,230 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     t1 = t2;
     t2 = t3;
 #endif
+    done |= k >= len;
     const uint32_t type = e.tf & 0xFFu;
-    if ((e.tf & CDR_SEF_BATCH_FIRST) || k == 0) {
-      if (k > 0) {
-        // ---- end of the previous call: stateBuilder.go:603-604, plus the replication
-        // state whose source is the call's last event (mutableStateBuilder.go:561-581)
-        if (isRS) {
-          const int src = cluster_for_version(B_.cluster, prev_ver);
-          if (src < 0) {  // the panic fires at the call's first event, before anything else
-            err = CDR_P_UNKNOWN_CLUSTER;
-            err_id = call_first_id;
-            err_k = call_first_k;
-          } else if (src != B_.cluster.current_cluster) {
-            RS->lri_version[src] = prev_ver;
-            RS->lri_last_event_id[src] = prev_id;
-            rs_mask |= 1u << src;
-          }
-        }
-        if (err != CDR_OK) break;
-        x_next_event = prev_id + 1;
-        call_idx++;
+    // ---- call boundary: end of the previous call (stateBuilder.go:603-604), plus the
+    // replication state whose source is the call's last event (mutableStateBuilder.go:561-581)
+    const bool bf = !done && ((e.tf & CDR_SEF_BATCH_FIRST) || k == 0);
+    const bool end_call = bf && k > 0;
+    if (isRS && end_call) {  // 2DC only; lane-masked block (rare)
+      const int src = cluster_for_version(B_.cluster, prev_ver);
+      if (src < 0) {  // the panic fires at the call's first event, before anything else
+        err = CDR_P_UNKNOWN_CLUSTER;
+        err_id = call_first_id;
+        err_k = call_first_k;
+      } else if (src != B_.cluster.current_cluster) {
+        RS->lri_version[src] = prev_ver;
+        RS->lri_last_event_id[src] = prev_id;
+        rs_mask |= 1u << src;
       }
-      call_first_id = e.id;
-      call_first_k = k;
     }
-    prev_id = e.id;
-    prev_ver = e.ver;
-    if (stop_at_call_end) continue;  // rest of a failed call: only its last event matters (2DC)
+    done |= end_call && err != CDR_OK;  // a failed call ends the replay (the Go caller returns)
+    const bool nxt_call = end_call && !done;
+    x_next_event = SEL(nxt_call, prev_id + 1, x_next_event);
+    call_idx += nxt_call ? 1u : 0u;
+    const bool start_call = bf && !done;
+    call_first_id = SEL(start_call, e.id, call_first_id);
+    call_first_k = SEL(start_call, k, call_first_k);
+    prev_id = SEL(done, prev_id, e.id);
+    prev_ver = SEL(done, prev_ver, e.ver);
+    bool go = !done && !stop_at_call_end;  // rest of a failed call: only its last event matters (2DC)
+#if CDR_EXP == 2
+    x_signals += go ? (int32_t)(e.ts ^ e.key ^ e.aux ^ e.h ^ e.n) : 0;
+    continue;
+#endif
 
     // ---- version prelude (stateBuilder.go:134-154); 2DC: UpdateReplicationStateVersion
     // (v, true) leaves CurrentVersion = e.ver, read back from prev_ver at the end
     if (isVH) {
-      if (x_state == CDR_STATE_CREATED || x_state == CDR_STATE_RUNNING) curv = e.ver;  // UpdateCurrentVersion
+      const bool gv = go;
+      curv = SEL(gv && (x_state == CDR_STATE_CREATED || x_state == CDR_STATE_RUNNING), e.ver, curv);
       // NewVersionHistoryItem + AddOrUpdateItem (versionHistory.go:31-42,203-236)
-      if (e.id < 0 || (e.ver < 0 && e.ver != CDR_EMPTY_VERSION)) {
-        FAIL(CDR_P_VH_ITEM_INVALID);
-        continue;
-      }
-      if (n_vh != 0 && e.ver < vh_last_ver) {
-        FAIL(CDR_E_VH_LOWER_VERSION);
-        continue;
-      }
-      if (n_vh != 0 && e.id <= vh_last_id) {
-        FAIL(CDR_E_VH_LOWER_EVENT_ID);
-        continue;
-      }
-      if (n_vh == 0 || e.ver > vh_last_ver) {
-        if (n_vh >= CP.vh_cap) {
-          FAIL(CDR_E_BAD_INPUT);
-          continue;
-        }
-        if (n_vh) gput(vh + (n_vh - 1), cdr_vh_item{vh_last_id, vh_last_ver});  // close the previous item
-        n_vh++;
-        vh_last_ver = e.ver;
-      }
-      vh_last_id = e.id;
+      const bool newitem = n_vh == 0 || e.ver > vh_last_ver;
+      const int32_t code = (e.id < 0 || (e.ver < 0 && e.ver != CDR_EMPTY_VERSION)) ? CDR_P_VH_ITEM_INVALID
+                           : (n_vh != 0 && e.ver < vh_last_ver)                     ? CDR_E_VH_LOWER_VERSION
+                           : (n_vh != 0 && e.id <= vh_last_id)                      ? CDR_E_VH_LOWER_EVENT_ID
+                           : (newitem && n_vh >= vh_cap)                            ? CDR_E_BAD_INPUT
+                                                                                    : CDR_OK;
+      const bool f = gv && code != CDR_OK;
+      PFAIL(f, code);
+      go = go && !f;
+      const bool add = go && newitem;
+      if (add && n_vh != 0) gput(vh + (n_vh - 1), cdr_vh_item{vh_last_id, vh_last_ver});  // close the previous item
+      n_vh += add ? 1u : 0u;
+      vh_last_ver = SEL(add, e.ver, vh_last_ver);
+      vh_last_id = SEL(go, e.id, vh_last_id);
     }
     // LastEventTaskID (:155) is read once after the loop (last applied event)
+#if CDR_EXP == 1
+    x_signals += go ? (int32_t)(e.ts ^ e.key ^ e.aux ^ e.h ^ e.n) : 0;
+    continue;
+#endif
 
-    // ---- dispatch (stateBuilder.go:157-600): one pass per distinct event type in
-    // the wave, each with a wave-uniform type, so the switch is a scalar branch tree
-    // and a pass executes only its own case
-    for (bool todo = true; todo;) {
-      const uint32_t ut = __builtin_amdgcn_readfirstlane(type);
-      if (type != ut) continue;
-      todo = false;
+    // ---- dispatch (stateBuilder.go:157-600): one pass per distinct event type among
+    // the lanes that apply an event; the type of each pass is wave-uniform, so the
+    // switch is a scalar branch tree and a pass executes only its own case
+    for (uint64_t pend = __builtin_amdgcn_ballot_w64(go); pend;) {
+      uint32_t ut = __builtin_amdgcn_readlane(type, __builtin_ctzll(pend));
+      asm volatile("" : "+s"(ut));  // keep the switch on the SGPR copy
+      const bool mine = go && type == ut;
+      pend &= ~__builtin_amdgcn_ballot_w64(mine);
       switch (ut) {
         case CDR_EV_WF_STARTED: {  // stateBuilder.go:158-184 -> mutableStateBuilder.go:1639-1716
-          const GAS cdr_attr_wf_started* a = gp((const cdr_attr_wf_started*)(B_.ev.arena + (uint64_t)e.aux));
+          // every lane reads a valid record (the first one for lanes of other types)
+          const GAS cdr_attr_wf_started* a =
+              gp((const cdr_attr_wf_started*)(B_.ev.arena + (uint64_t)(mine ? e.aux : 0)));
           const uint32_t af = a->flags;
-          if ((af & CDR_SF_HAS_PARENT_DOMAIN) && (af & CDR_SF_PARENT_DOMAIN_MISSING)) {
-            FAIL(CDR_E_DOMAIN_NOT_FOUND);
-            break;
-          }
-          if (!transition_ok(x_state, x_close, CDR_STATE_CREATED, CDR_CLOSE_NONE)) {
-            FAIL(CDR_E_INVALID_STATE_TRANSITION);
-            break;
-          }
+          const bool f1 = mine && (af & CDR_SF_HAS_PARENT_DOMAIN) && (af & CDR_SF_PARENT_DOMAIN_MISSING);
+          const bool f2 = mine && !f1 && !transition_ok(x_state, x_close, CDR_STATE_CREATED, CDR_CLOSE_NONE);
+          PFAIL(f1, CDR_E_DOMAIN_NOT_FOUND);
+          PFAIL(f2, CDR_E_INVALID_STATE_TRANSITION);
+          const bool ok = mine && !f1 && !f2;
           const bool first = !(x_flags & CDR_XI_STARTED);  // fields absent from a first Started stay zero
-          X->domain_id = D.domain_id;
-          X->workflow_id = D.workflow_id;
-          X->run_id = D.run_id;
-          X->create_request_id = D.request_id;
-          X->task_list = a->task_list;
-          X->workflow_type = a->workflow_type;
-          X->workflow_timeout = a->exec_timeout_s;
-          X->cron_schedule = a->cron_schedule;
-          X->attempt = a->attempt;
-          X->initiated_id = (af & CDR_SF_HAS_PARENT_INITIATED) ? a->parent_initiated_id : CDR_EMPTY_EVENT_ID;
-          x_dt_timeout_value = a->task_timeout_s;
-          x_state = CDR_STATE_CREATED;
-          x_close = CDR_CLOSE_NONE;
-          x_last_processed = CDR_EMPTY_EVENT_ID;
-          dv = CDR_EMPTY_VERSION;
-          dsched = CDR_EMPTY_EVENT_ID;
-          dstart = CDR_EMPTY_EVENT_ID;
-          dreq = EU;
-          dto = 0;
-          if (af & CDR_SF_HAS_PARENT_DOMAIN) X->parent_domain_id = a->parent_domain_id;
-          else if (first) X->parent_domain_id = 0;
-          if (af & CDR_SF_HAS_PARENT_EXEC) {
-            X->parent_workflow_id = a->parent_workflow_id;
-            X->parent_run_id = a->parent_run_id;
-          } else if (first) {
-            X->parent_workflow_id = 0;
-            X->parent_run_id = 0;
-          }
-          if (a->expiration_ts != 0) {
-            X->expiration_time = a->expiration_ts;
-            x_flags |= CDR_XI_HAS_EXPIRATION;
-          } else if (first) {
-            X->expiration_time = 0;
-          }
-          if (af & CDR_SF_HAS_RETRY) {
-            x_flags |= CDR_XI_HAS_RETRY;
-            X->backoff_coefficient = a->backoff_coefficient;
-            X->expiration_seconds = a->retry_expiration_s;
-            X->initial_interval = a->retry_initial_s;
-            X->maximum_attempts = a->retry_max_attempts;
-            X->maximum_interval = a->retry_max_interval_s;
-            X->nonretriable = a->nonretriable;
-          } else if (first) {
-            X->backoff_coefficient = 0.0;
-            X->expiration_seconds = 0;
-            X->initial_interval = 0;
-            X->maximum_attempts = 0;
-            X->maximum_interval = 0;
-            X->nonretriable = 0;
-          }
-          // rolloverAutoResetPointsWithExpiringTime (:3184-3205)
-          n_rp = 0;
-          cks_ok = 0;
-          x_flags &= ~CDR_XI_HAS_RESET_POINTS;
-          if (af & CDR_SF_HAS_RESET_POINTS) {
-            x_flags |= CDR_XI_HAS_RESET_POINTS;
-            const int64_t expiring = e.ts + (int64_t)D.retention_days * 24ll * 3600ll * NS_PER_S;
-            const uint32_t crun = a->continued_run_id, off = a->reset_points_off, cnt = a->reset_points_len;
-            for (uint32_t q = 0; q < cnt && q < CP.rp_cap; q++) {
-              cdr_reset_point p = gget(gp(B_.rps) + (off + q));
-              const uint32_t run = (p.flags & CDR_RP_HAS_RUN_ID) ? p.run_id : 0u;
-              if (run == crun) {
-                p.flags |= CDR_RP_HAS_EXPIRING;
-                p.expiring_time_nano = expiring;
-              }
-              gput(rp + n_rp++, p);
+          uint32_t nrp = n_rp, nsa = n_sa, xf = x_flags;
+          if (ok) {  // output-record side effects (lane-masked)
+            X->domain_id = D.domain_id;
+            X->workflow_id = D.workflow_id;
+            X->run_id = D.run_id;
+            X->create_request_id = D.request_id;
+            X->task_list = a->task_list;
+            X->workflow_type = a->workflow_type;
+            X->workflow_timeout = a->exec_timeout_s;
+            X->cron_schedule = a->cron_schedule;
+            X->attempt = a->attempt;
+            X->initiated_id = (af & CDR_SF_HAS_PARENT_INITIATED) ? a->parent_initiated_id : CDR_EMPTY_EVENT_ID;
+            if (af & CDR_SF_HAS_PARENT_DOMAIN) X->parent_domain_id = a->parent_domain_id;
+            else if (first) X->parent_domain_id = 0;
+            if (af & CDR_SF_HAS_PARENT_EXEC) {
+              X->parent_workflow_id = a->parent_workflow_id;
+              X->parent_run_id = a->parent_run_id;
+            } else if (first) {
+              X->parent_workflow_id = 0;
+              X->parent_run_id = 0;
             }
+            if (a->expiration_ts != 0) {
+              X->expiration_time = a->expiration_ts;
+              xf |= CDR_XI_HAS_EXPIRATION;
+            } else if (first) {
+              X->expiration_time = 0;
+            }
+            if (af & CDR_SF_HAS_RETRY) {
+              xf |= CDR_XI_HAS_RETRY;
+              X->backoff_coefficient = a->backoff_coefficient;
+              X->expiration_seconds = a->retry_expiration_s;
+              X->initial_interval = a->retry_initial_s;
+              X->maximum_attempts = a->retry_max_attempts;
+              X->maximum_interval = a->retry_max_interval_s;
+              X->nonretriable = a->nonretriable;
+            } else if (first) {
+              X->backoff_coefficient = 0.0;
+              X->expiration_seconds = 0;
+              X->initial_interval = 0;
+              X->maximum_attempts = 0;
+              X->maximum_interval = 0;
+              X->nonretriable = 0;
+            }
+            // rolloverAutoResetPointsWithExpiringTime (:3184-3205)
+            nrp = 0;
+            xf &= ~CDR_XI_HAS_RESET_POINTS;
+            if (af & CDR_SF_HAS_RESET_POINTS) {
+              xf |= CDR_XI_HAS_RESET_POINTS;
+              const int64_t expiring = e.ts + (int64_t)D.retention_days * 24ll * 3600ll * NS_PER_S;
+              const uint32_t crun = a->continued_run_id, off = a->reset_points_off, cnt = a->reset_points_len;
+              const uint32_t cap = CP.rp_cap;
+              for (uint32_t q = 0; q < cnt && q < cap; q++) {
+                cdr_reset_point p = gget(gp(B_.rps) + (off + q));
+                const uint32_t run = (p.flags & CDR_RP_HAS_RUN_ID) ? p.run_id : 0u;
+                if (run == crun) {
+                  p.flags |= CDR_RP_HAS_EXPIRING;
+                  p.expiring_time_nano = expiring;
+                }
+                gput(rp + nrp++, p);
+              }
+            }
+            if (af & CDR_SF_HAS_MEMO) {
+              xf |= CDR_XI_HAS_MEMO;
+              X->memo = a->memo;
+            } else if (first) {
+              X->memo = 0;
+            }
+            if (af & CDR_SF_HAS_SEARCH_ATTR) {
+              nsa = 0;
+              const uint32_t off = a->search_attr_off, cnt = a->search_attr_len, cap = CP.sa_cap;
+              for (uint32_t q = 0; q < cnt && q < cap; q++) gput(sa + nsa++, gget(gp(B_.kvs) + (off + q)));
+              if (nsa) xf |= CDR_XI_HAS_SEARCH_ATTR;
+              else xf &= ~CDR_XI_HAS_SEARCH_ATTR;
+            }
+            xf |= CDR_XI_STARTED | (isVH ? CDR_XI_VH_BRANCH : CDR_XI_HAS_BRANCH);
+            // SetHistoryTree (:313-339): branch token on ExecutionInfo, or on the VH for NDC
+            uint64_t lo, hi;
+            cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_BRANCH, e.id, &lo, &hi);
+            X->branch_tree_id = D.run_id;
+            X->branch_id_lo = lo;
+            X->branch_id_hi = hi;
+            if (isRS) RS->start_version = e.ver;  // :182-184
           }
-          if (af & CDR_SF_HAS_MEMO) {
-            x_flags |= CDR_XI_HAS_MEMO;
-            X->memo = a->memo;
-          } else if (first) {
-            X->memo = 0;
-          }
-          if (af & CDR_SF_HAS_SEARCH_ATTR) {
-            n_sa = 0;
-            const uint32_t off = a->search_attr_off, cnt = a->search_attr_len;
-            for (uint32_t q = 0; q < cnt && q < CP.sa_cap; q++) gput(sa + n_sa++, gget(gp(B_.kvs) + (off + q)));
-            if (n_sa) x_flags |= CDR_XI_HAS_SEARCH_ATTR;
-            else x_flags &= ~CDR_XI_HAS_SEARCH_ATTR;
-          }
-          x_flags |= CDR_XI_STARTED;
-          // SetHistoryTree (:313-339): branch token on ExecutionInfo, or on the VH for NDC
-          uint64_t lo, hi;
-          cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_BRANCH, e.id, &lo, &hi);
-          X->branch_tree_id = D.run_id;
-          X->branch_id_lo = lo;
-          X->branch_id_hi = hi;
-          x_flags |= isVH ? CDR_XI_VH_BRANCH : CDR_XI_HAS_BRANCH;
-          if (isRS) RS->start_version = e.ver;  // :182-184
+          n_rp = SEL(ok, nrp, n_rp);
+          n_sa = SEL(ok, nsa, n_sa);
+          x_flags = SEL(ok, xf, x_flags);
+          cks_ok = SEL(ok, 0u, cks_ok);
+          x_dt_timeout_value = SEL(ok, a->task_timeout_s, x_dt_timeout_value);
+          x_state = SEL(ok, (int32_t)CDR_STATE_CREATED, x_state);
+          x_close = SEL(ok, (int32_t)CDR_CLOSE_NONE, x_close);
+          x_last_processed = SEL(ok, CDR_EMPTY_EVENT_ID, x_last_processed);
+          dv = SEL(ok, CDR_EMPTY_VERSION, dv);
+          dsched = SEL(ok, CDR_EMPTY_EVENT_ID, dsched);
+          dstart = SEL(ok, CDR_EMPTY_EVENT_ID, dstart);
+          dreq = SEL(ok, EU, dreq);
+          dto = SEL(ok, 0, dto);
           break;
         }
         case CDR_EV_DT_SCHEDULED:  // :186-200 -> mutableStateDecisionTaskManager.go:143-167
-          dv = e.ver;
-          dsched = e.id;
-          dstart = CDR_EMPTY_EVENT_ID;
-          dreq = EU;
-          dto = e.n;
-          datt = e.aux;
-          dsc_ts = e.ts;
-          dst_ts = 0;
-          dorig_ts = e.ts;
+          dv = SEL(mine, e.ver, dv);
+          dsched = SEL(mine, e.id, dsched);
+          dstart = SEL(mine, CDR_EMPTY_EVENT_ID, dstart);
+          dreq = SEL(mine, EU, dreq);
+          dto = SEL(mine, e.n, dto);
+          datt = SEL(mine, e.aux, datt);
+          dsc_ts = SEL(mine, e.ts, dsc_ts);
+          dst_ts = SEL(mine, (int64_t)0, dst_ts);
+          dorig_ts = SEL(mine, e.ts, dorig_ts);
           break;
-        case CDR_EV_DT_STARTED:  // :202-213 -> :200-253
-          if (e.key != dsched) {
-            FAIL(CDR_E_DECISION_NOT_FOUND);
-            break;
-          }
-          if (x_state == CDR_STATE_CREATED) x_state = CDR_STATE_RUNNING;  // always accepted (:56-60)
-          dv = e.ver;
-          dstart = e.id;
-          dreq = e.h;
-          datt = 0;
-          dst_ts = e.ts;
+        case CDR_EV_DT_STARTED: {  // :202-213 -> :200-253
+          const bool f = mine && e.key != dsched;
+          PFAIL(f, CDR_E_DECISION_NOT_FOUND);
+          const bool ok = mine && !f;
+          x_state = SEL(ok && x_state == CDR_STATE_CREATED, (int32_t)CDR_STATE_RUNNING, x_state);  // (:56-60)
+          dv = SEL(ok, e.ver, dv);
+          dstart = SEL(ok, e.id, dstart);
+          dreq = SEL(ok, e.h, dreq);
+          datt = SEL(ok, (int64_t)0, datt);
+          dst_ts = SEL(ok, e.ts, dst_ts);
           break;
+        }
         case CDR_EV_DT_COMPLETED: {  // :215-219 -> :255-262,659-674,789-800
-          dv = CDR_EMPTY_VERSION;
-          dsched = CDR_EMPTY_EVENT_ID;
-          dstart = CDR_EMPTY_EVENT_ID;
-          dreq = EU;
-          dto = 0;
-          datt = 0;
-          dst_ts = 0;
-          dsc_ts = 0;  // OriginalScheduledTimestamp kept
-          x_last_processed = e.aux;
+          dv = SEL(mine, CDR_EMPTY_VERSION, dv);
+          dsched = SEL(mine, CDR_EMPTY_EVENT_ID, dsched);
+          dstart = SEL(mine, CDR_EMPTY_EVENT_ID, dstart);
+          dreq = SEL(mine, EU, dreq);
+          dto = SEL(mine, 0, dto);
+          datt = SEL(mine, (int64_t)0, datt);
+          dst_ts = SEL(mine, (int64_t)0, dst_ts);
+          dsc_ts = SEL(mine, (int64_t)0, dsc_ts);  // OriginalScheduledTimestamp kept
+          x_last_processed = SEL(mine, e.aux, x_last_processed);
           const uint32_t cks = e.h;
-          if (cks && cks != cks_ok) {  // addBinaryCheckSumIfNotExists (mutableStateBuilder.go:1798-1842)
+          const bool chk = mine && cks != 0 && cks != cks_ok;
+          if (__builtin_amdgcn_ballot_w64(chk)) {  // addBinaryCheckSumIfNotExists (mutableStateBuilder.go:1798-1842)
             bool exists = false;
-            for (uint32_t q = 0; q < n_rp; q++) {
+            for (uint32_t q = 0; chk && q < n_rp; q++) {
               const cdr_reset_point p = gget(rp + q);
               exists |= ((p.flags & CDR_RP_HAS_CHECKSUM) ? p.binary_checksum : 0u) == cks;
             }
-            if (!exists) {
-              if (n_rp >= CP.rp_cap) {
-                FAIL(CDR_E_BAD_INPUT);
-                break;
-              }
+            const bool app = chk && !exists;
+            const bool f = app && n_rp >= CP.rp_cap;
+            PFAIL(f, CDR_E_BAD_INPUT);
+            const bool put = app && !f;
+            if (put) {
               const bool resettable = live_chi == 0 && live_can == 0 && live_sig == 0;
               cdr_reset_point p;
               p.binary_checksum = cks;
@@ -744,89 +828,87 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
               p.flags = CDR_RP_HAS_CHECKSUM | CDR_RP_HAS_RUN_ID | CDR_RP_HAS_FIRST_DC_ID | CDR_RP_HAS_CREATED |
                         CDR_RP_HAS_RESETTABLE | (resettable ? CDR_RP_RESETTABLE : 0u);
               p._pad = 0;
-              gput(rp + n_rp++, p);
-              x_flags |= CDR_XI_HAS_RESET_POINTS;
+              gput(rp + n_rp, p);
             }
-            cks_ok = cks;  // the list only grows until the next WorkflowExecutionStarted
+            n_rp += put ? 1u : 0u;
+            x_flags |= put ? CDR_XI_HAS_RESET_POINTS : 0u;
+            cks_ok = SEL(chk && !f, cks, cks_ok);  // the list only grows until the next Started
           }
           break;
         }
         case CDR_EV_DT_TIMED_OUT:  // :221-239 -> FailDecision :635-656 + transient :169-198
         case CDR_EV_DT_FAILED: {   // :241-257
-          const bool inc = type == CDR_EV_DT_FAILED || e.n != CDR_TIMEOUT_SCHEDULE_TO_START;
+          const bool inc = ut == CDR_EV_DT_FAILED || e.n != CDR_TIMEOUT_SCHEDULE_TO_START;
           const int64_t now = B_.now_ns;
-          datt = inc ? datt + 1 : 0;
-          dv = CDR_EMPTY_VERSION;
-          dsched = CDR_EMPTY_EVENT_ID;
-          dstart = CDR_EMPTY_EVENT_ID;
-          dreq = EU;
-          dto = 0;
-          dst_ts = 0;
-          dorig_ts = 0;
-          dsc_ts = inc ? now : 0;
-          if (datt != 0) {  // transient decision: no decision is pending here by construction
-            dv = isRS ? e.ver : (isVH ? curv : CDR_EMPTY_VERSION);
-            dsched = x_next_event;  // NextEventID as of the call's start
-            dto = x_dt_timeout_value;
-            dsc_ts = now;
-          }
+          const int64_t na = inc ? datt + 1 : 0;
+          const bool tr = na != 0;  // transient decision: no decision is pending here by construction
+          dv = SEL(mine, tr ? (isRS ? e.ver : (isVH ? curv : CDR_EMPTY_VERSION)) : CDR_EMPTY_VERSION, dv);
+          dsched = SEL(mine, tr ? x_next_event : CDR_EMPTY_EVENT_ID, dsched);  // NextEventID as of the call's start
+          dstart = SEL(mine, CDR_EMPTY_EVENT_ID, dstart);
+          dreq = SEL(mine, EU, dreq);
+          dto = SEL(mine, tr ? x_dt_timeout_value : 0, dto);
+          dst_ts = SEL(mine, (int64_t)0, dst_ts);
+          dorig_ts = SEL(mine, (int64_t)0, dorig_ts);
+          dsc_ts = SEL(mine, (tr || inc) ? now : (int64_t)0, dsc_ts);
+          datt = SEL(mine, na, datt);
           break;
         }
         case CDR_EV_AT_SCHEDULED: {  // :259-269 -> mutableStateBuilder.go:1982-2028
           const uint32_t aid = (uint32_t)e.key;
           int slot = -1;
-          for (uint32_t j = 0; j < hw_act; j++) {
-            if (A.ld(j, AP_SID) == DEAD_KEY) {
-              if (slot < 0) slot = (int)j;
-            } else {
-              const uint64_t m = (uint64_t)A.ld(j, AP_META);
-              if ((uint32_t)m == aid && (m & META_FLAG(AF_AIDMAP)))  // byActivityID[aid] is overwritten
-                A.st(j, AP_META, (int64_t)(m & ~META_FLAG(AF_AIDMAP)));
-            }
+          for (uint32_t j = 0; j < act_cap; j++) {
+            const bool in = mine && j < hw_act;
+            const int64_t sid = A.ld(j, AP_SID);
+            const uint64_t m = (uint64_t)A.ld(j, AP_META);
+            slot = SEL(in && sid == DEAD_KEY && slot < 0, (int)j, slot);
+            // byActivityID[aid] is overwritten: drop the mapping flag of the old holder
+            const bool clr = in && sid != DEAD_KEY && (uint32_t)m == aid && (m & META_FLAG(AF_AIDMAP));
+            if (clr) A.st(j, AP_META, (int64_t)(m & ~META_FLAG(AF_AIDMAP)));
           }
-          if (slot < 0) {
-            if (hw_act >= act_cap) {
-              FAIL(CDR_E_BAD_INPUT);
-              break;
-            }
-            slot = (int)hw_act++;
+          const bool grow = mine && slot < 0;
+          const bool f = grow && hw_act >= act_cap;
+          PFAIL(f, CDR_E_BAD_INPUT);
+          const bool ok = mine && !f;
+          slot = SEL(grow, (int)hw_act, slot);
+          hw_act += (grow && !f) ? 1u : 0u;
+          if (ok) {
+            const uint32_t j = (uint32_t)slot;
+            const int32_t s2c = (int32_t)e.h, s2s = e.n;
+            A.st(j, AP_SID, e.id);
+            A.st(j, AP_TS2C, e.ts + (int64_t)s2c * NS_PER_S);
+            A.st(j, AP_TALT, e.ts + (int64_t)s2s * NS_PER_S);
+            A.st(j, AP_THB, T_NONE);
+            A.st(j, AP_META, (int64_t)(aid | META_FLAG(AF_AIDMAP)));
+            A.st(j, AP_VER, e.ver);
+            A.st(j, AP_STARTED_ID, CDR_EMPTY_EVENT_ID);
+            A.st(j, AP_STARTED_TIME, 0);
+            A.st(j, AP_CANCEL_ID, CDR_EMPTY_EVENT_ID);
+            A.st(j, AP_ROWS, (int64_t)(k | ((uint64_t)call_first_k << 32)));
+            A.st(j, AP_STC_HB, (int64_t)(((uint64_t)e.key >> 32) | ((uint64_t)e.aux & 0xFFFFFFFF00000000ull)));
+            A.st(j, AP_REQ, 0);
           }
-          const uint32_t j = (uint32_t)slot;
-          const int32_t s2c = (int32_t)e.h, s2s = e.n;
-          A.st(j, AP_SID, e.id);
-          A.st(j, AP_TS2C, e.ts + (int64_t)s2c * NS_PER_S);
-          A.st(j, AP_TALT, e.ts + (int64_t)s2s * NS_PER_S);
-          A.st(j, AP_THB, T_NONE);
-          A.st(j, AP_META, (int64_t)(aid | META_FLAG(AF_AIDMAP)));
-          A.st(j, AP_VER, e.ver);
-          A.st(j, AP_STARTED_ID, CDR_EMPTY_EVENT_ID);
-          A.st(j, AP_STARTED_TIME, 0);
-          A.st(j, AP_CANCEL_ID, CDR_EMPTY_EVENT_ID);
-          A.st(j, AP_ROWS, (int64_t)(k | ((uint64_t)call_first_k << 32)));
-          A.st(j, AP_STC_HB, (int64_t)(((uint64_t)e.key >> 32) | ((uint64_t)e.aux & 0xFFFFFFFF00000000ull)));
-          A.st(j, AP_REQ, 0);
-          act_pick(A, hw_act);
+          act_pick_p(A, hw_act, act_cap, ok);
           break;
         }
         case CDR_EV_AT_STARTED: {  // :271-278 -> :2083-2098
           int slot = -1;
-          for (uint32_t j = 0; j < hw_act; j++)
-            if (A.ld(j, AP_SID) == e.key) slot = (int)j;
-          if (slot < 0) {
-            FAIL(CDR_P_ACTIVITY_STARTED_NIL);  // nil deref in Go
-            break;
+          for (uint32_t j = 0; j < act_cap; j++) slot = SEL(mine && j < hw_act && A.ld(j, AP_SID) == e.key, (int)j, slot);
+          const bool f = mine && slot < 0;
+          PFAIL(f, CDR_P_ACTIVITY_STARTED_NIL);  // nil deref in Go
+          const bool ok = mine && !f;
+          if (ok) {
+            const uint32_t j = (uint32_t)slot;
+            const uint64_t th = (uint64_t)A.ld(j, AP_STC_HB);
+            const int32_t stc = (int32_t)(uint32_t)th, hb = (int32_t)(uint32_t)(th >> 32);
+            A.st(j, AP_VER, e.ver);
+            A.st(j, AP_STARTED_ID, e.id);
+            A.st(j, AP_REQ, (int64_t)e.h);
+            A.st(j, AP_STARTED_TIME, e.ts);  // LastHeartBeatUpdatedTime = StartedTime
+            A.st(j, AP_META, (int64_t)((uint64_t)A.ld(j, AP_META) | META_FLAG(AF_STARTED)));
+            A.st(j, AP_TALT, e.ts + (int64_t)stc * NS_PER_S);
+            A.st(j, AP_THB, hb > 0 ? e.ts + (int64_t)hb * NS_PER_S : T_NONE);
           }
-          const uint32_t j = (uint32_t)slot;
-          const uint64_t th = (uint64_t)A.ld(j, AP_STC_HB);
-          const int32_t stc = (int32_t)(uint32_t)th, hb = (int32_t)(uint32_t)(th >> 32);
-          A.st(j, AP_VER, e.ver);
-          A.st(j, AP_STARTED_ID, e.id);
-          A.st(j, AP_REQ, (int64_t)e.h);
-          A.st(j, AP_STARTED_TIME, e.ts);  // LastHeartBeatUpdatedTime = StartedTime
-          A.st(j, AP_META, (int64_t)((uint64_t)A.ld(j, AP_META) | META_FLAG(AF_STARTED)));
-          A.st(j, AP_TALT, e.ts + (int64_t)stc * NS_PER_S);
-          A.st(j, AP_THB, hb > 0 ? e.ts + (int64_t)hb * NS_PER_S : T_NONE);
-          act_pick(A, hw_act);
+          act_pick_p(A, hw_act, act_cap, ok);
           break;
         }
         case CDR_EV_AT_COMPLETED:  // :280-305,312-319 -> DeleteActivity :1247-1269
@@ -834,119 +916,126 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
         case CDR_EV_AT_TIMED_OUT:
         case CDR_EV_AT_CANCELED: {
           int slot = -1;
-          for (uint32_t j = 0; j < hw_act; j++)
-            if (A.ld(j, AP_SID) == e.key) slot = (int)j;
-          if (slot < 0) {
-            FAIL(CDR_E_ACTIVITY_NOT_FOUND);
-            break;
-          }
-          const uint64_t m = (uint64_t)A.ld((uint32_t)slot, AP_META);
-          const uint32_t aid = (uint32_t)m;
-          A.st((uint32_t)slot, AP_SID, DEAD_KEY);
-          A.st((uint32_t)slot, AP_META, (int64_t)(m & ~META_FLAG(AF_AIDMAP)));
-          bool found = (m & META_FLAG(AF_AIDMAP)) != 0;
-          if (!found)
-            for (uint32_t j = 0; j < hw_act; j++) {
-              if (A.ld(j, AP_SID) == DEAD_KEY) continue;
-              const uint64_t mj = (uint64_t)A.ld(j, AP_META);
-              if ((uint32_t)mj == aid && (mj & META_FLAG(AF_AIDMAP))) {
-                A.st(j, AP_META, (int64_t)(mj & ~META_FLAG(AF_AIDMAP)));
-                found = true;
+          for (uint32_t j = 0; j < act_cap; j++) slot = SEL(mine && j < hw_act && A.ld(j, AP_SID) == e.key, (int)j, slot);
+          const bool f = mine && slot < 0;
+          PFAIL(f, CDR_E_ACTIVITY_NOT_FOUND);
+          bool ok = mine && !f;
+          bool found = false;
+          if (ok) {
+            const uint64_t m = (uint64_t)A.ld((uint32_t)slot, AP_META);
+            const uint32_t aid = (uint32_t)m;
+            A.st((uint32_t)slot, AP_SID, DEAD_KEY);
+            A.st((uint32_t)slot, AP_META, (int64_t)(m & ~META_FLAG(AF_AIDMAP)));
+            found = (m & META_FLAG(AF_AIDMAP)) != 0;
+            if (!found)
+              for (uint32_t j = 0; j < hw_act; j++) {
+                if (A.ld(j, AP_SID) == DEAD_KEY) continue;
+                const uint64_t mj = (uint64_t)A.ld(j, AP_META);
+                if ((uint32_t)mj == aid && (mj & META_FLAG(AF_AIDMAP))) {
+                  A.st(j, AP_META, (int64_t)(mj & ~META_FLAG(AF_AIDMAP)));
+                  found = true;
+                }
               }
-            }
-          if (!found) {
-            FAIL(CDR_E_ACTIVITY_ID_NOT_FOUND);
-            break;
           }
-          act_pick(A, hw_act);
+          const bool f2 = ok && !found;
+          PFAIL(f2, CDR_E_ACTIVITY_ID_NOT_FOUND);
+          ok = ok && !f2;
+          act_pick_p(A, hw_act, act_cap, ok);
           break;
         }
         case CDR_EV_AT_CANCEL_REQUESTED: {  // :307-310 -> :2264-2285
           const uint32_t aid = (uint32_t)e.key;
           int slot = -1;
-          for (uint32_t j = 0; j < hw_act; j++) {
-            if (A.ld(j, AP_SID) == DEAD_KEY) continue;
+          for (uint32_t j = 0; j < act_cap; j++) {
+            const int64_t sid = A.ld(j, AP_SID);
             const uint64_t mj = (uint64_t)A.ld(j, AP_META);
-            if ((uint32_t)mj == aid && (mj & META_FLAG(AF_AIDMAP))) slot = (int)j;
+            slot = SEL(mine && j < hw_act && sid != DEAD_KEY && (uint32_t)mj == aid && (mj & META_FLAG(AF_AIDMAP)),
+                       (int)j, slot);
           }
-          if (slot < 0) {
-            FAIL(CDR_E_MISSING_ACTIVITY_INFO);
-            break;
+          const bool f = mine && slot < 0;
+          PFAIL(f, CDR_E_MISSING_ACTIVITY_INFO);
+          if (mine && !f) {
+            const uint32_t j = (uint32_t)slot;
+            A.st(j, AP_VER, e.ver);
+            A.st(j, AP_META, (int64_t)((uint64_t)A.ld(j, AP_META) | META_FLAG(AF_CANCEL)));
+            A.st(j, AP_CANCEL_ID, e.id);
           }
-          const uint32_t j = (uint32_t)slot;
-          A.st(j, AP_VER, e.ver);
-          A.st(j, AP_META, (int64_t)((uint64_t)A.ld(j, AP_META) | META_FLAG(AF_CANCEL)));
-          A.st(j, AP_CANCEL_ID, e.id);
           break;
         }
         case CDR_EV_TIMER_STARTED: {  // :324-332 -> :2877-2900
           const uint32_t tid = (uint32_t)e.key;
           int slot = -1, free_slot = -1;
-          for (uint32_t j = 0; j < hw_tim; j++) {
-            if (T.ld(j, TP_SID) == DEAD_KEY) {
-              if (free_slot < 0) free_slot = (int)j;
-            } else if ((uint32_t)T.ld(j, TP_TID_TASK) == tid) {
-              slot = (int)j;
-            }
+          for (uint32_t j = 0; j < tim_cap; j++) {
+            const bool in = mine && j < hw_tim;
+            const int64_t sid = T.ld(j, TP_SID);
+            const uint32_t tj = (uint32_t)T.ld(j, TP_TID_TASK);
+            free_slot = SEL(in && sid == DEAD_KEY && free_slot < 0, (int)j, free_slot);
+            slot = SEL(in && sid != DEAD_KEY && tj == tid, (int)j, slot);
           }
-          if (slot < 0) slot = free_slot;
-          if (slot < 0) {
-            if (hw_tim >= tim_cap) {
-              FAIL(CDR_E_BAD_INPUT);
-              break;
-            }
-            slot = (int)hw_tim++;
+          slot = slot < 0 ? free_slot : slot;
+          const bool grow = mine && slot < 0;
+          const bool f = grow && hw_tim >= tim_cap;
+          PFAIL(f, CDR_E_BAD_INPUT);
+          const bool ok = mine && !f;
+          slot = SEL(grow, (int)hw_tim, slot);
+          hw_tim += (grow && !f) ? 1u : 0u;
+          if (ok) {
+            const uint32_t j = (uint32_t)slot;
+            T.st(j, TP_SID, e.id);
+            T.st(j, TP_TID_TASK, (int64_t)tid);  // TaskID = TimerTaskStatusNone
+            T.st(j, TP_EXPIRY, e.ts + e.aux * NS_PER_S);
+            T.st(j, TP_VER, e.ver);
           }
-          const uint32_t j = (uint32_t)slot;
-          T.st(j, TP_SID, e.id);
-          T.st(j, TP_TID_TASK, (int64_t)tid);  // TaskID = TimerTaskStatusNone
-          T.st(j, TP_EXPIRY, e.ts + e.aux * NS_PER_S);
-          T.st(j, TP_VER, e.ver);
-          tim_pick(T, hw_tim);
+          tim_pick_p(T, hw_tim, tim_cap, ok);
           break;
         }
         case CDR_EV_TIMER_FIRED:       // :334-341
         case CDR_EV_TIMER_CANCELED: {  // :343-350
           const uint32_t tid = (uint32_t)e.key;
-          for (uint32_t j = 0; j < hw_tim; j++)
-            if (T.ld(j, TP_SID) != DEAD_KEY && (uint32_t)T.ld(j, TP_TID_TASK) == tid) T.st(j, TP_SID, DEAD_KEY);
-          tim_pick(T, hw_tim);
+          for (uint32_t j = 0; j < tim_cap; j++) {
+            const bool hit = mine && j < hw_tim && T.ld(j, TP_SID) != DEAD_KEY && (uint32_t)T.ld(j, TP_TID_TASK) == tid;
+            if (hit) T.st(j, TP_SID, DEAD_KEY);
+          }
+          tim_pick_p(T, hw_tim, tim_cap, mine);
           break;
         }
         case CDR_EV_CHILD_INITIATED: {  // :355-371 -> :3256-3280
-          const int slot = alloc_initiated(chi, hw_chi, CP.child_cap);
-          if (slot < 0) {
-            FAIL(CDR_E_BAD_INPUT);
-            break;
+          int slot = -1;
+          if (mine) slot = alloc_initiated(chi, hw_chi, CP.child_cap);
+          const bool f = mine && slot < 0;
+          PFAIL(f, CDR_E_BAD_INPUT);
+          const bool ok = mine && !f;
+          if (ok) {
+            cdr_child_info c;
+            c.version = e.ver;
+            c.initiated_id = e.id;
+            c.initiated_event_batch_id = call_first_id;
+            c.started_id = CDR_EMPTY_EVENT_ID;
+            uint64_t lo, hi;
+            cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_CHILD_REQ, e.id, &lo, &hi);
+            c.create_request_lo = lo;
+            c.create_request_hi = hi;
+            c.started_workflow_id = e.h;
+            c.started_run_id = 0;
+            c.domain_name = (uint32_t)e.key;
+            c.workflow_type = (uint32_t)e.aux;
+            c.parent_close_policy = e.n;
+            c._pad = 0;
+            gput(chi + slot, c);
           }
-          cdr_child_info c;
-          c.version = e.ver;
-          c.initiated_id = e.id;
-          c.initiated_event_batch_id = call_first_id;
-          c.started_id = CDR_EMPTY_EVENT_ID;
-          uint64_t lo, hi;
-          cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_CHILD_REQ, e.id, &lo, &hi);
-          c.create_request_lo = lo;
-          c.create_request_hi = hi;
-          c.started_workflow_id = e.h;
-          c.started_run_id = 0;
-          c.domain_name = (uint32_t)e.key;
-          c.workflow_type = (uint32_t)e.aux;
-          c.parent_close_policy = e.n;
-          c._pad = 0;
-          gput(chi + slot, c);
-          live_chi++;
-          if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
+          live_chi += ok ? 1u : 0u;
+          PFAIL(ok && (e.tf & CDR_SEF_DOMAIN_MISSING), CDR_E_DOMAIN_NOT_FOUND);
           break;
         }
         case CDR_EV_CHILD_STARTED: {  // :378-381 -> :3312-3325
-          const int slot = find_initiated(chi, hw_chi, e.key);
-          if (slot < 0) {
-            FAIL(CDR_P_CHILD_STARTED_NIL);
-            break;
+          int slot = -1;
+          if (mine) slot = find_initiated(chi, hw_chi, e.key);
+          const bool f = mine && slot < 0;
+          PFAIL(f, CDR_P_CHILD_STARTED_NIL);
+          if (mine && !f) {
+            chi[slot].started_id = e.id;
+            chi[slot].started_run_id = e.h;
           }
-          chi[slot].started_id = e.id;
-          chi[slot].started_run_id = e.h;
           break;
         }
         case CDR_EV_CHILD_START_FAILED:
@@ -955,71 +1044,72 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
         case CDR_EV_CHILD_CANCELED:
         case CDR_EV_CHILD_TIMED_OUT:
         case CDR_EV_CHILD_TERMINATED: {  // DeletePendingChildExecution :1138-1144
-          const int slot = find_initiated(chi, hw_chi, e.key);
-          if (slot >= 0) {
-            chi[slot].initiated_id = DEAD_KEY;
-            live_chi--;
-          }
+          int slot = -1;
+          if (mine) slot = find_initiated(chi, hw_chi, e.key);
+          if (slot >= 0) chi[slot].initiated_id = DEAD_KEY;
+          live_chi -= slot >= 0 ? 1u : 0u;
           break;
         }
         case CDR_EV_RCE_INITIATED: {  // :408-427 -> :2577-2596
-          const int slot = alloc_initiated(can, hw_can, CP.cancel_cap);
-          if (slot < 0) {
-            FAIL(CDR_E_BAD_INPUT);
-            break;
+          int slot = -1;
+          if (mine) slot = alloc_initiated(can, hw_can, CP.cancel_cap);
+          const bool f = mine && slot < 0;
+          PFAIL(f, CDR_E_BAD_INPUT);
+          const bool ok = mine && !f;
+          if (ok) {
+            cdr_cancel_info c;
+            c.version = e.ver;
+            c.initiated_event_batch_id = call_first_id;
+            c.initiated_id = e.id;
+            uint64_t lo, hi;
+            cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_CANCEL_REQ, e.id, &lo, &hi);
+            c.cancel_request_lo = lo;
+            c.cancel_request_hi = hi;
+            gput(can + slot, c);
           }
-          cdr_cancel_info c;
-          c.version = e.ver;
-          c.initiated_event_batch_id = call_first_id;
-          c.initiated_id = e.id;
-          uint64_t lo, hi;
-          cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_CANCEL_REQ, e.id, &lo, &hi);
-          c.cancel_request_lo = lo;
-          c.cancel_request_hi = hi;
-          gput(can + slot, c);
-          live_can++;
-          if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
+          live_can += ok ? 1u : 0u;
+          PFAIL(ok && (e.tf & CDR_SEF_DOMAIN_MISSING), CDR_E_DOMAIN_NOT_FOUND);
           break;
         }
         case CDR_EV_RCE_FAILED:
         case CDR_EV_EXT_CANCEL_REQUESTED: {  // DeletePendingRequestCancel :1147-1153
-          const int slot = find_initiated(can, hw_can, e.key);
-          if (slot >= 0) {
-            can[slot].initiated_id = DEAD_KEY;
-            live_can--;
-          }
+          int slot = -1;
+          if (mine) slot = find_initiated(can, hw_can, e.key);
+          if (slot >= 0) can[slot].initiated_id = DEAD_KEY;
+          live_can -= slot >= 0 ? 1u : 0u;
           break;
         }
         case CDR_EV_SE_INITIATED: {  // :439-458 -> :2701-2723
-          const int slot = alloc_initiated(sig, hw_sig, CP.signal_cap);
-          if (slot < 0) {
-            FAIL(CDR_E_BAD_INPUT);
-            break;
+          int slot = -1;
+          if (mine) slot = alloc_initiated(sig, hw_sig, CP.signal_cap);
+          const bool f = mine && slot < 0;
+          PFAIL(f, CDR_E_BAD_INPUT);
+          const bool ok = mine && !f;
+          if (ok) {
+            cdr_signal_info c;
+            c.version = e.ver;
+            c.initiated_event_batch_id = call_first_id;
+            c.initiated_id = e.id;
+            uint64_t lo, hi;
+            cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_SIGNAL_REQ, e.id, &lo, &hi);
+            c.signal_request_lo = lo;
+            c.signal_request_hi = hi;
+            c.signal_name = e.h;
+            c.input = (uint32_t)((uint64_t)e.aux >> 32);
+            c.control = (uint32_t)e.aux;
+            c._pad = 0;
+            gput(sig + slot, c);
           }
-          cdr_signal_info c;
-          c.version = e.ver;
-          c.initiated_event_batch_id = call_first_id;
-          c.initiated_id = e.id;
-          uint64_t lo, hi;
-          cdr_uuid(B_.uuid_seed, D.wf_key, CDR_UUID_SIGNAL_REQ, e.id, &lo, &hi);
-          c.signal_request_lo = lo;
-          c.signal_request_hi = hi;
-          c.signal_name = e.h;
-          c.input = (uint32_t)((uint64_t)e.aux >> 32);
-          c.control = (uint32_t)e.aux;
-          c._pad = 0;
-          gput(sig + slot, c);
-          live_sig++;
-          if (e.tf & CDR_SEF_DOMAIN_MISSING) FAIL(CDR_E_DOMAIN_NOT_FOUND);
+          live_sig += ok ? 1u : 0u;
+          PFAIL(ok && (e.tf & CDR_SEF_DOMAIN_MISSING), CDR_E_DOMAIN_NOT_FOUND);
           break;
         }
         case CDR_EV_SE_FAILED:
         case CDR_EV_EXT_SIGNALED: {  // DeletePendingSignal :1156-1162
-          const int slot = find_initiated(sig, hw_sig, e.key);
-          if (slot >= 0) {
-            sig[slot].initiated_id = DEAD_KEY;
-            live_sig--;
-          }
+          int slot = -1;
+          if (mine) slot = find_initiated(sig, hw_sig, e.key);
+          if (slot >= 0) sig[slot].initiated_id = DEAD_KEY;
+          live_sig -= slot >= 0 ? 1u : 0u;
           break;
         }
         case CDR_EV_AT_REQ_CANCEL_FAILED:
@@ -1027,10 +1117,10 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
         case CDR_EV_MARKER_RECORDED:
           break;
         case CDR_EV_WF_SIGNALED:  // :473-476
-          x_signals++;
+          x_signals += mine ? 1 : 0;
           break;
         case CDR_EV_WF_CANCEL_REQUESTED:  // :478-481
-          x_flags |= CDR_XI_CANCEL_REQUESTED;
+          x_flags |= mine ? CDR_XI_CANCEL_REQUESTED : 0u;
           break;
         case CDR_EV_WF_COMPLETED:
         case CDR_EV_WF_FAILED:
@@ -1042,54 +1132,60 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
                          : ut == CDR_EV_WF_TIMED_OUT ? CDR_CLOSE_TIMED_OUT
                          : ut == CDR_EV_WF_CANCELED  ? CDR_CLOSE_CANCELED
                                                      : CDR_CLOSE_TERMINATED;
-          if (!transition_ok(x_state, x_close, CDR_STATE_COMPLETED, cs)) {
-            FAIL(CDR_E_INVALID_STATE_TRANSITION);
-            break;
-          }
-          x_state = CDR_STATE_COMPLETED;
-          x_close = cs;
-          x_completion_batch = call_first_id;
+          const bool f = mine && !transition_ok(x_state, x_close, CDR_STATE_COMPLETED, cs);
+          PFAIL(f, CDR_E_INVALID_STATE_TRANSITION);
+          const bool ok = mine && !f;
+          x_state = SEL(ok, (int32_t)CDR_STATE_COMPLETED, x_state);
+          x_close = SEL(ok, (int32_t)cs, x_close);
+          x_completion_batch = SEL(ok, call_first_id, x_completion_batch);
           break;
         }
         case CDR_EV_UPSERT_SA: {  // :533-535 -> :2746-2768
-          const uint64_t off = (uint64_t)e.aux;
-          const uint32_t cnt = e.h;
-          for (uint32_t q = 0; q < cnt; q++) {
-            const cdr_kv kv = gget(gp(B_.kvs) + (off + q));
-            bool found = false;
-            for (uint32_t j = 0; j < n_sa; j++)
-              if (sa[j].key == kv.key) {
-                sa[j].value = kv.value;
-                found = true;
-              }
-            if (!found && n_sa < CP.sa_cap) gput(sa + n_sa++, kv);
+          uint32_t nsa = n_sa;
+          if (mine) {
+            const uint64_t off = (uint64_t)e.aux;
+            const uint32_t cnt = e.h, cap = CP.sa_cap;
+            for (uint32_t q = 0; q < cnt; q++) {
+              const cdr_kv kv = gget(gp(B_.kvs) + (off + q));
+              bool found = false;
+              for (uint32_t j = 0; j < nsa; j++)
+                if (sa[j].key == kv.key) {
+                  sa[j].value = kv.value;
+                  found = true;
+                }
+              if (!found && nsa < cap) gput(sa + nsa++, kv);
+            }
           }
-          x_flags |= CDR_XI_HAS_SEARCH_ATTR;
+          n_sa = SEL(mine, nsa, n_sa);
+          x_flags |= mine ? CDR_XI_HAS_SEARCH_ATTR : 0u;
           break;
         }
         case CDR_EV_WF_CONTINUED_AS_NEW: {  // :537-595
-          const int32_t nr = D.newrun;
-          if (nr < 0 || call_idx != D.newrun_call || gp(B_.wfs)[nr].ev_len == 0) {
-            FAIL(CDR_E_NEWRUN_HISTORY_EMPTY);
-            break;
+          bool empty = true;
+          if (mine) {
+            const int32_t nr = D.newrun;
+            empty = nr < 0 || call_idx != D.newrun_call || gp(B_.wfs)[nr].ev_len == 0;
           }
-          newrun_applied = true;  // the new run replays in its own lane; k_finalize joins
-          if (!transition_ok(x_state, x_close, CDR_STATE_COMPLETED, CDR_CLOSE_CONTINUED_AS_NEW)) {
-            FAIL(CDR_E_INVALID_STATE_TRANSITION);
-            break;
-          }
-          x_state = CDR_STATE_COMPLETED;
-          x_close = CDR_CLOSE_CONTINUED_AS_NEW;
-          x_completion_batch = call_first_id;
+          const bool f = mine && empty;
+          PFAIL(f, CDR_E_NEWRUN_HISTORY_EMPTY);
+          const bool ap = mine && !f;
+          newrun_applied |= ap;  // the new run replays in its own lane; k_finalize joins
+          const bool f2 = ap && !transition_ok(x_state, x_close, CDR_STATE_COMPLETED, CDR_CLOSE_CONTINUED_AS_NEW);
+          PFAIL(f2, CDR_E_INVALID_STATE_TRANSITION);
+          const bool ok = ap && !f2;
+          x_state = SEL(ok, (int32_t)CDR_STATE_COMPLETED, x_state);
+          x_close = SEL(ok, (int32_t)CDR_CLOSE_CONTINUED_AS_NEW, x_close);
+          x_completion_batch = SEL(ok, call_first_id, x_completion_batch);
           break;
         }
         default:
-          FAIL(CDR_E_UNKNOWN_EVENT_TYPE);  // :597-599
+          PFAIL(mine, CDR_E_UNKNOWN_EVENT_TYPE);  // :597-599
           break;
       }
     }
   }
-#undef FAIL
+#undef PFAIL
+#undef SEL
   // ---- end of the last call
   if (len > 0 && (err == CDR_OK || stop_at_call_end)) {
     if (isRS) {
