@@ -94,6 +94,7 @@ class DeviceBatch:
         self.h_sc_off = np.zeros(info.n_slices, np.uint64)
         self.h_sc_act = np.zeros(info.n_slices, np.uint32)
         self.h_sc_tim = np.zeros(info.n_slices, np.uint32)
+        self.h_sflags = np.zeros(info.n_slices, np.uint32)
         self.h_arena = np.empty(max(1, info.arena_words), np.uint64)
         self.h_wfs = (abi.CdrWfDesc * info.n_entries)()
         self.h_caps = (abi.CdrWfCaps * info.n_entries)()
@@ -106,6 +107,7 @@ class DeviceBatch:
         s.arena = self.h_arena.ctypes.data
         s.slice_scratch_off, s.slice_act_slots, s.slice_tim_slots = (
             self.h_sc_off.ctypes.data, self.h_sc_act.ctypes.data, self.h_sc_tim.ctypes.data)
+        s.slice_flags = self.h_sflags.ctypes.data
         meta = abi.CdrBatch()
         threads = min(32, os.cpu_count() or 8)
         rc = L.cdr_synth_sliced_fill(C.byref(p), C.byref(s), self.h_wfs, self.h_caps, self.h_kvs.ctypes.data,
@@ -134,8 +136,9 @@ class DeviceBatch:
         db.ev.slice_scratch_off = up(self.h_sc_off)
         db.ev.slice_act_slots = up(self.h_sc_act)
         db.ev.slice_tim_slots = up(self.h_sc_tim)
-        L.cdr_plan_scratch(self.h_caps, self.h_lane.ctypes.data, info.n_slices, None, None, None,
-                           C.byref(sc_words := C.c_uint64()))
+        db.ev.slice_flags = up(self.h_sflags)
+        L.cdr_plan_scratch(self.h_caps, self.h_lane.ctypes.data, info.n_slices, None, None, None, None,
+                           C.byref(sc_words := C.c_uint64()), None)
         self.scratch_t = torch.zeros(max(8, sc_words.value * 8), dtype=torch.uint8, device=dev)
         db.scratch = self.scratch_t.data_ptr()
         db.wfs, db.caps = up_ct(self.h_wfs), up_ct(self.h_caps)
@@ -143,6 +146,8 @@ class DeviceBatch:
         db.n_wfs = info.n_entries
         db.max_act_slots = int(self.h_sc_act.max()) if len(self.h_sc_act) else 0
         db.max_tim_slots = int(self.h_sc_tim.max()) if len(self.h_sc_tim) else 0
+        self.n_fast = int(((self.h_sflags & abi.SLICE_FAST) != 0).sum())
+        db.n_fast_slices = self.n_fast
         db.empty_uuid = meta.empty_uuid
         db.cluster = meta.cluster
         db.now_ns = meta.now_ns
@@ -259,6 +264,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0x5EED0002)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stream-peak", action="store_true")
+    ap.add_argument("--no-fast-path", action="store_true", help="replay every slice with the general kernel")
     args = ap.parse_args()
 
     import torch
@@ -274,11 +280,14 @@ def main():
     ctx = L.cdr_create(torch.cuda.current_device())
     if not ctx:
         raise SystemExit("cdr_create failed (no GPU?) — the engine has no CPU fallback")
+    if args.no_fast_path:
+        L.cdr_set_fast_path(ctx, 0)
 
     total = args.wfs * world
     mine, _ = assign_shards(total, world, rank)
     log(f"[rank {rank}] {len(mine)} of {total} workflows (shard->GPU greedy over {NUM_SHARDS} shards)")
     db = DeviceBatch(torch, args.config, mine, args.seed)
+    log(f"[rank {rank}] {db.n_fast} of {db.info.n_slices} slices on the fast-path kernel")
     log(f"[rank {rank}] packed {db.n_events:,} events in {db.pack_s:.2f}s (host SoA), H2D {db.h2d_s:.2f}s "
         f"({db.in_bytes / 1e9:.2f} GB in, {db.out_bytes / 1e9:.2f} GB out buffers)")
     stream = torch.cuda.current_stream().cuda_stream

@@ -228,10 +228,14 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   db.ev.slab = (const uint8_t*)up(slab.data(), slab.size());
   db.ev.arena = (const uint64_t*)up(arena.data(), arena.size() * 8);
   std::vector<uint64_t> sc_off(ns);
-  std::vector<uint32_t> sc_act(ns), sc_tim(ns);
+  std::vector<uint32_t> sc_act(ns), sc_tim(ns), sflags(ns);
   uint64_t sc_words = 0;
-  rc = cdr_plan_scratch(caps, lane.data(), ns, sc_off.data(), sc_act.data(), sc_tim.data(), &sc_words);
+  uint32_t n_fast = 0;
+  rc = cdr_plan_scratch(caps, lane.data(), ns, sc_off.data(), sc_act.data(), sc_tim.data(), sflags.data(), &sc_words,
+                        &n_fast);
   if (rc) return rc;
+  db.ev.slice_flags = (const uint32_t*)up(sflags.data(), ns * 4ull);
+  db.n_fast_slices = n_fast;
   db.ev.slice_scratch_off = (const uint64_t*)up(sc_off.data(), ns * 8ull);
   db.ev.slice_act_slots = (const uint32_t*)up(sc_act.data(), ns * 4ull);
   db.ev.slice_tim_slots = (const uint32_t*)up(sc_tim.data(), ns * 4ull);

@@ -71,8 +71,9 @@ namespace cdr_internal {
 
 uint32_t arena_words_for(uint32_t type) { return ::arena_words_for(type); }
 
-void caps_one(const cdr_event* ev, uint64_t n, cdr_wf_caps* out) {
+void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* out) {
   cdr_wf_caps c{};
+  bool fast = builder != CDR_BUILDER_2DC && n > 0 && ev[0].type == CDR_EV_WF_STARTED;
   bool have_ver = false;
   int64_t last_ver = 0;
   uint32_t vh = 0;
@@ -85,6 +86,7 @@ void caps_one(const cdr_event* ev, uint64_t n, cdr_wf_caps* out) {
     if (e.type == CDR_EV_AT_COMPLETED || e.type == CDR_EV_AT_FAILED || e.type == CDR_EV_AT_TIMED_OUT ||
         e.type == CDR_EV_AT_CANCELED)
       live = std::max<int64_t>(0, live - 1);
+    fast = fast && e.type < 64 && (CDR_FAST_TYPES & (1ull << e.type)) && (k == 0 || e.type != CDR_EV_WF_STARTED);
     if (!have_ver || e.version > last_ver) {
       vh++;
       last_ver = e.version;
@@ -123,6 +125,7 @@ void caps_one(const cdr_event* ev, uint64_t n, cdr_wf_caps* out) {
   c.vh_cap = vh;
   c.act_live = (uint32_t)live_max;
   c.timer_live = c.timer_cap;
+  c.flags = (fast && live_max <= 1) ? CDR_CAP_FAST : 0u;
   *out = c;
 }
 
@@ -295,7 +298,7 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
       }
     }
     cdr_wf_caps c{};
-    cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, &c);
+    cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c);
     c.act_off = t.act;
     t.act += c.act_cap;
     c.timer_off = t.timer;
@@ -346,23 +349,32 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
 }
 
 int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n_slices, uint64_t* scratch_off,
-                     uint32_t* act_slots, uint32_t* tim_slots, uint64_t* total_words) {
+                     uint32_t* act_slots, uint32_t* tim_slots, uint32_t* slice_flags, uint64_t* total_words,
+                     uint32_t* n_fast) {
   if (!caps || !lane_wf || !total_words) return CDR_API_EINVAL;
   uint64_t off = 0;
+  uint32_t nf = 0;
   for (uint32_t s = 0; s < n_slices; s++) {
-    uint32_t a = 0, t = 0;
+    uint32_t a = 0, t = 0, lanes = 0;
+    bool fast = true;
     for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
       const int32_t w = lane_wf[(size_t)s * CDR_SLICE_WIDTH + l];
       if (w < 0) continue;
       a = std::max(a, caps[w].act_live);
       t = std::max(t, caps[w].timer_live);
+      fast = fast && (caps[w].flags & CDR_CAP_FAST);
+      lanes++;
     }
+    fast = fast && lanes > 0;
+    nf += fast ? 1u : 0u;
     if (scratch_off) scratch_off[s] = off;
     if (act_slots) act_slots[s] = a;
     if (tim_slots) tim_slots[s] = t;
+    if (slice_flags) slice_flags[s] = fast ? CDR_SLICE_FAST : 0u;
     off += ((uint64_t)a * CDR_ACT_PLANES + (uint64_t)t * CDR_TIM_PLANES) * CDR_SLICE_WIDTH;
   }
   *total_words = off;
+  if (n_fast) *n_fast = nf;
   return CDR_API_OK;
 }
 

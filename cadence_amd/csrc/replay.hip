@@ -440,6 +440,8 @@ struct cdr_launch {
   cdr_dev_batch B;
   cdr_out O;
   uint32_t la, lt;  // activity / user-timer working slots per lane held in LDS
+  uint32_t fast;    // CDR_SLICE_FAST slices go to k_replay_fast (else every slice here)
+  uint32_t _pad;
 };
 #define AS4 __attribute__((address_space(4)))
 __device__ __forceinline__ const AS4 cdr_launch* KA() {
@@ -471,6 +473,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   const uint32_t tim_cap = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_tim_slots[s]);
   const uint32_t la = KA()->la, lt = KA()->lt;
   if ((act_cap <= la && tim_cap <= lt) != LDS) return;
+  if (KA()->fast && (__builtin_amdgcn_readfirstlane(KA()->B.ev.slice_flags[s]) & CDR_SLICE_FAST)) return;
   const uint64_t row0_ = KA()->B.ev.slice_row0[s];
   const uint64_t row0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(row0_ >> 32)) << 32) |
                         __builtin_amdgcn_readfirstlane((uint32_t)row0_);
@@ -1354,6 +1357,8 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
 #undef O_
 }
 
+#include "replay_fast.inc"
+
 // Per-workflow table epilogue: move live rows to the front in key order (the
 // canonical order of the Go maps' keys), sort the SearchAttributes map by key, and
 // turn high-water marks into live counts.
@@ -1412,6 +1417,7 @@ __global__ void k_finalize(cdr_dev_batch B, cdr_out O) {
 // ============================================================ host API
 struct cdr_ctx {
   int device;
+  int fast = 1;  // cdr_set_fast_path
   hipEvent_t ev[4];
   bool timed;
   // optional per-launch timing ring (bench): event pairs around every replay kernel
@@ -1445,6 +1451,13 @@ cdr_ctx* cdr_create(int device) {
   return c;
 }
 
+int cdr_set_fast_path(cdr_ctx* c, int enable) {
+  if (!c) return CDR_API_EINVAL;
+  const int old = c->fast;
+  c->fast = enable ? 1 : 0;
+  return old;
+}
+
 void cdr_destroy(cdr_ctx* c) {
   if (!c) return;
   for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
@@ -1463,12 +1476,18 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const size_t lds = (size_t)(la * CDR_ACT_PLANES + lt * CDR_TIM_PLANES) * CDR_SLICE_WIDTH * sizeof(uint64_t);
   const bool spill = in->max_act_slots > la || in->max_tim_slots > lt;
   const uint32_t blocks = in->ev.n_slices;
+  const bool fast = c->fast && in->n_fast_slices > 0;
+  const bool general = !fast || in->n_fast_slices < in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
-  cdr_launch L{*in, *out, la, lt};
-  if (blocks) hipLaunchKernelGGL(k_replay<true>, dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, L);
+  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, 0u};
+  if (blocks && fast)
+    hipLaunchKernelGGL(k_replay_fast, dim3(blocks), dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, st, L);
   HIPCHK(hipGetLastError());
-  if (blocks && spill) hipLaunchKernelGGL(k_replay<false>, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
+  if (blocks && general) hipLaunchKernelGGL(k_replay<true>, dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, L);
+  HIPCHK(hipGetLastError());
+  if (blocks && general && spill)
+    hipLaunchKernelGGL(k_replay<false>, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used + 1] : c->ev[1], st));
   if (ring) {

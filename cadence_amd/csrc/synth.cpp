@@ -455,12 +455,14 @@ struct Gen {
   }
 
   // one injected fault (error-path coverage)
-  void inject_fault() {
+  void inject_fault(uint32_t mask) {
     std::vector<cdr_event>& ev = o.ev;
     if (ev.size() < 4) return;
     size_t k = 2 + r.below((uint32_t)ev.size() - 2);
     cdr_event& e = ev[k];
-    switch (r.below(8)) {
+    uint32_t kind = r.below(8);
+    while (mask && !(mask & (1u << kind))) kind = (kind + 1) & 7;
+    switch (kind) {
       case 0:
         e.type = 42 + r.below(10);  // unknown event type
         break;
@@ -552,7 +554,7 @@ void gen_one(const cdr_synth_params& P, uint32_t local, WfOut& o) {
     for (auto& e : o.ev) e.version = CDR_EMPTY_VERSION;
     for (auto& e : o.newrun) e.version = CDR_EMPTY_VERSION;
   }
-  if (P.error_rate > 0 && r2.uni() < P.error_rate) g.inject_fault();
+  if (P.error_rate > 0 && r2.uni() < P.error_rate) g.inject_fault(P.fault_kinds);
   o.d.wf_key = cdr_mix64(P.seed ^ (0xC0FFEEull + w));
   o.d.domain_id = H_DOMAIN0 + 15;
   o.d.workflow_id = wf_handle(w, 0);
@@ -632,8 +634,9 @@ void size_pass(const cdr_synth_params& P, Sizes& S, int threads, bool want_caps 
     S.n_kv[w] = (uint32_t)o.kvs.size();
     S.n_rp[w] = (uint32_t)o.rps.size();
     if (want_caps) {
-      cdr_internal::caps_one(o.ev.data(), o.ev.size(), &S.cap_ev[w]);
-      cdr_internal::caps_one(o.newrun.data(), o.newrun.size(), &S.cap_nr[w]);
+      cdr_internal::caps_one(o.ev.data(), o.ev.size(), o.d.builder, &S.cap_ev[w]);
+      cdr_internal::caps_one(o.newrun.data(), o.newrun.size(),
+                             o.newrun_ndc ? (uint32_t)CDR_BUILDER_NDC : (uint32_t)CDR_BUILDER_2DC, &S.cap_nr[w]);
       S.aw_ev[w] = arena_of(o.ev);
       S.aw_nr[w] = arena_of(o.newrun);
     }
@@ -855,7 +858,8 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
   if (o->slice_scratch_off && o->slice_act_slots && o->slice_tim_slots) {
     uint64_t words = 0;
     rc = cdr_plan_scratch(caps, o->lane_wf, ns, const_cast<uint64_t*>(o->slice_scratch_off),
-                          const_cast<uint32_t*>(o->slice_act_slots), const_cast<uint32_t*>(o->slice_tim_slots), &words);
+                          const_cast<uint32_t*>(o->slice_act_slots), const_cast<uint32_t*>(o->slice_tim_slots),
+                          const_cast<uint32_t*>(o->slice_flags), &words, nullptr);
     if (rc) return rc;
   }
   // entry -> (slice, lane)

@@ -70,11 +70,12 @@ def default_cluster() -> abi.CdrClusterMeta:
 
 
 def synth_batch(config: int, n_wfs: int, seed: int, target_len: int = 0, max_len: int = 0,
-                error_rate: float = 0.0, builder: int = -1, rebuild: bool = False) -> Batch:
+                error_rate: float = 0.0, builder: int = -1, rebuild: bool = False, fault_kinds: int = 0) -> Batch:
     """Deterministic synthetic batch (cadence_amd/csrc/synth.cpp) in natural order."""
     L = abi.lib()
     p = abi.CdrSynthParams(config=config, n_wfs=n_wfs, seed=seed, target_len=target_len, max_len=max_len,
-                           error_rate=error_rate, builder=builder, rebuild=1 if rebuild else 0)
+                           error_rate=error_rate, builder=builder, rebuild=1 if rebuild else 0,
+                           fault_kinds=fault_kinds)
     sz = abi.CdrSynthSizes()
     rc = L.cdr_synth_size(C.byref(p), C.byref(sz))
     if rc:
@@ -98,6 +99,19 @@ def synth_batch(config: int, n_wfs: int, seed: int, target_len: int = 0, max_len
 class Plan:
     caps: C.Array
     totals: abi.CdrTotals
+
+
+def fast_slices(batch: Batch, pl: "Plan | None" = None) -> tuple:
+    """(fast-path slices, slices) of the batch's slice plan (host planner only)."""
+    L = abi.lib()
+    pl = pl or plan(batch)
+    ns, rows = C.c_uint32(), C.c_uint64()
+    L.cdr_plan_slices(batch.wfs, batch.n_wfs, None, None, None, C.byref(ns), C.byref(rows))
+    lane = np.zeros(max(1, ns.value) * 64, np.int32)
+    L.cdr_plan_slices(batch.wfs, batch.n_wfs, lane.ctypes.data, None, None, C.byref(ns), C.byref(rows))
+    words, nf = C.c_uint64(), C.c_uint32()
+    L.cdr_plan_scratch(pl.caps, lane.ctypes.data, ns.value, None, None, None, None, C.byref(words), C.byref(nf))
+    return nf.value, ns.value
 
 
 def plan(batch: Batch) -> Plan:
@@ -145,11 +159,17 @@ class Outputs:
 class Engine:
     """One device context (the analogue of one stateBuilder provider)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, fast_path: bool = True):
         L = abi.lib()
         self.ctx = L.cdr_create(device)
         if not self.ctx:
             raise RuntimeError("cdr_create failed: no usable HIP device (the engine has no CPU fallback)")
+        L.cdr_set_fast_path(self.ctx, 1 if fast_path else 0)
+
+    def set_fast_path(self, enable: bool) -> bool:
+        """Route sequential-activity slices to the fast-path kernel (default) or replay
+        everything with the general kernel; returns the previous setting."""
+        return bool(abi.lib().cdr_set_fast_path(self.ctx, 1 if enable else 0))
 
     def close(self):
         if self.ctx:

@@ -105,7 +105,19 @@ typedef struct cdr_slices {
   const uint64_t* slice_scratch_off; /* [n_slices] 8-byte-word offset into the scratch buffer */
   const uint32_t* slice_act_slots;   /* [n_slices] activity working slots per lane */
   const uint32_t* slice_tim_slots;   /* [n_slices] user-timer working slots per lane */
+  const uint32_t* slice_flags;       /* [n_slices] CDR_SLICE_* */
 } cdr_slices;
+#define CDR_SLICE_FAST 0x1u /* every lane's history has CDR_CAP_FAST */
+/* event types the fast-path kernel replays (bit = cdr_event_type) */
+#define CDR_FAST_TYPES                                                                                       \
+  (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_WF_COMPLETED) | CDR_TB(CDR_EV_WF_FAILED) |                      \
+   CDR_TB(CDR_EV_WF_TIMED_OUT) | CDR_TB(CDR_EV_DT_SCHEDULED) | CDR_TB(CDR_EV_DT_STARTED) |                   \
+   CDR_TB(CDR_EV_DT_COMPLETED) | CDR_TB(CDR_EV_DT_TIMED_OUT) | CDR_TB(CDR_EV_DT_FAILED) |                    \
+   CDR_TB(CDR_EV_AT_SCHEDULED) | CDR_TB(CDR_EV_AT_STARTED) | CDR_TB(CDR_EV_AT_COMPLETED) |                   \
+   CDR_TB(CDR_EV_AT_FAILED) | CDR_TB(CDR_EV_AT_TIMED_OUT) | CDR_TB(CDR_EV_AT_CANCEL_REQUESTED) |             \
+   CDR_TB(CDR_EV_AT_REQ_CANCEL_FAILED) | CDR_TB(CDR_EV_AT_CANCELED) | CDR_TB(CDR_EV_CANCEL_TIMER_FAILED) |   \
+   CDR_TB(CDR_EV_WF_CANCEL_REQUESTED) | CDR_TB(CDR_EV_WF_CANCELED) | CDR_TB(CDR_EV_MARKER_RECORDED) |        \
+   CDR_TB(CDR_EV_WF_SIGNALED) | CDR_TB(CDR_EV_WF_TERMINATED))
 
 #define CDR_ACT_PLANES 12 /* words per activity working slot (replay.hip) */
 #define CDR_TIM_PLANES 4  /* words per user-timer working slot */
@@ -168,6 +180,7 @@ typedef struct cdr_dev_batch {
   /* max over slices of slice_act_slots / slice_tim_slots (cdr_plan_scratch): the
    * launcher keeps up to this many working slots per lane in LDS (0 = all in scratch) */
   uint32_t max_act_slots, max_tim_slots;
+  uint32_t n_fast_slices, _pad2; /* slices with CDR_SLICE_FAST (cdr_plan_scratch) */
   cdr_cluster_meta cluster;
   int64_t now_ns;
   uint64_t uuid_seed;
@@ -188,10 +201,12 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
                     uint64_t* slice_row0, uint32_t* n_slices, uint64_t* n_rows);
 
 /* Working-state scratch layout: per slice, slots = max over its lanes of the live
- * bounds in caps; returns the total words via *total_words.  Outputs sized
- * [n_slices]; pass NULL outputs to query the total only. */
+ * bounds in caps, and the slice's CDR_SLICE_* flags; returns the total words via
+ * *total_words and the number of CDR_SLICE_FAST slices via *n_fast (nullable).
+ * Outputs sized [n_slices]; pass NULL outputs to query the totals only. */
 int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n_slices, uint64_t* scratch_off,
-                     uint32_t* act_slots, uint32_t* tim_slots, uint64_t* total_words);
+                     uint32_t* act_slots, uint32_t* tim_slots, uint32_t* slice_flags, uint64_t* total_words,
+                     uint32_t* n_fast);
 
 /* Arena words needed by the batch's attribute records. */
 uint64_t cdr_plan_arena_words(const cdr_batch* b);
@@ -206,6 +221,10 @@ int cdr_pack_slices(const cdr_batch* b, cdr_slices* out, int threads);
 typedef struct cdr_ctx cdr_ctx;
 cdr_ctx* cdr_create(int device);
 void cdr_destroy(cdr_ctx* ctx);
+
+/* Route CDR_SLICE_FAST slices to the fast-path kernel (default 1) or replay every
+ * slice with the general kernel (0; parity tests run both).  Returns the old value. */
+int cdr_set_fast_path(cdr_ctx* ctx, int enable);
 
 /* Replay a device-resident sliced batch into device-resident outputs on `stream`
  * (a hipStream_t; NULL = default stream).  Asynchronous: enqueues the replay

@@ -471,7 +471,12 @@ typedef struct cdr_wf_caps {
   /* upper bounds of the live set (working slots): activities = max over prefixes of
    * (#scheduled - #closed), timers = #TimerStarted */
   uint32_t act_live, timer_live;
+  uint32_t flags, _pad; /* CDR_CAP_* */
 } cdr_wf_caps;
+/* the history fits the fast-path replay kernel (replay_fast.inc): Started first and
+ * only there, event types in CDR_FAST_TYPES, at most one pending activity, builder
+ * NDC or local */
+#define CDR_CAP_FAST 0x1u
 
 typedef struct cdr_totals {
   uint64_t act, timer, child, cancel, signal, vh, rp, sa;

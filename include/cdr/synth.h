@@ -18,6 +18,8 @@ typedef struct cdr_synth_params {
   double error_rate;    /* fraction of workflows with one injected fault */
   int32_t builder;      /* -1 = config default, else cdr_builder */
   int32_t rebuild;      /* set expected_next_event_id (nDCStateRebuilder check) */
+  uint32_t fault_kinds; /* bit i allows injected fault kind i (synth.cpp inject_fault); 0 = all */
+  uint32_t _pad;
   const uint32_t* index_map; /* optional [n_wfs]: global index of each generated workflow */
 } cdr_synth_params;
 typedef struct cdr_synth_sizes {

@@ -154,3 +154,15 @@ def test_engine_fails_loudly_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError):
         engine.Engine(0)
+
+
+def test_fast_path_eligibility():
+    """The planner routes sequential-activity histories (C1/C2 shapes, NDC or local
+    builder) to the fast-path kernel and everything else to the general one."""
+    for cfg, builder, expect_all in ((1, -1, True), (2, -1, True), (2, abi.BUILDER_LOCAL, True),
+                                     (2, abi.BUILDER_2DC, False), (3, -1, False), (4, -1, False)):
+        b = engine.synth_batch(cfg, 256, seed=7, builder=builder)
+        nf, ns = engine.fast_slices(b)
+        assert (nf == ns) if expect_all else (nf < ns), (cfg, builder, nf, ns)
+    pl = engine.plan(engine.synth_batch(2, 64, seed=1))
+    assert all(pl.caps[w].flags & abi.CAP_FAST for w in range(64))

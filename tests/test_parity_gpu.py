@@ -12,12 +12,20 @@ from cadence_amd import abi, engine
 pytestmark = pytest.mark.gpu
 
 
-def _check(batch, eng):
+def _check(batch, eng, both_paths=False):
     import oracle
     ref = oracle.replay(batch)
     got = eng.replay(batch)
     bad = engine.compare(batch, got, ref)
     assert not bad, "\n".join(bad[:10])
+    if both_paths:  # the same batch through the general kernel only
+        old = eng.set_fast_path(False)
+        try:
+            got = eng.replay(batch)
+        finally:
+            eng.set_fast_path(old)
+        bad = engine.compare(batch, got, ref)
+        assert not bad, "general kernel: " + "\n".join(bad[:10])
     return ref
 
 
@@ -51,3 +59,25 @@ def test_rebuild_next_event_check(engine_gpu):
 def test_long_histories(engine_gpu):
     b = engine.synth_batch(4, 40, seed=5, target_len=3000, max_len=20000)
     _check(b, engine_gpu)
+
+
+@pytest.mark.parametrize("cfg", [1, 2])
+@pytest.mark.parametrize("err", [0.0, 0.3])
+def test_fast_path(engine_gpu, cfg, err):
+    """Sequential-activity shapes run on the fast-path kernel; with and without
+    injected faults it must agree with the oracle and with the general kernel."""
+    b = engine.synth_batch(cfg, 700, seed=0x5EED0000 + cfg + int(err * 10), error_rate=err,
+                           fault_kinds=abi.FAULTS_FAST)
+    nf, ns = engine.fast_slices(b)
+    assert nf > 0, (nf, ns)
+    _check(b, engine_gpu, both_paths=True)
+
+
+@pytest.mark.parametrize("builder", [abi.BUILDER_LOCAL, abi.BUILDER_NDC])
+@pytest.mark.parametrize("err", [0.0, 0.2])
+def test_fast_path_builders(engine_gpu, builder, err):
+    b = engine.synth_batch(2, 300, seed=91 + builder, builder=builder, error_rate=err, fault_kinds=abi.FAULTS_FAST)
+    nf, ns = engine.fast_slices(b)
+    if err == 0.0:  # faults may leave two activities pending (not a fast-path shape)
+        assert nf == ns
+    _check(b, engine_gpu, both_paths=True)
