@@ -190,22 +190,20 @@ EL_BYTES = sum(np.dtype(t).itemsize for _, t in SLAB_COLS)  # CDR_EL_BYTES
 SEF_BATCH_FIRST, SEF_DOMAIN_MISSING = 1 << 8, 1 << 9
 
 
-def slab_columns(slab, row0, slen, cols=None):
-    """Columns of a slice-major slab (uint8 array) in global element order: element
-    (row0[s] + k) * 64 + lane of the result is event k of lane `lane` of slice s."""
-    slab = np.asarray(slab).view(np.uint8)
-    want = [c for c in SLAB_COLS if cols is None or c[0] in cols]
-    out = {name: [] for name, _ in want}
-    for r0, ln in zip(np.asarray(row0, np.uint64).tolist(), np.asarray(slen, np.uint32).tolist()):
-        E = int(ln) * SLICE_WIDTH
-        base = int(r0) * SLICE_WIDTH * EL_BYTES
-        off = 0
-        for name, dt in SLAB_COLS:
-            size = np.dtype(dt).itemsize
-            if name in out:
-                out[name].append(slab[base + off * E: base + (off + size) * E].view(dt))
-            off += size
-    return {k: (np.concatenate(v) if v else np.zeros(0, dict(SLAB_COLS)[k])) for k, v in out.items()}
+ROW_BYTES = EL_BYTES * SLICE_WIDTH  # CDR_ROW_BYTES
+
+
+def slab_columns(slab, row0=None, slen=None, cols=None):
+    """Columns of a slab (uint8 array of rows, cdr.h) in global element order: element
+    row * 64 + lane of the result is the event in that slab row for that lane."""
+    rows = np.asarray(slab).view(np.uint8).reshape(-1, ROW_BYTES)
+    out, off = {}, 0
+    for name, dt in SLAB_COLS:
+        size = np.dtype(dt).itemsize
+        if cols is None or name in cols:
+            out[name] = np.ascontiguousarray(rows[:, off * SLICE_WIDTH:(off + size) * SLICE_WIDTH]).view(dt).reshape(-1)
+        off += size
+    return out
 CdrDevBatch = _S("cdr_dev_batch", [
     ("ev", CdrSlices), ("scratch", C.c_void_p), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
     ("n_wfs", u32), ("empty_uuid", u32), ("max_act_slots", u32), ("max_tim_slots", u32),

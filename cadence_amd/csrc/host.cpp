@@ -131,20 +131,20 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
 
 void pack_lane(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t len, uint32_t l, uint64_t apos,
                const cdr_slices* o) {
-  uint8_t* blk = const_cast<uint8_t*>(o->slab) + row0 * CDR_SLICE_WIDTH * CDR_EL_BYTES;
-  const uint64_t E = (uint64_t)len * CDR_SLICE_WIDTH;
-  int64_t* eid = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_EVENT_ID, E));
-  int64_t* ver = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_VERSION, E));
-  int64_t* ts = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_TIMESTAMP, E));
-  int64_t* task = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_TASK_ID, E));
-  int64_t* key = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_KEY, E));
-  int64_t* aux = reinterpret_cast<int64_t*>(blk + cdr_col_off(CDR_COL_AUX, E));
-  uint32_t* tf = reinterpret_cast<uint32_t*>(blk + cdr_col_off(CDR_COL_TYPE_FLAGS, E));
-  uint32_t* hh = reinterpret_cast<uint32_t*>(blk + cdr_col_off(CDR_COL_H, E));
-  int32_t* nn = reinterpret_cast<int32_t*>(blk + cdr_col_off(CDR_COL_N, E));
+  uint8_t* const blk0 = const_cast<uint8_t*>(o->slab) + row0 * CDR_ROW_BYTES;
   uint64_t* arena = const_cast<uint64_t*>(o->arena);
   for (uint32_t k = 0; k < len; k++) {
-    const uint64_t i = (uint64_t)k * CDR_SLICE_WIDTH + l;
+    uint8_t* const row = blk0 + (uint64_t)k * CDR_ROW_BYTES;
+    int64_t* eid = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_EVENT_ID));
+    int64_t* ver = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_VERSION));
+    int64_t* ts = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_TIMESTAMP));
+    int64_t* task = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_TASK_ID));
+    int64_t* key = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_KEY));
+    int64_t* aux = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_AUX));
+    uint32_t* tf = reinterpret_cast<uint32_t*>(row + cdr_col_off(CDR_COL_TYPE_FLAGS));
+    uint32_t* hh = reinterpret_cast<uint32_t*>(row + cdr_col_off(CDR_COL_H));
+    int32_t* nn = reinterpret_cast<int32_t*>(row + cdr_col_off(CDR_COL_N));
+    const uint32_t i = l;
     if (k >= n_ev) {
       tf[i] = CDR_EV_PAD;
       eid[i] = ver[i] = ts[i] = task[i] = key[i] = aux[i] = 0;

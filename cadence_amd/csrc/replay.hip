@@ -217,12 +217,13 @@ __device__ __forceinline__ uint32_t bld32(rsrc_t r, uint32_t voff, uint32_t soff
 struct Slice {
   rsrc_t r;
   uint32_t elems;  // slice_len * 64
-  __device__ __forceinline__ uint32_t col(int c) const { return (uint32_t)cdr_col_off(c, elems); }
+  uint32_t l4;     // lane * 4: an element of a 4-byte column sits l4 below its 8-byte twin
+  __device__ __forceinline__ uint32_t col(int c) const { return cdr_col_off(c); }
 };
-// voffset of element (k, lane) in an 8-byte column (4-byte columns: half of it);
-// OOB_BIT when k is past the lane's history
+// voffset of element (k, lane) of an 8-byte column relative to the column's start in
+// row 0 (OOB_BIT set when k is past the lane's history); 4-byte columns: minus l4
 __device__ __forceinline__ uint32_t el8(uint32_t k, uint32_t len, uint32_t lane) {
-  return k < len ? (k * CDR_SLICE_WIDTH + lane) * 8u : OOB_BIT;
+  return (k < len ? k * CDR_ROW_BYTES : OOB_BIT) + lane * 8u;
 }
 
 // one event's operands (cdr.h "operand columns per type"); task_id is read once,
@@ -233,14 +234,14 @@ struct Ev {
   int64_t id, ver, ts, key, aux;
 };
 __device__ __forceinline__ uint32_t load_tf(const Slice& S, uint32_t o8) {
-  return bld32(S.r, (o8 >> 1) | (o8 & OOB_BIT), S.col(CDR_COL_TYPE_FLAGS));
+  return bld32(S.r, o8 - S.l4, S.col(CDR_COL_TYPE_FLAGS));
 }
 // need bit b of tf (CDR_SEF_NEED_*) clear -> OOB_BIT
 __device__ __forceinline__ uint32_t gate(uint32_t off, uint32_t tf, uint32_t bit) {
   return off | ((tf & bit) ? 0u : OOB_BIT);
 }
 __device__ __forceinline__ Ev load_ops(const Slice& S, uint32_t o8, uint32_t tf) {
-  const uint32_t o4 = (o8 >> 1) | (o8 & OOB_BIT);
+  const uint32_t o4 = o8 - S.l4;
   Ev e;
   e.tf = tf;
   e.id = bld64(S.r, o8, S.col(CDR_COL_EVENT_ID));
@@ -479,8 +480,9 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
                         __builtin_amdgcn_readfirstlane((uint32_t)row0_);
   Slice S;
   S.elems = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_len[s]) * CDR_SLICE_WIDTH;
-  S.r = __builtin_amdgcn_make_buffer_rsrc((void*)(KA()->B.ev.slab + row0 * CDR_SLICE_WIDTH * CDR_EL_BYTES), (short)0,
+  S.r = __builtin_amdgcn_make_buffer_rsrc((void*)(KA()->B.ev.slab + row0 * CDR_ROW_BYTES), (short)0,
                                           (int)(S.elems * CDR_EL_BYTES), 0x00020000);
+  S.l4 = lane * 4u;
   const int32_t w = KA()->B.ev.lane_wf[(uint64_t)s * CDR_SLICE_WIDTH + lane];
   if (w < 0) return;
 

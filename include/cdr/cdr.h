@@ -42,14 +42,15 @@ extern "C" {
 
 #define CDR_SLICE_WIDTH 64 /* workflows per slice = one wavefront */
 
-/* Sliced event layout ("SELL-64" in a slice-major slab): workflows are grouped 64
- * to a slice (one lane each, slices sorted by length).  Slice s owns one contiguous
- * block of the slab, starting at byte slice_row0[s] * 64 * CDR_EL_BYTES, that holds
- * its E = slice_len[s] * 64 elements column after column (cdr_col_off below).  Event
- * k of lane L is element k * 64 + L of every column of its slice, so a wavefront
- * that walks its 64 histories in lockstep reads each column fully coalesced, and
- * one buffer descriptor per slice addresses every column.  The kernel reads only
- * the operand columns an event's type needs (CDR_SEF_NEED_* bits of type_flags).
+/* Sliced event layout ("SELL-64" rows in a slab): workflows are grouped 64 to a
+ * slice (one lane each, slices sorted by length).  Slice s owns slice_len[s]
+ * consecutive rows of the slab starting at row slice_row0[s]; row k of a slice holds
+ * event k of its 64 lanes, column after column (cdr_col_off below), in
+ * CDR_ROW_BYTES.  A wavefront that walks its 64 histories in lockstep therefore reads
+ * each column of a step as one coalesced 256/512-B access and a whole step from one
+ * contiguous 3.75 KB row (DRAM-page friendly), and one buffer descriptor per slice
+ * addresses every column with an immediate column offset.  The kernel reads only the
+ * operand columns an event's type needs (CDR_SEF_NEED_* bits of type_flags).
  *
  * Operand columns per type (all others 0):
  *   WorkflowExecutionStarted  aux = arena word offset of cdr_attr_wf_started
@@ -85,10 +86,13 @@ enum cdr_col {
   CDR_NUM_COLS
 };
 #define CDR_EL_BYTES 60u /* bytes of one (row, lane) element over all columns */
-/* element size and byte offset (within a slice block of `elems` elements) of a column */
+#define CDR_ROW_BYTES (CDR_EL_BYTES * CDR_SLICE_WIDTH) /* 3840: one event of 64 lanes */
+/* element size of a column and its byte offset within a row; element (k, L) of
+ * column c of a slice is at k * CDR_ROW_BYTES + cdr_col_off(c) + L * cdr_col_size(c)
+ * from the slice's first row */
 CDR_HD uint32_t cdr_col_size(int c) { return c < CDR_COL_TYPE_FLAGS ? 8u : 4u; }
-CDR_HD uint64_t cdr_col_off(int c, uint64_t elems) {
-  return elems * (c <= CDR_COL_TYPE_FLAGS ? 8u * (uint32_t)c : 48u + 4u * (uint32_t)(c - CDR_COL_TYPE_FLAGS));
+CDR_HD uint32_t cdr_col_off(int c) {
+  return CDR_SLICE_WIDTH * (c <= CDR_COL_TYPE_FLAGS ? 8u * (uint32_t)c : 48u + 4u * (uint32_t)(c - CDR_COL_TYPE_FLAGS));
 }
 
 typedef struct cdr_slices {
@@ -98,7 +102,7 @@ typedef struct cdr_slices {
   const uint64_t* slice_row0; /* [n_slices] prefix sum of slice_len */
   const uint32_t* slice_len;  /* [n_slices] */
   const int32_t* lane_wf;     /* [n_slices*64] workflow index, -1 = empty lane */
-  const uint8_t* slab;        /* n_rows * 64 * CDR_EL_BYTES bytes of event columns */
+  const uint8_t* slab;        /* n_rows * CDR_ROW_BYTES bytes of event rows */
   const uint64_t* arena; /* WorkflowExecutionStarted / ActivityTaskScheduled attribute records */
   /* working-state scratch of each slice (cdr_plan_scratch): pending activities and
    * user timers are kept lane-interleaved ("plane j*P+p, lane L") while they are live */
