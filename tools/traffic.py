@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Summarise a tools/pmc.sh run (gpurun_out/<tag>_pmc) for the replay kernel into
+profiles/<name>_pmc.txt and profiles/traffic_latest.json (read by bench.py).
+
+HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of
+a coalesced streaming read (128-B requests tallied at 64 B), so it is doubled;
+WRITE_SIZE is taken as is.  Counters are averaged over the profiled dispatches.
+usage: tools/traffic.py <tag> <workload> <profile-name> [kernel-substring]"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag, workload, name = sys.argv[1:4]
+    kern = sys.argv[4] if len(sys.argv) > 4 else "k_replay"
+    agg = collections.defaultdict(float)
+    nd = collections.defaultdict(set)
+    for f in glob.glob(os.path.join(ROOT, "gpurun_out", f"{tag}_pmc", "*", "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if kern not in r["Kernel_Name"]:
+                continue
+            agg[r["Counter_Name"]] += float(r["Counter_Value"])
+            nd[r["Counter_Name"]].add(r["Dispatch_Id"])
+    avg = {c: v / len(nd[c]) for c, v in agg.items()}
+    lines = [f"{c:24s} {v:.6g}" for c, v in sorted(avg.items())]
+    waves = avg.get("SQ_WAVES", 0)
+    out = {"workload": workload, "kernel": kern, "source": f"rocprofv3 --pmc passes, tools/pmc.sh ({tag})",
+           "counters": avg}
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        rd = avg["FETCH_SIZE"] * 1024 * 2
+        wr = avg["WRITE_SIZE"] * 1024
+        out.update({"read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "bytes_per_launch": rd + wr,
+                    "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count), WRITE_SIZE KiB x 1024"})
+        lines.append(f"HBM read  bytes/launch  {rd:.4g} (FETCH_SIZE x 2 KiB)")
+        lines.append(f"HBM write bytes/launch  {wr:.4g}")
+    if waves:
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS"):
+            if c in avg:
+                lines.append(f"{c} per wave            {avg[c] / waves:.1f}")
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    open(os.path.join(ROOT, "profiles", f"{name}_pmc.txt"), "w").write("\n".join(lines) + "\n")
+    json.dump(out, open(os.path.join(ROOT, "profiles", "traffic_latest.json"), "w"), indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
