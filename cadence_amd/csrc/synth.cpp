@@ -520,9 +520,13 @@ int default_builder(int cfg, Rng& r) {
   }
 }
 
+inline uint32_t global_index(const cdr_synth_params& P, uint32_t local) {
+  return P.index_map ? P.index_map[local] : local;
+}
+
 // generate workflow `w` (pure function of params and w)
 void gen_one(const cdr_synth_params& P, uint32_t local, WfOut& o) {
-  const uint32_t w = P.index_map ? P.index_map[local] : local;  // global workflow index
+  const uint32_t w = global_index(P, local);  // global workflow index
   Gen g(P, w, o);
   Rng r2(P.seed ^ cdr_mix64(0xB17D + (uint64_t)w));
   const int builder = P.builder >= 0 ? P.builder : default_builder(P.config, r2);
@@ -725,10 +729,10 @@ int cdr_synth_fill(const cdr_synth_params* p, cdr_event* ev, cdr_wf_desc* wfs, c
       n.wf_key = cdr_mix64(o.d.wf_key ^ CDR_UUID_NEWRUN_KEY);
       n.ev_off = ev_base[w] + o.ev.size();
       n.ev_len = o.newrun.size();
-      n.run_id = wf_handle(w, 30);  // == the CAN event's NewExecutionRunId
+      n.run_id = wf_handle(global_index(*p, w), 30);  // == the CAN event's NewExecutionRunId
       uint64_t lo, hi;
       cdr_uuid(p->seed, o.d.wf_key, CDR_UUID_NEWRUN_REQ, 0, &lo, &hi);
-      n.request_id = wf_handle(w, 12);  // host-interned uuid.New() (stateBuilder.go:566)
+      n.request_id = wf_handle(global_index(*p, w), 12);  // host-interned uuid.New() (stateBuilder.go:566)
       (void)lo;
       (void)hi;
       n.builder = o.newrun_ndc ? CDR_BUILDER_NDC : CDR_BUILDER_2DC;
@@ -893,8 +897,8 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
       n.wf_key = cdr_mix64(g.d.wf_key ^ CDR_UUID_NEWRUN_KEY);
       n.ev_off = 0;
       n.ev_len = g.newrun.size();
-      n.run_id = wf_handle(w, 30);
-      n.request_id = wf_handle(w, 12);
+      n.run_id = wf_handle(global_index(*p, w), 30);
+      n.request_id = wf_handle(global_index(*p, w), 12);
       n.builder = g.newrun_ndc ? CDR_BUILDER_NDC : CDR_BUILDER_2DC;
       n.expected_next_event_id = 0;
       n.parent = (int32_t)i;

@@ -1,0 +1,95 @@
+"""Multi-rank (N>1) path of bench.py on CPU: gloo, world size 2.
+
+The replay shards with no data-path collective: historyShardID = Fingerprint32(wid) %
+16384 (common/util.go:249-252), shards -> ranks greedily, each rank replays only its
+workflows, and one all-reduce (sum) of {events, workflows, ok, checksum} closes the
+step.  Here each rank replays its share with the CPU restatement (oracle/, the parity
+checker — no GPU in this container) and the all-reduced totals must equal a
+single-process replay of the whole population, workflow for workflow."""
+import hashlib
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import bench
+import oracle
+from cadence_amd import abi, engine
+
+TOTAL = 600
+SEED = 0x5EED0003
+
+
+def _wf_digest(batch, out, w) -> int:
+    s = json.dumps(engine.export_state(batch, out, w), sort_keys=True).encode()
+    return int.from_bytes(hashlib.sha256(s).digest()[:8], "little")
+
+
+def _stats(batch, out):
+    n_ev = len(batch.events)
+    ok = sum(1 for w in range(batch.n_wfs) if out.result[w].code == abi.OK)
+    cs = sum(_wf_digest(batch, out, w) for w in range(batch.n_wfs)) & (2 ** 64 - 1)
+    return [n_ev, batch.n_wfs, ok, cs - 2 ** 64 if cs >= 2 ** 63 else cs]
+
+
+def _share(mine, cfg):
+    b = engine.synth_batch(cfg, len(mine), SEED, index_map=mine)
+    return b, oracle.replay(b)
+
+
+def _rank(rank, world, port, cfg, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine, _ = bench.assign_shards(TOTAL, world, rank)
+        b, out = _share(mine, cfg)
+        stats = torch.tensor(_stats(b, out), dtype=torch.int64)
+        dist.all_reduce(stats)
+        owned = [None] * world
+        dist.all_gather_object(owned, mine.tolist())
+        if rank == 0:
+            q.put((stats.tolist(), owned))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("cfg", [3, 4])
+def test_two_rank_shards_match_single_process(cfg):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, cfg, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    stats, owned = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # the shard->rank assignment partitions the population
+    allw = np.sort(np.concatenate([np.array(o, np.int64) for o in owned]))
+    assert np.array_equal(allw, np.arange(TOTAL))
+    assert all(len(o) > 0 for o in owned)
+    # the all-reduced totals equal one process replaying everything
+    b, out = _share(np.arange(TOTAL, dtype=np.uint32), cfg)
+    assert stats == _stats(b, out)
+
+
+def test_shard_assignment_balances_events():
+    lengths = np.random.default_rng(1).lognormal(np.log(200), 1.0, TOTAL)
+    loads = []
+    for r in range(4):
+        mine, load = bench.assign_shards(TOTAL, 4, r, lengths)
+        loads.append(lengths[mine].sum())
+    assert np.isclose(sum(loads), lengths.sum())
+    assert max(loads) / (sum(loads) / 4) < 1.25
