@@ -128,19 +128,21 @@ CdrBatch = _S("cdr_batch", [
 
 # ------------------------------------------------------------------ output
 CdrExecInfo = _S("cdr_exec_info", [
+    # first 128 B: set by WorkflowExecutionStarted
     ("domain_id", u32), ("workflow_id", u32), ("run_id", u32), ("create_request_id", u32),
     ("parent_domain_id", u32), ("parent_workflow_id", u32), ("parent_run_id", u32), ("task_list", u32),
-    ("workflow_type", u32), ("decision_request_id", u32), ("cron_schedule", u32), ("memo", u32),
-    ("nonretriable", u32), ("branch_tree_id", u32), ("flags", u32), ("_pad0", u32),
-    ("initiated_id", i64), ("completion_event_batch_id", i64), ("workflow_timeout", i32),
-    ("decision_timeout_value", i32), ("state", i32), ("close_status", i32), ("last_first_event_id", i64),
-    ("last_event_task_id", i64), ("next_event_id", i64), ("last_processed_event", i64), ("signal_count", i32),
-    ("decision_timeout", i32), ("decision_version", i64), ("decision_schedule_id", i64),
-    ("decision_started_id", i64), ("decision_attempt", i64), ("decision_started_ts", i64),
-    ("decision_scheduled_ts", i64), ("decision_original_scheduled_ts", i64), ("attempt", i32),
-    ("initial_interval", i32), ("backoff_coefficient", f64), ("maximum_interval", i32), ("maximum_attempts", i32),
-    ("expiration_time", i64), ("expiration_seconds", i32), ("_pad1", i32), ("branch_id_lo", u64),
-    ("branch_id_hi", u64), ("reset_points_len", u32), ("search_attr_len", u32)])
+    ("workflow_type", u32), ("cron_schedule", u32), ("memo", u32), ("nonretriable", u32),
+    ("branch_tree_id", u32), ("workflow_timeout", i32), ("decision_timeout_value", i32), ("attempt", i32),
+    ("initiated_id", i64), ("initial_interval", i32), ("maximum_interval", i32), ("backoff_coefficient", f64),
+    ("maximum_attempts", i32), ("expiration_seconds", i32), ("expiration_time", i64), ("branch_id_lo", u64),
+    ("branch_id_hi", u64), ("_pad0", u32), ("_pad1", u32),
+    # second 128 B: updated by the replay
+    ("decision_request_id", u32), ("flags", u32), ("completion_event_batch_id", i64), ("state", i32),
+    ("close_status", i32), ("last_first_event_id", i64), ("last_event_task_id", i64), ("next_event_id", i64),
+    ("last_processed_event", i64), ("signal_count", i32), ("decision_timeout", i32), ("decision_version", i64),
+    ("decision_schedule_id", i64), ("decision_started_id", i64), ("decision_attempt", i64),
+    ("decision_started_ts", i64), ("decision_scheduled_ts", i64), ("decision_original_scheduled_ts", i64),
+    ("reset_points_len", u32), ("search_attr_len", u32)])
 CdrReplState = _S("cdr_repl_state", [
     ("current_version", i64), ("start_version", i64), ("last_write_version", i64), ("last_write_event_id", i64),
     ("lri_version", i64 * MAX_CLUSTERS), ("lri_last_event_id", i64 * MAX_CLUSTERS), ("lri_mask", u32),

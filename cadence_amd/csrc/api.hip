@@ -98,7 +98,7 @@ __global__ void k_checksum(cdr_dev_batch B, cdr_out O, unsigned long long* sum) 
     if (r.code == CDR_OK) {
       const cdr_wf_caps c = B.caps[w];
       h = hash_bytes(h, &O.exec[w], sizeof(cdr_exec_info));
-      h = hash_bytes(h, &O.repl[w], sizeof(cdr_repl_state));
+      if (B.wfs[w].builder == CDR_BUILDER_2DC) h = hash_bytes(h, &O.repl[w], sizeof(cdr_repl_state));
       h = hash_bytes(h, O.vh + c.vh_off, r.n_vh * sizeof(cdr_vh_item));
       h = hash_bytes(h, O.act + c.act_off, r.n_activity * sizeof(cdr_activity_info));
       h = hash_bytes(h, O.timer + c.timer_off, r.n_timer * sizeof(cdr_timer_info));

@@ -1342,9 +1342,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
       }
     RS->lri_mask = rs_mask;
     RS->present = 1;
-  } else {
-    gput(RS, cdr_repl_state{});
-  }
+  }  // other builders: ReplicationState is nil and the record is left untouched (schema.h)
 #undef D
 #undef CP
 #undef X

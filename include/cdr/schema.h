@@ -21,6 +21,7 @@
 #ifndef CDR_SCHEMA_H
 #define CDR_SCHEMA_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #if defined(__HIPCC__)
@@ -382,29 +383,42 @@ typedef struct cdr_batch {
 #define CDR_XI_HAS_RESET_POINTS 0x040u /* AutoResetPoints non-nil */
 #define CDR_XI_STARTED 0x080u          /* a WorkflowExecutionStarted event was applied */
 #define CDR_XI_VH_BRANCH 0x100u        /* branch_* fields hold the NDC VersionHistory token */
+/* Two 128-B halves (records are 256-B aligned in cdr_out): the first holds what
+ * WorkflowExecutionStarted fixes (written once, when it is applied), the second what
+ * the rest of the replay updates (written once, at the end) — so that each 128-B line
+ * of the record reaches HBM once. */
 typedef struct cdr_exec_info {
+  /* -- set by WorkflowExecutionStarted (ReplicateWorkflowExecutionStartedEvent) */
   uint32_t domain_id, workflow_id, run_id, create_request_id;
   uint32_t parent_domain_id, parent_workflow_id, parent_run_id, task_list;
-  uint32_t workflow_type, decision_request_id, cron_schedule, memo;
-  uint32_t nonretriable, branch_tree_id, flags, _pad0;
-  int64_t initiated_id, completion_event_batch_id;
-  int32_t workflow_timeout, decision_timeout_value;
+  uint32_t workflow_type, cron_schedule, memo, nonretriable;
+  uint32_t branch_tree_id;
+  int32_t workflow_timeout, decision_timeout_value, attempt;
+  int64_t initiated_id;
+  int32_t initial_interval, maximum_interval;
+  double backoff_coefficient;
+  int32_t maximum_attempts, expiration_seconds;
+  int64_t expiration_time;
+  uint64_t branch_id_lo, branch_id_hi;
+  uint32_t _pad0, _pad1;
+  /* -- updated by the replay */
+  uint32_t decision_request_id, flags;
+  int64_t completion_event_batch_id;
   int32_t state, close_status;
   int64_t last_first_event_id, last_event_task_id, next_event_id, last_processed_event;
   int32_t signal_count, decision_timeout;
   int64_t decision_version, decision_schedule_id, decision_started_id, decision_attempt;
   int64_t decision_started_ts, decision_scheduled_ts, decision_original_scheduled_ts;
-  int32_t attempt, initial_interval;
-  double backoff_coefficient;
-  int32_t maximum_interval, maximum_attempts;
-  int64_t expiration_time;
-  int32_t expiration_seconds, _pad1;
-  uint64_t branch_id_lo, branch_id_hi;
   uint32_t reset_points_len, search_attr_len;
 } cdr_exec_info;
+#ifdef __cplusplus
+static_assert(sizeof(cdr_exec_info) == 256 && offsetof(cdr_exec_info, decision_request_id) == 128, "cdr_exec_info");
+#endif
 
 /* ReplicationState (dataInterfaces.go:325-331) + LastReplicationInfo map keyed by
- * cluster index (bit i of lri_mask = entry present) */
+ * cluster index (bit i of lri_mask = entry present).  Written only for entries replayed
+ * with the 2DC builder (present = 1); for other builders Go's ReplicationState is nil
+ * and the record is left untouched. */
 typedef struct cdr_repl_state {
   int64_t current_version, start_version, last_write_version, last_write_event_id;
   int64_t lri_version[CDR_MAX_CLUSTERS];
