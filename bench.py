@@ -76,12 +76,13 @@ def assign_shards(total_wfs: int, world: int, rank: int, lengths=None):
 class DeviceBatch:
     """Synthetic batch generated straight into the sliced layout, uploaded to HBM."""
 
-    def __init__(self, torch, config, index_map, seed, target_len=0):
+    def __init__(self, torch, config, index_map, seed, target_len=0, plan_mode=abi.PLAN_WAVE):
         L = abi.lib()
         self.torch = torch
         self.index_map = index_map
         p = abi.CdrSynthParams(config=config, n_wfs=len(index_map), seed=seed, target_len=target_len, max_len=0,
-                               error_rate=0.0, builder=-1, rebuild=0, index_map=index_map.ctypes.data)
+                               error_rate=0.0, builder=-1, rebuild=0, index_map=index_map.ctypes.data,
+                               plan_mode=plan_mode)
         self.params = p
         t0 = time.perf_counter()
         info = abi.CdrSynthPlanInfo()
@@ -147,7 +148,9 @@ class DeviceBatch:
         db.max_act_slots = int(self.h_sc_act.max()) if len(self.h_sc_act) else 0
         db.max_tim_slots = int(self.h_sc_tim.max()) if len(self.h_sc_tim) else 0
         self.n_fast = int(((self.h_sflags & abi.SLICE_FAST) != 0).sum())
+        self.n_wave = int(((self.h_sflags & abi.SLICE_WAVE) != 0).sum())
         db.n_fast_slices = self.n_fast
+        db.n_wave_slices = self.n_wave
         db.empty_uuid = meta.empty_uuid
         db.cluster = meta.cluster
         db.now_ns = meta.now_ns
@@ -265,6 +268,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stream-peak", action="store_true")
     ap.add_argument("--no-fast-path", action="store_true", help="replay every slice with the general kernel")
+    ap.add_argument("--no-wave", action="store_true", help="no wave slices: divergent histories in lane slices")
     args = ap.parse_args()
 
     import torch
@@ -286,8 +290,8 @@ def main():
     total = args.wfs * world
     mine, _ = assign_shards(total, world, rank)
     log(f"[rank {rank}] {len(mine)} of {total} workflows (shard->GPU greedy over {NUM_SHARDS} shards)")
-    db = DeviceBatch(torch, args.config, mine, args.seed)
-    log(f"[rank {rank}] {db.n_fast} of {db.info.n_slices} slices on the fast-path kernel")
+    db = DeviceBatch(torch, args.config, mine, args.seed, plan_mode=0 if args.no_wave else abi.PLAN_WAVE)
+    log(f"[rank {rank}] {db.n_fast} of {db.info.n_slices} slices on the fast-path kernel, {db.n_wave} wave slices")
     log(f"[rank {rank}] packed {db.n_events:,} events in {db.pack_s:.2f}s (host SoA), H2D {db.h2d_s:.2f}s "
         f"({db.in_bytes / 1e9:.2f} GB in, {db.out_bytes / 1e9:.2f} GB out buffers)")
     stream = torch.cuda.current_stream().cuda_stream

@@ -183,7 +183,10 @@ CdrSlices = _S("cdr_slices", [
         "slice_row0", "slice_len", "lane_wf", "slab", "arena", "slice_scratch_off", "slice_act_slots",
         "slice_tim_slots", "slice_flags")])
 SLICE_FAST = 0x1
+SLICE_WAVE = 0x2
 CAP_FAST = 0x1
+CAP_WAVE = 0x2
+PLAN_WAVE = 0x1
 
 # slice-major slab of event columns (cdr.h enum cdr_col): name, dtype, in order
 SLAB_COLS = (("event_id", np.int64), ("version", np.int64), ("timestamp", np.int64), ("task_id", np.int64),
@@ -209,13 +212,13 @@ def slab_columns(slab, row0=None, slen=None, cols=None):
 CdrDevBatch = _S("cdr_dev_batch", [
     ("ev", CdrSlices), ("scratch", C.c_void_p), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
     ("n_wfs", u32), ("empty_uuid", u32), ("max_act_slots", u32), ("max_tim_slots", u32),
-    ("n_fast_slices", u32), ("_pad2", u32),
+    ("n_fast_slices", u32), ("n_wave_slices", u32),
     ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64)])
 
 # ------------------------------------------------------------------ synth
 CdrSynthParams = _S("cdr_synth_params", [
     ("config", i32), ("n_wfs", u32), ("seed", u64), ("target_len", u32), ("max_len", u32), ("error_rate", f64),
-    ("builder", i32), ("rebuild", i32), ("fault_kinds", u32), ("_pad", u32), ("index_map", C.c_void_p)])
+    ("builder", i32), ("rebuild", i32), ("fault_kinds", u32), ("plan_mode", u32), ("index_map", C.c_void_p)])
 # synth fault kinds that keep a sequential-activity history on the fast path (synth.cpp inject_fault)
 FAULTS_FAST = (1 << 1) | (1 << 2) | (1 << 3) | (1 << 5) | (1 << 6)
 CdrSynthSizes = _S("cdr_synth_sizes", [("n_events", u64), ("n_entries", u32), ("_pad", u32), ("n_kvs", u64),
@@ -239,10 +242,13 @@ EXPORTS = {
     "cdr_plan_caps": (i32, [C.POINTER(CdrBatch), C.POINTER(CdrWfCaps), C.POINTER(CdrTotals)]),
     "cdr_plan_slices": (i32, [C.POINTER(CdrWfDesc), u32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(u32),
                               C.POINTER(u64)]),
+    "cdr_plan_slices_ex": (i32, [C.POINTER(CdrWfDesc), C.c_void_p, u32, u32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_void_p, C.POINTER(u32), C.POINTER(u64), C.POINTER(u32)]),
     "cdr_plan_arena_words": (u64, [C.POINTER(CdrBatch)]),
     "cdr_plan_scratch": (i32, [C.c_void_p, C.c_void_p, u32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                C.POINTER(u64), C.c_void_p]),
     "cdr_set_fast_path": (i32, [C.c_void_p, i32]),
+    "cdr_set_plan_mode": (i32, [C.c_void_p, u32]),
     "cdr_pack_slices": (i32, [C.POINTER(CdrBatch), C.POINTER(CdrSlices), i32]),
     "cdr_create": (C.c_void_p, [i32]),
     "cdr_destroy": (None, [C.c_void_p]),

@@ -11,6 +11,8 @@
 
 #include "cdr/cdr.h"
 
+extern "C" uint32_t cdr_get_plan_mode(const cdr_ctx* ctx);  // replay.hip
+
 #define HIPCHK(x)                                                                                     \
   do {                                                                                                \
     hipError_t _e = (x);                                                                              \
@@ -174,14 +176,16 @@ int cdr_checksum_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out
 int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot, cdr_out* out) {
   if (!ctx || !b || !caps || !tot || !out) return CDR_API_EINVAL;
   // ---- plan + pack on the host
-  uint32_t ns = 0;
+  uint32_t ns = 0, n_wave = 0;
   uint64_t rows = 0;
-  int rc = cdr_plan_slices(b->wfs, b->n_wfs, nullptr, nullptr, nullptr, &ns, &rows);
+  const uint32_t mode = cdr_get_plan_mode(ctx);
+  int rc = cdr_plan_slices_ex(b->wfs, caps, b->n_wfs, mode, nullptr, nullptr, nullptr, nullptr, &ns, &rows, &n_wave);
   if (rc) return rc;
   std::vector<int32_t> lane(ns * (size_t)CDR_SLICE_WIDTH);
-  std::vector<uint32_t> slen(ns);
+  std::vector<uint32_t> slen(ns), sflags(ns);
   std::vector<uint64_t> row0(ns);
-  rc = cdr_plan_slices(b->wfs, b->n_wfs, lane.data(), slen.data(), row0.data(), &ns, &rows);
+  rc = cdr_plan_slices_ex(b->wfs, caps, b->n_wfs, mode, lane.data(), slen.data(), row0.data(), sflags.data(), &ns,
+                          &rows, &n_wave);
   if (rc) return rc;
   const uint64_t ne = rows * CDR_SLICE_WIDTH;
   const uint64_t aw = cdr_plan_arena_words(b);
@@ -194,6 +198,7 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   hs.slice_row0 = row0.data();
   hs.slice_len = slen.data();
   hs.lane_wf = lane.data();
+  hs.slice_flags = sflags.data();
   hs.slab = slab.data();
   hs.arena = arena.data();
   rc = cdr_pack_slices(b, &hs, 0);
@@ -228,7 +233,7 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   db.ev.slab = (const uint8_t*)up(slab.data(), slab.size());
   db.ev.arena = (const uint64_t*)up(arena.data(), arena.size() * 8);
   std::vector<uint64_t> sc_off(ns);
-  std::vector<uint32_t> sc_act(ns), sc_tim(ns), sflags(ns);
+  std::vector<uint32_t> sc_act(ns), sc_tim(ns);
   uint64_t sc_words = 0;
   uint32_t n_fast = 0;
   rc = cdr_plan_scratch(caps, lane.data(), ns, sc_off.data(), sc_act.data(), sc_tim.data(), sflags.data(), &sc_words,
@@ -236,6 +241,7 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   if (rc) return rc;
   db.ev.slice_flags = (const uint32_t*)up(sflags.data(), ns * 4ull);
   db.n_fast_slices = n_fast;
+  db.n_wave_slices = n_wave;
   db.ev.slice_scratch_off = (const uint64_t*)up(sc_off.data(), ns * 8ull);
   db.ev.slice_act_slots = (const uint32_t*)up(sc_act.data(), ns * 4ull);
   db.ev.slice_tim_slots = (const uint32_t*)up(sc_tim.data(), ns * 4ull);

@@ -77,7 +77,7 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   bool have_ver = false;
   int64_t last_ver = 0;
   uint32_t vh = 0;
-  int64_t live = 0, live_max = 0;
+  int64_t live = 0, live_max = 0, tlive = 0, tlive_max = 0;
   for (uint64_t k = 0; k < n; k++) {
     const cdr_event& e = ev[k];
     // live-activity bound: a close of a missing activity stops the replay, so before
@@ -86,6 +86,9 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
     if (e.type == CDR_EV_AT_COMPLETED || e.type == CDR_EV_AT_FAILED || e.type == CDR_EV_AT_TIMED_OUT ||
         e.type == CDR_EV_AT_CANCELED)
       live = std::max<int64_t>(0, live - 1);
+    // live user timers: an upper bound (a restarted live timer reuses its slot)
+    if (e.type == CDR_EV_TIMER_STARTED) tlive_max = std::max(tlive_max, ++tlive);
+    if (e.type == CDR_EV_TIMER_FIRED || e.type == CDR_EV_TIMER_CANCELED) tlive = std::max<int64_t>(0, tlive - 1);
     fast = fast && e.type < 64 && (CDR_FAST_TYPES & (1ull << e.type)) && (k == 0 || e.type != CDR_EV_WF_STARTED);
     if (!have_ver || e.version > last_ver) {
       vh++;
@@ -126,34 +129,36 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   c.act_live = (uint32_t)live_max;
   c.timer_live = c.timer_cap;
   c.flags = (fast && live_max <= 1) ? CDR_CAP_FAST : 0u;
+  const uint32_t W = CDR_WAVE_SLOTS;
+  if (!(c.flags & CDR_CAP_FAST) && live_max <= (int64_t)W && tlive_max <= (int64_t)W && c.child_cap <= W &&
+      c.cancel_cap <= W && c.signal_cap <= W && c.sa_cap <= W)
+    c.flags |= CDR_CAP_WAVE;
   *out = c;
 }
 
-void pack_lane(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t len, uint32_t l, uint64_t apos,
-               const cdr_slices* o) {
-  uint8_t* const blk0 = const_cast<uint8_t*>(o->slab) + row0 * CDR_ROW_BYTES;
-  uint64_t* arena = const_cast<uint64_t*>(o->arena);
-  for (uint32_t k = 0; k < len; k++) {
-    uint8_t* const row = blk0 + (uint64_t)k * CDR_ROW_BYTES;
-    int64_t* eid = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_EVENT_ID));
-    int64_t* ver = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_VERSION));
-    int64_t* ts = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_TIMESTAMP));
-    int64_t* task = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_TASK_ID));
-    int64_t* key = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_KEY));
-    int64_t* aux = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_AUX));
-    uint32_t* tf = reinterpret_cast<uint32_t*>(row + cdr_col_off(CDR_COL_TYPE_FLAGS));
-    uint32_t* hh = reinterpret_cast<uint32_t*>(row + cdr_col_off(CDR_COL_H));
-    int32_t* nn = reinterpret_cast<int32_t*>(row + cdr_col_off(CDR_COL_N));
-    const uint32_t i = l;
-    if (k >= n_ev) {
-      tf[i] = CDR_EV_PAD;
-      eid[i] = ver[i] = ts[i] = task[i] = key[i] = aux[i] = 0;
-      hh[i] = 0;
-      nn[i] = 0;
-      continue;
-    }
-    const cdr_event& e = ev[k];
-    uint32_t flags = (e.flags & CDR_EVF_BATCH_FIRST) || k == 0 ? CDR_SEF_BATCH_FIRST : 0;
+// one event (or padding when e == nullptr) into element i of the slab row `row`;
+// attribute records go to the arena at *apos
+void put_event(uint8_t* row, uint32_t i, const cdr_event* ep, bool first, uint64_t* apos_p, uint64_t* arena) {
+  int64_t* eid = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_EVENT_ID));
+  int64_t* ver = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_VERSION));
+  int64_t* ts = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_TIMESTAMP));
+  int64_t* task = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_TASK_ID));
+  int64_t* key = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_KEY));
+  int64_t* aux = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_AUX));
+  uint32_t* tf = reinterpret_cast<uint32_t*>(row + cdr_col_off(CDR_COL_TYPE_FLAGS));
+  uint32_t* hh = reinterpret_cast<uint32_t*>(row + cdr_col_off(CDR_COL_H));
+  int32_t* nn = reinterpret_cast<int32_t*>(row + cdr_col_off(CDR_COL_N));
+  if (!ep) {
+    tf[i] = CDR_EV_PAD;
+    eid[i] = ver[i] = ts[i] = task[i] = key[i] = aux[i] = 0;
+    hh[i] = 0;
+    nn[i] = 0;
+    return;
+  }
+  uint64_t& apos = *apos_p;
+  {
+    const cdr_event& e = *ep;
+    uint32_t flags = (e.flags & CDR_EVF_BATCH_FIRST) || first ? CDR_SEF_BATCH_FIRST : 0;
     int64_t kk = 0, ax = 0;
     uint32_t h = 0;
     int32_t n = 0;
@@ -269,6 +274,24 @@ void pack_lane(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t len, 
   }
 }
 
+void pack_lane(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t len, uint32_t l, uint64_t apos,
+               const cdr_slices* o) {
+  uint8_t* const blk0 = const_cast<uint8_t*>(o->slab) + row0 * CDR_ROW_BYTES;
+  uint64_t* arena = const_cast<uint64_t*>(o->arena);
+  for (uint32_t k = 0; k < len; k++)
+    put_event(blk0 + (uint64_t)k * CDR_ROW_BYTES, l, k < n_ev ? ev + k : nullptr, k == 0, &apos, arena);
+}
+
+// a wave slice: event k of the one workflow in row k/64, lane k%64 (cdr.h)
+void pack_chunked(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t rows, uint64_t apos,
+                  const cdr_slices* o) {
+  uint8_t* const blk0 = const_cast<uint8_t*>(o->slab) + row0 * CDR_ROW_BYTES;
+  uint64_t* arena = const_cast<uint64_t*>(o->arena);
+  for (uint64_t k = 0; k < (uint64_t)rows * CDR_SLICE_WIDTH; k++)
+    put_event(blk0 + (k / CDR_SLICE_WIDTH) * CDR_ROW_BYTES, (uint32_t)(k % CDR_SLICE_WIDTH),
+              k < n_ev ? ev + k : nullptr, k == 0, &apos, arena);
+}
+
 }  // namespace cdr_internal
 
 extern "C" {
@@ -321,31 +344,57 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
   return CDR_API_OK;
 }
 
-int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, uint32_t* slice_len,
-                    uint64_t* slice_row0, uint32_t* n_slices, uint64_t* n_rows) {
+int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
+                       int32_t* lane_wf, uint32_t* slice_len, uint64_t* slice_row0, uint32_t* slice_flags,
+                       uint32_t* n_slices, uint64_t* n_rows, uint32_t* n_wave) {
   if (!wfs && n_wfs) return CDR_API_EINVAL;
-  uint32_t ns = (n_wfs + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH;
-  std::vector<uint32_t> order(n_wfs);
-  std::iota(order.begin(), order.end(), 0u);
+  if ((mode & CDR_PLAN_WAVE) && !caps && n_wfs) return CDR_API_EINVAL;
+  std::vector<uint32_t> lanes, waves;
+  lanes.reserve(n_wfs);
+  for (uint32_t w = 0; w < n_wfs; w++)
+    ((mode & CDR_PLAN_WAVE) && (caps[w].flags & CDR_CAP_WAVE) ? waves : lanes).push_back(w);
   // longest first: a slice's rows = its longest lane, so neighbours in length
-  // share slices and padding stays small (SELL-C-sigma with sigma = batch).
-  std::stable_sort(order.begin(), order.end(),
-                   [&](uint32_t a, uint32_t c) { return wfs[a].ev_len > wfs[c].ev_len; });
+  // share slices and padding stays small (SELL-C-sigma with sigma = batch); wave
+  // slices longest first too, so the longest histories start first
+  auto longer = [&](uint32_t a, uint32_t c) { return wfs[a].ev_len > wfs[c].ev_len; };
+  std::stable_sort(lanes.begin(), lanes.end(), longer);
+  std::stable_sort(waves.begin(), waves.end(), longer);
+  const uint32_t nl = (uint32_t)((lanes.size() + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
+  const uint32_t nw = (uint32_t)waves.size();
   uint64_t rows = 0;
-  for (uint32_t s = 0; s < ns; s++) {
-    uint32_t len = (uint32_t)wfs[order[(size_t)s * CDR_SLICE_WIDTH]].ev_len;
+  for (uint32_t s = 0; s < nl; s++) {
+    const uint32_t len = (uint32_t)wfs[lanes[(size_t)s * CDR_SLICE_WIDTH]].ev_len;
     if (slice_len) slice_len[s] = len;
     if (slice_row0) slice_row0[s] = rows;
+    if (slice_flags) slice_flags[s] = 0;
     rows += len;
     if (lane_wf)
       for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
-        size_t i = (size_t)s * CDR_SLICE_WIDTH + l;
-        lane_wf[i] = i < n_wfs ? (int32_t)order[i] : -1;
+        const size_t i = (size_t)s * CDR_SLICE_WIDTH + l;
+        lane_wf[i] = i < lanes.size() ? (int32_t)lanes[i] : -1;
       }
   }
-  if (n_slices) *n_slices = ns;
+  for (uint32_t q = 0; q < nw; q++) {
+    const uint32_t s = nl + q;
+    const uint32_t len = (uint32_t)((wfs[waves[q]].ev_len + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
+    if (slice_len) slice_len[s] = len;
+    if (slice_row0) slice_row0[s] = rows;
+    if (slice_flags) slice_flags[s] = CDR_SLICE_WAVE;
+    rows += len;
+    if (lane_wf)
+      for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++)
+        lane_wf[(size_t)s * CDR_SLICE_WIDTH + l] = l == 0 ? (int32_t)waves[q] : -1;
+  }
+  if (n_slices) *n_slices = nl + nw;
   if (n_rows) *n_rows = rows;
+  if (n_wave) *n_wave = nw;
   return CDR_API_OK;
+}
+
+int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, uint32_t* slice_len,
+                    uint64_t* slice_row0, uint32_t* n_slices, uint64_t* n_rows) {
+  return cdr_plan_slices_ex(wfs, nullptr, n_wfs, 0, lane_wf, slice_len, slice_row0, nullptr, n_slices, n_rows,
+                            nullptr);
 }
 
 int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n_slices, uint64_t* scratch_off,
@@ -355,6 +404,13 @@ int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n
   uint64_t off = 0;
   uint32_t nf = 0;
   for (uint32_t s = 0; s < n_slices; s++) {
+    if (slice_flags && (slice_flags[s] & CDR_SLICE_WAVE)) {  // lane-distributed tables: no scratch
+      if (scratch_off) scratch_off[s] = off;
+      if (act_slots) act_slots[s] = 0;
+      if (tim_slots) tim_slots[s] = 0;
+      slice_flags[s] = CDR_SLICE_WAVE;
+      continue;
+    }
     uint32_t a = 0, t = 0, lanes = 0;
     bool fast = true;
     for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
@@ -400,6 +456,15 @@ int cdr_pack_slices(const cdr_batch* b, cdr_slices* o, int threads) {
   parallel_for(o->n_slices, threads, [&](uint64_t s) {
     const uint64_t row0 = o->slice_row0[s];
     const uint32_t len = o->slice_len[s];
+    if (o->slice_flags && (o->slice_flags[s] & CDR_SLICE_WAVE)) {
+      const int32_t w = o->lane_wf[s * CDR_SLICE_WIDTH];
+      if (w < 0 || b->wfs[w].ev_len > (uint64_t)len * CDR_SLICE_WIDTH) {
+        bad = 1;
+        return;
+      }
+      cdr_internal::pack_chunked(b->events + b->wfs[w].ev_off, b->wfs[w].ev_len, row0, len, arena_base[w], o);
+      return;
+    }
     for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
       const int32_t w = o->lane_wf[s * CDR_SLICE_WIDTH + l];
       if (w >= 0 && b->wfs[w].ev_len > len) {

@@ -16,6 +16,8 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* c)
 // Pack one workflow's events into lane `lane` of a slice whose first row is row0 and
 // whose length is len (rows beyond n are padding).  `apos` is the workflow's arena
 // word offset; kv/rp offsets inside the events are rebased by kv_base/rp_base.
+void pack_chunked(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t rows, uint64_t apos,
+                  const cdr_slices* o);
 void pack_lane(const cdr_event* ev, uint64_t n, uint64_t row0, uint32_t len, uint32_t lane, uint64_t apos,
                const cdr_slices* o);
 

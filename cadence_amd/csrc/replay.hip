@@ -474,7 +474,11 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   const uint32_t tim_cap = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_tim_slots[s]);
   const uint32_t la = KA()->la, lt = KA()->lt;
   if ((act_cap <= la && tim_cap <= lt) != LDS) return;
-  if (KA()->fast && (__builtin_amdgcn_readfirstlane(KA()->B.ev.slice_flags[s]) & CDR_SLICE_FAST)) return;
+  {
+    const uint32_t sf = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_flags[s]);
+    if (sf & CDR_SLICE_WAVE) return;  // k_replay_wave
+    if (KA()->fast && (sf & CDR_SLICE_FAST)) return;
+  }
   const uint64_t row0_ = KA()->B.ev.slice_row0[s];
   const uint64_t row0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(row0_ >> 32)) << 32) |
                         __builtin_amdgcn_readfirstlane((uint32_t)row0_);
@@ -1358,6 +1362,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
 }
 
 #include "replay_fast.inc"
+#include "replay_wave.inc"
 
 // Per-workflow table epilogue: move live rows to the front in key order (the
 // canonical order of the Go maps' keys), sort the SearchAttributes map by key, and
@@ -1418,6 +1423,7 @@ __global__ void k_finalize(cdr_dev_batch B, cdr_out O) {
 struct cdr_ctx {
   int device;
   int fast = 1;  // cdr_set_fast_path
+  uint32_t plan_mode = CDR_PLAN_WAVE;  // cdr_set_plan_mode
   hipEvent_t ev[4];
   bool timed;
   // optional per-launch timing ring (bench): event pairs around every replay kernel
@@ -1458,6 +1464,14 @@ int cdr_set_fast_path(cdr_ctx* c, int enable) {
   return old;
 }
 
+int cdr_set_plan_mode(cdr_ctx* c, uint32_t mode) {
+  if (!c || (mode & ~CDR_PLAN_WAVE)) return CDR_API_EINVAL;
+  const uint32_t old = c->plan_mode;
+  c->plan_mode = mode;
+  return (int)old;
+}
+uint32_t cdr_get_plan_mode(const cdr_ctx* c) { return c ? c->plan_mode : 0u; }
+
 void cdr_destroy(cdr_ctx* c) {
   if (!c) return;
   for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
@@ -1477,12 +1491,15 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const bool spill = in->max_act_slots > la || in->max_tim_slots > lt;
   const uint32_t blocks = in->ev.n_slices;
   const bool fast = c->fast && in->n_fast_slices > 0;
-  const bool general = !fast || in->n_fast_slices < in->ev.n_slices;
+  const bool wave = in->n_wave_slices > 0;
+  const bool general = (fast ? in->n_fast_slices : 0u) + in->n_wave_slices < in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
   cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, 0u};
   if (blocks && fast)
     hipLaunchKernelGGL(k_replay_fast, dim3(blocks), dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, st, L);
+  HIPCHK(hipGetLastError());
+  if (blocks && wave) hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
   HIPCHK(hipGetLastError());
   if (blocks && general) hipLaunchKernelGGL(k_replay<true>, dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, L);
   HIPCHK(hipGetLastError());

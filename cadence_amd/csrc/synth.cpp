@@ -771,6 +771,7 @@ int cdr_synth_sliced_plan(const cdr_synth_params* p, cdr_synth_plan_info* info) 
   size_pass(*p, S, 0, true);
   cdr_synth_plan_info z{};
   std::vector<cdr_wf_desc> lens;
+  std::vector<cdr_wf_caps> lcaps;
   for (uint32_t w = 0; w < p->n_wfs; w++) {
     z.n_events += S.n_ev[w] + S.n_nr[w];
     z.n_entries += 1 + (S.has_nr[w] ? 1 : 0);
@@ -790,11 +791,13 @@ int cdr_synth_sliced_plan(const cdr_synth_params* p, cdr_synth_plan_info* info) 
       cdr_wf_desc d{};
       d.ev_len = j == 0 ? S.n_ev[w] : S.n_nr[w];
       lens.push_back(d);
+      lcaps.push_back(*cs[j]);
     }
   }
   uint32_t ns = 0;
   uint64_t rows = 0;
-  cdr_plan_slices(lens.data(), (uint32_t)lens.size(), nullptr, nullptr, nullptr, &ns, &rows);
+  cdr_plan_slices_ex(lens.data(), lcaps.data(), (uint32_t)lens.size(), p->plan_mode, nullptr, nullptr, nullptr,
+                     nullptr, &ns, &rows, nullptr);
   z.n_slices = ns;
   z.n_rows = rows;
   *info = z;
@@ -807,6 +810,7 @@ int cdr_synth_sliced_plan(const cdr_synth_params* p, cdr_synth_plan_info* info) 
 int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc* wfs, cdr_wf_caps* caps,
                           cdr_kv* kvs, cdr_reset_point* rps, cdr_batch* meta, int threads) {
   if (!p || !o || !wfs || !caps || !meta) return CDR_API_EINVAL;
+  if (p->plan_mode && !o->slice_flags) return CDR_API_EINVAL;  // wave slices are marked there
   Sizes S;
   size_pass(*p, S, threads, true);
   const uint32_t nw = p->n_wfs;
@@ -855,8 +859,9 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
   if (ab > o->arena_words || ab >= (1ull << 32)) return CDR_API_EINVAL;  // u32 arena offsets (cdr.h)
   uint32_t ns = 0;
   uint64_t rows = 0;
-  int rc = cdr_plan_slices(lens.data(), ent, const_cast<int32_t*>(o->lane_wf), const_cast<uint32_t*>(o->slice_len),
-                           const_cast<uint64_t*>(o->slice_row0), &ns, &rows);
+  int rc = cdr_plan_slices_ex(lens.data(), caps, ent, p->plan_mode, const_cast<int32_t*>(o->lane_wf),
+                              const_cast<uint32_t*>(o->slice_len), const_cast<uint64_t*>(o->slice_row0),
+                              const_cast<uint32_t*>(o->slice_flags), &ns, &rows, nullptr);
   if (rc) return rc;
   if (ns != o->n_slices || rows != o->n_rows) return CDR_API_EINVAL;
   if (o->slice_scratch_off && o->slice_act_slots && o->slice_tim_slots) {
@@ -870,11 +875,20 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
   std::vector<uint32_t> where(ent);
   for (uint32_t i = 0; i < ns * (uint32_t)CDR_SLICE_WIDTH; i++)
     if (o->lane_wf[i] >= 0) where[o->lane_wf[i]] = i;
-  // empty lanes of the last slice
-  for (uint32_t i = ent; i < ns * (uint32_t)CDR_SLICE_WIDTH; i++) {
+  // empty lanes of lane slices (wave slices pad their own last row)
+  auto is_wave = [&](uint32_t s) { return o->slice_flags && (o->slice_flags[s] & CDR_SLICE_WAVE); };
+  for (uint32_t i = 0; i < ns * (uint32_t)CDR_SLICE_WIDTH; i++) {
     const uint32_t s = i / CDR_SLICE_WIDTH;
-    cdr_internal::pack_lane(nullptr, 0, o->slice_row0[s], o->slice_len[s], i % CDR_SLICE_WIDTH, 0, o);
+    if (o->lane_wf[i] < 0 && !is_wave(s))
+      cdr_internal::pack_lane(nullptr, 0, o->slice_row0[s], o->slice_len[s], i % CDR_SLICE_WIDTH, 0, o);
   }
+  auto pack = [&](const std::vector<cdr_event>& ev, uint32_t at, uint64_t apos) {
+    const uint32_t s = at / CDR_SLICE_WIDTH;
+    if (is_wave(s))
+      cdr_internal::pack_chunked(ev.data(), ev.size(), o->slice_row0[s], o->slice_len[s], apos, o);
+    else
+      cdr_internal::pack_lane(ev.data(), ev.size(), o->slice_row0[s], o->slice_len[s], at % CDR_SLICE_WIDTH, apos, o);
+  };
   par(nw, threads, [&](uint32_t w) {
     WfOut g;
     gen_one(*p, w, g);
@@ -886,11 +900,7 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
     cdr_wf_desc d = g.d;
     d.ev_off = 0;
     d.ev_len = g.ev.size();
-    {
-      const uint32_t at = where[i], s = at / CDR_SLICE_WIDTH;
-      cdr_internal::pack_lane(g.ev.data(), g.ev.size(), o->slice_row0[s], o->slice_len[s], at % CDR_SLICE_WIDTH,
-                              arena_base[i], o);
-    }
+    pack(g.ev, where[i], arena_base[i]);
     if (g.has_newrun) {
       d.newrun = (int32_t)(i + 1);
       cdr_wf_desc n = g.d;
@@ -906,9 +916,7 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
       n.newrun_call = 0;
       n.newrun_ndc = 0;
       wfs[i + 1] = n;
-      const uint32_t at = where[i + 1], s = at / CDR_SLICE_WIDTH;
-      cdr_internal::pack_lane(g.newrun.data(), g.newrun.size(), o->slice_row0[s], o->slice_len[s],
-                              at % CDR_SLICE_WIDTH, arena_base[i + 1], o);
+      pack(g.newrun, where[i + 1], arena_base[i + 1]);
     }
     wfs[i] = d;
   });

@@ -109,17 +109,27 @@ class Plan:
     totals: abi.CdrTotals
 
 
-def fast_slices(batch: Batch, pl: "Plan | None" = None) -> tuple:
-    """(fast-path slices, slices) of the batch's slice plan (host planner only)."""
+def slice_kinds(batch: Batch, pl: "Plan | None" = None, mode: int = abi.PLAN_WAVE) -> tuple:
+    """(fast-path slices, wave slices, slices) of the batch's slice plan (host planner only)."""
     L = abi.lib()
     pl = pl or plan(batch)
-    ns, rows = C.c_uint32(), C.c_uint64()
-    L.cdr_plan_slices(batch.wfs, batch.n_wfs, None, None, None, C.byref(ns), C.byref(rows))
+    ns, rows, nw = C.c_uint32(), C.c_uint64(), C.c_uint32()
+    L.cdr_plan_slices_ex(batch.wfs, pl.caps, batch.n_wfs, mode, None, None, None, None, C.byref(ns), C.byref(rows),
+                         C.byref(nw))
     lane = np.zeros(max(1, ns.value) * 64, np.int32)
-    L.cdr_plan_slices(batch.wfs, batch.n_wfs, lane.ctypes.data, None, None, C.byref(ns), C.byref(rows))
+    flags = np.zeros(max(1, ns.value), np.uint32)
+    L.cdr_plan_slices_ex(batch.wfs, pl.caps, batch.n_wfs, mode, lane.ctypes.data, None, None, flags.ctypes.data,
+                         C.byref(ns), C.byref(rows), C.byref(nw))
     words, nf = C.c_uint64(), C.c_uint32()
-    L.cdr_plan_scratch(pl.caps, lane.ctypes.data, ns.value, None, None, None, None, C.byref(words), C.byref(nf))
-    return nf.value, ns.value
+    L.cdr_plan_scratch(pl.caps, lane.ctypes.data, ns.value, None, None, None, flags.ctypes.data, C.byref(words),
+                       C.byref(nf))
+    return nf.value, nw.value, ns.value
+
+
+def fast_slices(batch: Batch, pl: "Plan | None" = None) -> tuple:
+    """(fast-path slices, slices) of the batch's lane-slice plan (no wave slices)."""
+    nf, _, ns = slice_kinds(batch, pl, 0)
+    return nf, ns
 
 
 def plan(batch: Batch) -> Plan:
@@ -167,12 +177,19 @@ class Outputs:
 class Engine:
     """One device context (the analogue of one stateBuilder provider)."""
 
-    def __init__(self, device: int = 0, fast_path: bool = True):
+    def __init__(self, device: int = 0, fast_path: bool = True, wave: bool = True):
         L = abi.lib()
         self.ctx = L.cdr_create(device)
         if not self.ctx:
             raise RuntimeError("cdr_create failed: no usable HIP device (the engine has no CPU fallback)")
         L.cdr_set_fast_path(self.ctx, 1 if fast_path else 0)
+        L.cdr_set_plan_mode(self.ctx, abi.PLAN_WAVE if wave else 0)
+
+    def set_wave(self, enable: bool) -> bool:
+        """Plan divergent histories into wave slices (one wavefront per workflow,
+        replay_wave.inc; default) or into lane slices of the general kernel; returns
+        the previous setting."""
+        return bool(abi.lib().cdr_set_plan_mode(self.ctx, abi.PLAN_WAVE if enable else 0))
 
     def set_fast_path(self, enable: bool) -> bool:
         """Route sequential-activity slices to the fast-path kernel (default) or replay

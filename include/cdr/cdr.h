@@ -112,6 +112,10 @@ typedef struct cdr_slices {
   const uint32_t* slice_flags;       /* [n_slices] CDR_SLICE_* */
 } cdr_slices;
 #define CDR_SLICE_FAST 0x1u /* every lane's history has CDR_CAP_FAST */
+/* a wave slice: ONE workflow (lane_wf[64 s]; the other lanes -1) replayed by a whole
+ * wavefront (replay_wave.inc); its slice_len rows hold the workflow's events 64 at a
+ * time, event k in row k/64, lane k%64 (cdr_plan_slices_ex with CDR_PLAN_WAVE) */
+#define CDR_SLICE_WAVE 0x2u
 /* event types the fast-path kernel replays (bit = cdr_event_type) */
 #define CDR_FAST_TYPES                                                                                       \
   (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_WF_COMPLETED) | CDR_TB(CDR_EV_WF_FAILED) |                      \
@@ -184,7 +188,8 @@ typedef struct cdr_dev_batch {
   /* max over slices of slice_act_slots / slice_tim_slots (cdr_plan_scratch): the
    * launcher keeps up to this many working slots per lane in LDS (0 = all in scratch) */
   uint32_t max_act_slots, max_tim_slots;
-  uint32_t n_fast_slices, _pad2; /* slices with CDR_SLICE_FAST (cdr_plan_scratch) */
+  uint32_t n_fast_slices; /* slices with CDR_SLICE_FAST (cdr_plan_scratch) */
+  uint32_t n_wave_slices; /* slices with CDR_SLICE_WAVE (cdr_plan_slices_ex) */
   cdr_cluster_meta cluster;
   int64_t now_ns;
   uint64_t uuid_seed;
@@ -204,8 +209,18 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals);
 int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, uint32_t* slice_len,
                     uint64_t* slice_row0, uint32_t* n_slices, uint64_t* n_rows);
 
+/* As cdr_plan_slices, with a mode: CDR_PLAN_WAVE gives every entry whose caps carry
+ * CDR_CAP_WAVE a wave slice of its own (after the lane slices, longest first) and
+ * marks it in slice_flags (nullable; the other slices get 0).  `caps` may be NULL
+ * when mode is 0.  Returns the number of wave slices via *n_wave (nullable). */
+#define CDR_PLAN_WAVE 0x1u
+int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
+                       int32_t* lane_wf, uint32_t* slice_len, uint64_t* slice_row0, uint32_t* slice_flags,
+                       uint32_t* n_slices, uint64_t* n_rows, uint32_t* n_wave);
+
 /* Working-state scratch layout: per slice, slots = max over its lanes of the live
- * bounds in caps, and the slice's CDR_SLICE_* flags; returns the total words via
+ * bounds in caps, and the slice's CDR_SLICE_* flags (CDR_SLICE_WAVE, when set on input by
+ * cdr_plan_slices_ex, is kept and such slices get no scratch); returns the total words via
  * *total_words and the number of CDR_SLICE_FAST slices via *n_fast (nullable).
  * Outputs sized [n_slices]; pass NULL outputs to query the totals only. */
 int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n_slices, uint64_t* scratch_off,
@@ -229,6 +244,10 @@ void cdr_destroy(cdr_ctx* ctx);
 /* Route CDR_SLICE_FAST slices to the fast-path kernel (default 1) or replay every
  * slice with the general kernel (0; parity tests run both).  Returns the old value. */
 int cdr_set_fast_path(cdr_ctx* ctx, int enable);
+
+/* Slicing mode of cdr_replay_batch's planning (CDR_PLAN_*; default CDR_PLAN_WAVE).
+ * Returns the previous mode. */
+int cdr_set_plan_mode(cdr_ctx* ctx, uint32_t mode);
 
 /* Replay a device-resident sliced batch into device-resident outputs on `stream`
  * (a hipStream_t; NULL = default stream).  Asynchronous: enqueues the replay

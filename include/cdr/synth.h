@@ -19,7 +19,7 @@ typedef struct cdr_synth_params {
   int32_t builder;      /* -1 = config default, else cdr_builder */
   int32_t rebuild;      /* set expected_next_event_id (nDCStateRebuilder check) */
   uint32_t fault_kinds; /* bit i allows injected fault kind i (synth.cpp inject_fault); 0 = all */
-  uint32_t _pad;
+  uint32_t plan_mode;   /* CDR_PLAN_* of the sliced layout (cdr_plan_slices_ex) */
   const uint32_t* index_map; /* optional [n_wfs]: global index of each generated workflow */
 } cdr_synth_params;
 typedef struct cdr_synth_sizes {

@@ -166,3 +166,55 @@ def test_fast_path_eligibility():
         assert (nf == ns) if expect_all else (nf < ns), (cfg, builder, nf, ns)
     pl = engine.plan(engine.synth_batch(2, 64, seed=1))
     assert all(pl.caps[w].flags & abi.CAP_FAST for w in range(64))
+
+
+def test_wave_slices_plan_and_pack():
+    """CDR_PLAN_WAVE: divergent entries get one wave slice each (after the lane
+    slices), their events packed 64 to a row (event k in row k/64, lane k%64)."""
+    b = engine.synth_batch(3, 150, seed=11)
+    pl = engine.plan(b)
+    L = abi.lib()
+    ns, rows, nw = C.c_uint32(), C.c_uint64(), C.c_uint32()
+    L.cdr_plan_slices_ex(b.wfs, pl.caps, b.n_wfs, abi.PLAN_WAVE, None, None, None, None, C.byref(ns),
+                         C.byref(rows), C.byref(nw))
+    lane = np.zeros(ns.value * 64, np.int32)
+    slen = np.zeros(ns.value, np.uint32)
+    row0 = np.zeros(ns.value, np.uint64)
+    flags = np.zeros(ns.value, np.uint32)
+    L.cdr_plan_slices_ex(b.wfs, pl.caps, b.n_wfs, abi.PLAN_WAVE, lane.ctypes.data, slen.ctypes.data,
+                         row0.ctypes.data, flags.ctypes.data, C.byref(ns), C.byref(rows), C.byref(nw))
+    waves = np.nonzero(flags & abi.SLICE_WAVE)[0]
+    assert len(waves) == nw.value > 0
+    wave_wfs = {int(lane[s * 64]) for s in waves}
+    assert all((pl.caps[w].flags & abi.CAP_WAVE) for w in wave_wfs)
+    assert all((lane[s * 64 + 1:(s + 1) * 64] == -1).all() for s in waves)
+    # every entry exactly once
+    placed = sorted(int(x) for x in lane if x >= 0)
+    assert placed == list(range(b.n_wfs))
+    # scratch planning keeps the wave flag and gives wave slices no slots
+    words, nf = C.c_uint64(), C.c_uint32()
+    act = np.zeros(ns.value, np.uint32)
+    L.cdr_plan_scratch(pl.caps, lane.ctypes.data, ns.value, None, act.ctypes.data, None, flags.ctypes.data,
+                       C.byref(words), C.byref(nf))
+    assert (flags[waves] == abi.SLICE_WAVE).all() and (act[waves] == 0).all()
+    # pack and read back one wave workflow
+    aw = L.cdr_plan_arena_words(C.byref(b.cstruct()))
+    slab = np.zeros(int(rows.value) * 64 * abi.EL_BYTES, np.uint8)
+    arena = np.zeros(max(1, aw), np.uint64)
+    s_ = abi.CdrSlices(n_slices=ns.value, n_rows=rows.value, arena_words=aw)
+    s_.slice_row0, s_.slice_len, s_.lane_wf = row0.ctypes.data, slen.ctypes.data, lane.ctypes.data
+    s_.slab, s_.arena, s_.slice_flags = slab.ctypes.data, arena.ctypes.data, flags.ctypes.data
+    assert L.cdr_pack_slices(C.byref(b.cstruct()), C.byref(s_), 2) == 0
+    cols = abi.slab_columns(slab)
+    s = int(waves[len(waves) // 2])
+    w = int(lane[s * 64])
+    d = b.wfs[w]
+    n = int(d.ev_len)
+    assert slen[s] == (n + 63) // 64
+    r0 = int(row0[s])
+    got = cols["event_id"][r0 * 64:(r0 + int(slen[s])) * 64][:n]
+    want = [b.events[d.ev_off + k].event_id for k in range(n)]
+    assert got.tolist() == want
+    tf = cols["type_flags"][r0 * 64:(r0 + int(slen[s])) * 64]
+    assert [int(x) & 0xFF for x in tf[:n]] == [b.events[d.ev_off + k].type for k in range(n)]
+    assert all((int(x) & 0xFF) == 0xFF for x in tf[n:])

@@ -12,18 +12,30 @@ from cadence_amd import abi, engine
 pytestmark = pytest.mark.gpu
 
 
-def _check(batch, eng, both_paths=False):
+def _check(batch, eng, both_paths=False, lanes=True):
+    """Default routing (fast-path, wave and lane slices) vs the oracle; `lanes`: again
+    with no wave slices (divergent histories on the lane-per-workflow general kernel);
+    `both_paths`: again with the fast path off too (everything on the general kernel)."""
     import oracle
     ref = oracle.replay(batch)
     got = eng.replay(batch)
     bad = engine.compare(batch, got, ref)
-    assert not bad, "\n".join(bad[:10])
+    assert not bad, "default routing: " + "\n".join(bad[:10])
+    if lanes:
+        old = eng.set_wave(False)
+        try:
+            got = eng.replay(batch)
+        finally:
+            eng.set_wave(old)
+        bad = engine.compare(batch, got, ref)
+        assert not bad, "lane slices only: " + "\n".join(bad[:10])
     if both_paths:  # the same batch through the general kernel only
-        old = eng.set_fast_path(False)
+        old, oldw = eng.set_fast_path(False), eng.set_wave(False)
         try:
             got = eng.replay(batch)
         finally:
             eng.set_fast_path(old)
+            eng.set_wave(oldw)
         bad = engine.compare(batch, got, ref)
         assert not bad, "general kernel: " + "\n".join(bad[:10])
     return ref
@@ -32,6 +44,8 @@ def _check(batch, eng, both_paths=False):
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 0])
 def test_synth_configs_clean(engine_gpu, cfg):
     b = engine.synth_batch(cfg, 300, seed=0x5EED0000 + cfg)
+    if cfg in (3, 4, 5, 0):  # divergent shapes: the wave kernel must be exercised
+        assert engine.slice_kinds(b)[1] > 0
     ref = _check(b, engine_gpu)
     assert engine.status_histogram(ref).get("OK", 0) > 0
 
@@ -59,6 +73,16 @@ def test_rebuild_next_event_check(engine_gpu):
 def test_long_histories(engine_gpu):
     b = engine.synth_batch(4, 40, seed=5, target_len=3000, max_len=20000)
     _check(b, engine_gpu)
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 5])
+def test_wave_kernel_configs(engine_gpu, cfg):
+    """Larger divergent batches (every entry that fits the wave kernel gets a wave
+    slice), checked against the oracle only."""
+    b = engine.synth_batch(cfg, 1500, seed=0x5EED0100 + cfg, error_rate=0.1)
+    nf, nw, ns = engine.slice_kinds(b)
+    assert nw > 0, (nf, nw, ns)
+    _check(b, engine_gpu, lanes=False)
 
 
 @pytest.mark.parametrize("cfg", [1, 2])
