@@ -77,7 +77,20 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   bool have_ver = false;
   int64_t last_ver = 0;
   uint32_t vh = 0;
-  int64_t live = 0, live_max = 0, tlive = 0, tlive_max = 0;
+  int64_t live = 0, live_max = 0;
+  // live sets of the wave kernel's lane tables, simulated by key (its slots are
+  // reused first-free, so a table's high-water mark is its peak live count)
+  std::vector<int64_t> lv[4];  // user timers (timer id), children, request-cancels, signals (initiated id)
+  size_t lv_max[4] = {0, 0, 0, 0};
+  auto lv_add = [&](int t, int64_t key, bool unique) {
+    if (unique && std::find(lv[t].begin(), lv[t].end(), key) != lv[t].end()) return;
+    lv[t].push_back(key);
+    lv_max[t] = std::max(lv_max[t], lv[t].size());
+  };
+  auto lv_del = [&](int t, int64_t key) {
+    auto it = std::find(lv[t].begin(), lv[t].end(), key);
+    if (it != lv[t].end()) lv[t].erase(it);
+  };
   for (uint64_t k = 0; k < n; k++) {
     const cdr_event& e = ev[k];
     // live-activity bound: a close of a missing activity stops the replay, so before
@@ -86,9 +99,20 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
     if (e.type == CDR_EV_AT_COMPLETED || e.type == CDR_EV_AT_FAILED || e.type == CDR_EV_AT_TIMED_OUT ||
         e.type == CDR_EV_AT_CANCELED)
       live = std::max<int64_t>(0, live - 1);
-    // live user timers: an upper bound (a restarted live timer reuses its slot)
-    if (e.type == CDR_EV_TIMER_STARTED) tlive_max = std::max(tlive_max, ++tlive);
-    if (e.type == CDR_EV_TIMER_FIRED || e.type == CDR_EV_TIMER_CANCELED) tlive = std::max<int64_t>(0, tlive - 1);
+    switch (e.type) {
+      case CDR_EV_TIMER_STARTED: lv_add(0, e.a.timer.timer_id, true); break;
+      case CDR_EV_TIMER_FIRED: case CDR_EV_TIMER_CANCELED: lv_del(0, e.a.timer.timer_id); break;
+      case CDR_EV_CHILD_INITIATED: lv_add(1, e.event_id, false); break;
+      case CDR_EV_CHILD_START_FAILED: case CDR_EV_CHILD_COMPLETED: case CDR_EV_CHILD_FAILED:
+      case CDR_EV_CHILD_CANCELED: case CDR_EV_CHILD_TIMED_OUT: case CDR_EV_CHILD_TERMINATED:
+        lv_del(1, e.a.ref.initiated_event_id);
+        break;
+      case CDR_EV_RCE_INITIATED: lv_add(2, e.event_id, false); break;
+      case CDR_EV_RCE_FAILED: case CDR_EV_EXT_CANCEL_REQUESTED: lv_del(2, e.a.ref.initiated_event_id); break;
+      case CDR_EV_SE_INITIATED: lv_add(3, e.event_id, false); break;
+      case CDR_EV_SE_FAILED: case CDR_EV_EXT_SIGNALED: lv_del(3, e.a.ref.initiated_event_id); break;
+      default: break;
+    }
     fast = fast && e.type < 64 && (CDR_FAST_TYPES & (1ull << e.type)) && (k == 0 || e.type != CDR_EV_WF_STARTED);
     if (!have_ver || e.version > last_ver) {
       vh++;
@@ -130,8 +154,10 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   c.timer_live = c.timer_cap;
   c.flags = (fast && live_max <= 1) ? CDR_CAP_FAST : 0u;
   const uint32_t W = CDR_WAVE_SLOTS;
-  if (!(c.flags & CDR_CAP_FAST) && live_max <= (int64_t)W && tlive_max <= (int64_t)W && c.child_cap <= W &&
-      c.cancel_cap <= W && c.signal_cap <= W && c.sa_cap <= W)
+  // the wave kernel keeps one slot per lane and reuses freed slots first, so its
+  // high-water marks are the peak live counts
+  if (!(c.flags & CDR_CAP_FAST) && live_max <= (int64_t)W && lv_max[0] <= W && lv_max[1] <= W && lv_max[2] <= W &&
+      lv_max[3] <= W)
     c.flags |= CDR_CAP_WAVE;
   *out = c;
 }

@@ -492,8 +492,8 @@ typedef struct cdr_wf_caps {
  * NDC or local */
 #define CDR_CAP_FAST 0x1u
 /* the history fits the wave-per-workflow kernel (replay_wave.inc): at most 64 live
- * activities and timers and at most 64 children, request-cancels, signals and
- * search attributes; not CDR_CAP_FAST */
+ * activities, user timers, children, request-cancels and signals at any time; not
+ * CDR_CAP_FAST */
 #define CDR_CAP_WAVE 0x2u
 #define CDR_WAVE_SLOTS 64u
 
