@@ -105,3 +105,52 @@ def test_fast_path_builders(engine_gpu, builder, err):
     if err == 0.0:  # faults may leave two activities pending (not a fast-path shape)
         assert nf == ns
     _check(b, engine_gpu, both_paths=True)
+
+
+def _overflow_history(hb, wid, n_sa, n_rp, builder):
+    from cadence_amd.history import HistoryBuilder  # noqa: F401  (hb is one)
+    w = hb.workflow(workflow_id=wid, run_id=wid + "-run", request_id="q", builder=builder, failover_version=1)
+    t = 1_600_000_000 * 10 ** 9
+    ev = lambda i, ty, **a: dict(eventId=i, version=1, timestamp=t + i, eventType=ty, **a)  # noqa: E731
+    started = ev(1, "WorkflowExecutionStarted", workflowExecutionStartedEventAttributes={
+        "workflowType": {"name": "wt"}, "taskList": {"name": "tl"}, "executionStartToCloseTimeoutSeconds": 60,
+        "taskStartToCloseTimeoutSeconds": 10,
+        "searchAttributes": {"indexedFields": {f"key-{i}": f"v-{i}" for i in range(n_sa)}},
+        "prevAutoResetPoints": {"points": [{"binaryChecksum": f"cks-{i}", "runId": "old-run",
+                                            "firstDecisionCompletedId": 4, "createdTimeNano": 5,
+                                            "resettable": True} for i in range(n_rp)]}})
+    calls = [[started, ev(2, "DecisionTaskScheduled", decisionTaskScheduledEventAttributes={
+        "startToCloseTimeoutSeconds": 10, "attempt": 0})]]
+    i = 3
+    for cks in [f"cks-{n_rp - 1}", "cks-3", "brand-new", f"cks-{n_rp // 2}", "brand-new", "another"]:
+        calls.append([ev(i, "DecisionTaskStarted", decisionTaskStartedEventAttributes={
+            "scheduledEventId": i - 1, "requestId": f"r{i}"})])
+        calls.append([ev(i + 1, "DecisionTaskCompleted", decisionTaskCompletedEventAttributes={
+            "scheduledEventId": i - 1, "startedEventId": i, "binaryChecksum": cks}),
+            ev(i + 2, "UpsertWorkflowSearchAttributes", upsertWorkflowSearchAttributesEventAttributes={
+                "searchAttributes": {"indexedFields": {f"key-{n_sa - 1}": f"w{i}", "key-1": f"w{i}",
+                                                       f"fresh-{i}": "x"}}}),
+            ev(i + 3, "DecisionTaskScheduled", decisionTaskScheduledEventAttributes={
+                "startToCloseTimeoutSeconds": 10, "attempt": 0})])
+        i += 4
+    calls.append([ev(i, "DecisionTaskStarted", decisionTaskStartedEventAttributes={
+        "scheduledEventId": i - 1, "requestId": "r"})])
+    calls.append([ev(i + 1, "DecisionTaskCompleted", decisionTaskCompletedEventAttributes={
+        "scheduledEventId": i - 1, "startedEventId": i}),
+        ev(i + 2, "WorkflowExecutionCompleted", workflowExecutionCompletedEventAttributes={})])
+    w.calls = calls
+
+
+@pytest.mark.parametrize("n", [10, 64, 65, 150])
+def test_wave_kernel_table_overflow(engine_gpu, n):
+    """More than 64 search attributes and reset points: the wave kernel's lane tables
+    hold the first 64, the rest are looked up in their output rows."""
+    from cadence_amd.history import HistoryBuilder
+    hb = HistoryBuilder()
+    for j, bld in enumerate([abi.BUILDER_NDC, abi.BUILDER_2DC, abi.BUILDER_LOCAL]):
+        _overflow_history(hb, f"wf-{j}", n, n, bld)
+    b = hb.build()
+    nf, nw, ns = engine.slice_kinds(b)
+    assert nw == 3, (nf, nw, ns)
+    ref = _check(b, engine_gpu)
+    assert engine.status_histogram(ref) == {"OK": 3}
