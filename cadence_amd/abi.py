@@ -193,6 +193,7 @@ SLAB_COLS = (("event_id", np.int64), ("version", np.int64), ("timestamp", np.int
              ("key", np.int64), ("aux", np.int64), ("type_flags", np.uint32), ("h", np.uint32), ("n", np.int32))
 EL_BYTES = sum(np.dtype(t).itemsize for _, t in SLAB_COLS)  # CDR_EL_BYTES
 SEF_BATCH_FIRST, SEF_DOMAIN_MISSING = 1 << 8, 1 << 9
+SEF_ID_NEXT, SEF_VER_SAME = 1 << 21, 1 << 22  # delta bits (cdr.h)
 
 
 ROW_BYTES = EL_BYTES * SLICE_WIDTH  # CDR_ROW_BYTES

@@ -185,6 +185,10 @@ void put_event(uint8_t* row, uint32_t i, const cdr_event* ep, bool first, uint64
   {
     const cdr_event& e = *ep;
     uint32_t flags = (e.flags & CDR_EVF_BATCH_FIRST) || first ? CDR_SEF_BATCH_FIRST : 0;
+    if (!first) {  // the entry's events are contiguous: ep - 1 is the previous one
+      flags |= (uint64_t)e.event_id == (uint64_t)ep[-1].event_id + 1 ? CDR_SEF_ID_NEXT : 0u;
+      flags |= e.version == ep[-1].version ? CDR_SEF_VER_SAME : 0u;
+    }
     int64_t kk = 0, ax = 0;
     uint32_t h = 0;
     int32_t n = 0;

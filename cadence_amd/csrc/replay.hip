@@ -240,12 +240,15 @@ __device__ __forceinline__ uint32_t load_tf(const Slice& S, uint32_t o8) {
 __device__ __forceinline__ uint32_t gate(uint32_t off, uint32_t tf, uint32_t bit) {
   return off | ((tf & bit) ? 0u : OOB_BIT);
 }
+// DELTA: skip the event_id / version loads the packer's CDR_SEF_ID_NEXT / VER_SAME bits
+// make redundant (the consumer rebuilds them, ev_delta)
+template <bool DELTA = false>
 __device__ __forceinline__ Ev load_ops(const Slice& S, uint32_t o8, uint32_t tf) {
   const uint32_t o4 = o8 - S.l4;
   Ev e;
   e.tf = tf;
-  e.id = bld64(S.r, o8, S.col(CDR_COL_EVENT_ID));
-  e.ver = bld64(S.r, o8, S.col(CDR_COL_VERSION));
+  e.id = bld64(S.r, DELTA ? o8 | ((tf & CDR_SEF_ID_NEXT) ? OOB_BIT : 0u) : o8, S.col(CDR_COL_EVENT_ID));
+  e.ver = bld64(S.r, DELTA ? o8 | ((tf & CDR_SEF_VER_SAME) ? OOB_BIT : 0u) : o8, S.col(CDR_COL_VERSION));
 #if CDR_TYPED
   e.ts = bld64(S.r, gate(o8, tf, CDR_SEF_NEED_TS), S.col(CDR_COL_TIMESTAMP));
   e.key = bld64(S.r, gate(o8, tf, CDR_SEF_NEED_KEY), S.col(CDR_COL_KEY));

@@ -132,6 +132,13 @@ typedef struct cdr_slices {
 
 #define CDR_SEF_BATCH_FIRST (1u << 8)
 #define CDR_SEF_DOMAIN_MISSING (1u << 9)
+/* delta bits (set by the packer for every event after an entry's first): the event's
+ * event_id is the previous event's + 1 / its version equals the previous event's.  The
+ * columns still hold the full values; the fast-path kernel skips loading them when
+ * the bit is set (16 of the ~46 bytes a C2 event costs it) and rebuilds them from its
+ * registers */
+#define CDR_SEF_ID_NEXT (1u << 21)
+#define CDR_SEF_VER_SAME (1u << 22)
 /* operand columns the event's type reads (set by the packer from CDR_NEED_*) */
 #define CDR_SEF_NEED_TS (1u << 16)
 #define CDR_SEF_NEED_KEY (1u << 17)

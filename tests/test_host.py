@@ -89,6 +89,9 @@ def test_pack_round_trip():
             e = b.events[d.ev_off + k]
             assert cols["type_flags"][j] & 0xFF == e.type
             assert bool(cols["type_flags"][j] & abi.SEF_BATCH_FIRST) == bool(e.flags & 1 or k == 0)
+            p = b.events[d.ev_off + k - 1] if k > 0 else None
+            assert bool(cols["type_flags"][j] & abi.SEF_ID_NEXT) == (p is not None and e.event_id == p.event_id + 1)
+            assert bool(cols["type_flags"][j] & abi.SEF_VER_SAME) == (p is not None and e.version == p.version)
             need = (int(cols["type_flags"][j]) >> 16) & 0x1F  # CDR_SEF_NEED_{TS,KEY,AUX,H,N}
             if e.type == abi.EV["ActivityTaskScheduled"]:
                 assert need == 0x1F

@@ -6,7 +6,7 @@
 set -o pipefail
 tag=${1:-pmc}
 lib=${2:-cadence_amd/libcdr.so}
-shift 2 2>/dev/null
+shift; [ $# -gt 0 ] && shift
 extra="$*"
 out=gpurun_out/${tag}_pmc
 mkdir -p "$out"
