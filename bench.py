@@ -363,7 +363,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS,
                      "traffic": traffic["bytes_per_launch"] if traffic else None,
-                     "kernel": "k_replay", "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": alg_bytes,
+                     # HBM bytes actually moved per launch (PMC) / the live kernel time
+                     "traffic_gbs": traffic["bytes_per_launch"] / (kern_ms / 1e3) / 1e9 if traffic else None,
+                     "kernel": "k_replay_fast" if args.config in (1, 2) and not args.no_fast_path else "k_replay*",
+                     "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": alg_bytes,
                      "bytes_breakdown": {"events": ev_b, "per_workflow": wf_b, "pending_rows": row_b},
                      "stream_copy_peak_gbs": peak_meas},
         "cpu_baseline": cpu,
