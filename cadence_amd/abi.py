@@ -124,7 +124,7 @@ CdrClusterMeta = _S("cdr_cluster_meta", [("failover_version_increment", i64), ("
 CdrBatch = _S("cdr_batch", [
     ("events", C.POINTER(CdrEvent)), ("n_events", u64), ("wfs", C.POINTER(CdrWfDesc)), ("n_wfs", u32),
     ("empty_uuid", u32), ("kvs", C.POINTER(CdrKV)), ("n_kvs", u64), ("rps", C.POINTER(CdrResetPoint)),
-    ("n_rps", u64), ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64)])
+    ("n_rps", u64), ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64), ("carry", C.c_void_p)])
 
 # ------------------------------------------------------------------ output
 CdrExecInfo = _S("cdr_exec_info", [
@@ -178,6 +178,8 @@ CdrWfCaps = _S("cdr_wf_caps", [
 CdrTotals = _S("cdr_totals", [(n, u64) for n in ("act", "timer", "child", "cancel", "signal", "vh", "rp", "sa")])
 CdrOut = _S("cdr_out", [(n, C.c_void_p) for n in (
     "result", "exec", "repl", "vh", "act", "timer", "child", "cancel", "signal", "rp", "sa")])
+CdrCarry = _S("cdr_carry", [("src", C.c_void_p), ("caps", C.c_void_p), ("n_src", u32), ("_pad", u32),
+                            ("totals", CdrTotals), ("state", CdrOut)])
 CdrSlices = _S("cdr_slices", [
     ("n_slices", u32), ("_pad", u32), ("n_rows", u64), ("arena_words", u64)] + [(n, C.c_void_p) for n in (
         "slice_row0", "slice_len", "lane_wf", "slab", "arena", "slice_scratch_off", "slice_act_slots",
@@ -214,7 +216,7 @@ CdrDevBatch = _S("cdr_dev_batch", [
     ("ev", CdrSlices), ("scratch", C.c_void_p), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
     ("n_wfs", u32), ("empty_uuid", u32), ("max_act_slots", u32), ("max_tim_slots", u32),
     ("n_fast_slices", u32), ("n_wave_slices", u32),
-    ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64)])
+    ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64), ("carry", C.c_void_p)])
 
 # ------------------------------------------------------------------ synth
 CdrSynthParams = _S("cdr_synth_params", [
@@ -235,7 +237,7 @@ MIRRORS = {
     "cdr_vh_item": CdrVHItem, "cdr_activity_info": CdrActivityInfo, "cdr_timer_info": CdrTimerInfo,
     "cdr_child_info": CdrChildInfo, "cdr_cancel_info": CdrCancelInfo, "cdr_signal_info": CdrSignalInfo,
     "cdr_wf_result": CdrWfResult, "cdr_wf_caps": CdrWfCaps, "cdr_totals": CdrTotals, "cdr_out": CdrOut,
-    "cdr_slices": CdrSlices, "cdr_dev_batch": CdrDevBatch,
+    "cdr_slices": CdrSlices, "cdr_dev_batch": CdrDevBatch, "cdr_carry": CdrCarry,
 }
 
 # C ABI entry points declared in include/cdr/cdr.h and include/cdr/synth.h

@@ -254,6 +254,26 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   db.caps = (const cdr_wf_caps*)up(caps, (uint64_t)b->n_wfs * sizeof(cdr_wf_caps));
   db.kvs = (const cdr_kv*)up(b->kvs, b->n_kvs * sizeof(cdr_kv));
   db.rps = (const cdr_reset_point*)up(b->rps, b->n_rps * sizeof(cdr_reset_point));
+  if (b->carry && b->carry->src) {  // the loaded states, copied to the device as they are
+    const cdr_carry& hc = *b->carry;
+    const cdr_totals& t = hc.totals;
+    const uint64_t n = hc.n_src;
+    cdr_carry dc = hc;
+    dc.src = (const int32_t*)up(hc.src, (uint64_t)b->n_wfs * 4);
+    dc.caps = (const cdr_wf_caps*)up(hc.caps, n * sizeof(cdr_wf_caps));
+    dc.state.result = (cdr_wf_result*)up(hc.state.result, n * sizeof(cdr_wf_result));
+    dc.state.exec = (cdr_exec_info*)up(hc.state.exec, n * sizeof(cdr_exec_info));
+    dc.state.repl = (cdr_repl_state*)up(hc.state.repl, n * sizeof(cdr_repl_state));
+    dc.state.vh = (cdr_vh_item*)up(hc.state.vh, t.vh * sizeof(cdr_vh_item));
+    dc.state.act = (cdr_activity_info*)up(hc.state.act, t.act * sizeof(cdr_activity_info));
+    dc.state.timer = (cdr_timer_info*)up(hc.state.timer, t.timer * sizeof(cdr_timer_info));
+    dc.state.child = (cdr_child_info*)up(hc.state.child, t.child * sizeof(cdr_child_info));
+    dc.state.cancel = (cdr_cancel_info*)up(hc.state.cancel, t.cancel * sizeof(cdr_cancel_info));
+    dc.state.signal = (cdr_signal_info*)up(hc.state.signal, t.signal * sizeof(cdr_signal_info));
+    dc.state.rp = (cdr_reset_point*)up(hc.state.rp, t.rp * sizeof(cdr_reset_point));
+    dc.state.sa = (cdr_kv*)up(hc.state.sa, t.sa * sizeof(cdr_kv));
+    db.carry = (const cdr_carry*)up(&dc, sizeof(dc));
+  }
   db.n_wfs = b->n_wfs;
   db.empty_uuid = b->empty_uuid;
   db.cluster = b->cluster;

@@ -352,6 +352,26 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
     }
     cdr_wf_caps c{};
     cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c);
+    if (b->carry && b->carry->src && b->carry->src[w] >= 0) {
+      // a loaded state (cdr_carry): its rows are live from the start; only the
+      // general kernel replays onto a loaded state
+      const cdr_carry& cy = *b->carry;
+      const uint32_t src = (uint32_t)cy.src[w];
+      if (src >= cy.n_src || d.parent >= 0 || !cy.state.result) return CDR_API_EINVAL;
+      const cdr_wf_result& r = cy.state.result[src];
+      if (r.code != CDR_OK) return CDR_API_EINVAL;
+      c.act_cap += r.n_activity;
+      c.timer_cap += r.n_timer;
+      c.child_cap += r.n_child;
+      c.cancel_cap += r.n_cancel;
+      c.signal_cap += r.n_signal;
+      c.vh_cap += r.n_vh;
+      c.rp_cap += r.n_reset_points;
+      c.sa_cap += r.n_search_attr;
+      c.act_live += r.n_activity;
+      c.timer_live += r.n_timer;
+      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE);
+    }
     c.act_off = t.act;
     t.act += c.act_cap;
     c.timer_off = t.timer;
@@ -662,6 +682,7 @@ uint64_t cdr_struct_size(const char* name) {
       {"cdr_out", sizeof(cdr_out)},
       {"cdr_slices", sizeof(cdr_slices)},
       {"cdr_dev_batch", sizeof(cdr_dev_batch)},
+      {"cdr_carry", sizeof(cdr_carry)},
   };
   for (const E& e : table)
     if (std::strcmp(e.n, name) == 0) return e.s;

@@ -289,6 +289,7 @@ static_assert(TP_VER + 1 == CDR_TIM_PLANES, "timer planes");
 #define AF_CANCEL 0x4ull
 #define META_FLAG(f) ((f) << 32)
 #define META_TTS_SHIFT 40
+#define AP_CARRIED ((int64_t)1 << 62) /* AP_ROWS: row j of the loaded activity table (cdr_carry) */
 
 extern __shared__ uint64_t cdr_lds[];
 
@@ -464,6 +465,11 @@ __device__ __forceinline__ const GAS T* gp(const T* p) {
 
 // LDS = true: slices whose working slots fit (act_slots <= la, tim_slots <= lt);
 // LDS = false: the rest, with working slots in the global scratch.
+// loaded-state tables whose field names the kernel below uses as macros
+__device__ __forceinline__ const GAS cdr_reset_point* carry_rp(const GAS cdr_carry* c) { return gp(c->state.rp); }
+__device__ __forceinline__ const GAS cdr_kv* carry_sa(const GAS cdr_carry* c) { return gp(c->state.sa); }
+__device__ __forceinline__ const GAS cdr_vh_item* carry_vh(const GAS cdr_carry* c) { return gp(c->state.vh); }
+
 template <bool LDS>
 __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu(CDR_WPE, 8))) void k_replay(
     cdr_launch L) {
@@ -563,6 +569,101 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     err_k = k;               \
     stop_at_call_end = true; \
   } while (0)
+
+  // ---- carry-in (cdr_carry): start from a loaded state instead of the fresh builder
+  // (mutableStateBuilder.Load, mutableStateBuilder.go:272-295): the persisted records
+  // become the registers, working slots and output rows the replay continues from
+  const int32_t csrc = B_.carry ? gp(B_.carry)->src[w] : -1;
+  if (csrc >= 0) {
+    const GAS cdr_carry* CY = gp(B_.carry);
+    const cdr_wf_caps cc = gget(gp(CY->caps) + csrc);
+    const cdr_wf_result cr = gget(gp(CY->state.result) + csrc);
+    const cdr_exec_info x = gget(gp(CY->state.exec) + csrc);
+    gput(X, x);  // the Started half stays as loaded; the replay half is rewritten at the end
+    x_flags = x.flags;
+    x_completion_batch = x.completion_event_batch_id;
+    x_next_event = x.next_event_id;
+    x_last_processed = x.last_processed_event;
+    x_dt_timeout_value = x.decision_timeout_value;
+    x_state = x.state;
+    x_close = x.close_status;
+    x_signals = x.signal_count;
+    dv = x.decision_version;
+    dsched = x.decision_schedule_id;
+    dstart = x.decision_started_id;
+    datt = x.decision_attempt;
+    dst_ts = x.decision_started_ts;
+    dsc_ts = x.decision_scheduled_ts;
+    dorig_ts = x.decision_original_scheduled_ts;
+    dreq = x.decision_request_id;
+    dto = x.decision_timeout;
+    curv = CDR_EMPTY_VERSION;  // :291
+    if (isRS) {
+      const cdr_repl_state rs0 = gget(gp(CY->state.repl) + csrc);
+      gput(RS, rs0);
+      rs_mask = rs0.lri_mask;
+    }
+    n_rp = cr.n_reset_points;
+    for (uint32_t j = 0; j < n_rp; j++) gput(rp + j, gget(carry_rp(CY) + cc.rp_off + j));
+    n_sa = cr.n_search_attr;
+    for (uint32_t j = 0; j < n_sa; j++) gput(sa + j, gget(carry_sa(CY) + cc.sa_off + j));
+    if (isVH && cr.n_vh > 0) {
+      for (uint32_t j = 0; j + 1 < cr.n_vh; j++) gput(vh + j, gget(carry_vh(CY) + cc.vh_off + j));
+      const cdr_vh_item it = gget(carry_vh(CY) + cc.vh_off + cr.n_vh - 1);
+      n_vh = cr.n_vh;
+      vh_last_id = it.event_id;
+      vh_last_ver = it.version;
+    }
+    hw_chi = live_chi = cr.n_child;
+    for (uint32_t j = 0; j < hw_chi; j++) gput(chi + j, gget(gp(CY->state.child) + cc.child_off + j));
+    hw_can = live_can = cr.n_cancel;
+    for (uint32_t j = 0; j < hw_can; j++) gput(can + j, gget(gp(CY->state.cancel) + cc.cancel_off + j));
+    hw_sig = live_sig = cr.n_signal;
+    for (uint32_t j = 0; j < hw_sig; j++) gput(sig + j, gget(gp(CY->state.signal) + cc.signal_off + j));
+    // user timers: every field lives in the working slot
+    hw_tim = cr.n_timer;
+    for (uint32_t j = 0; j < hw_tim; j++) {
+      const cdr_timer_info t = gget(gp(CY->state.timer) + cc.timer_off + j);
+      T.st(j, TP_SID, t.started_id);
+      T.st(j, TP_TID_TASK, (int64_t)(t.timer_id | ((uint64_t)t.task_id << 32)));
+      T.st(j, TP_EXPIRY, t.expiry_time);
+      T.st(j, TP_VER, t.version);
+    }
+    // activities: the slot carries what the replay reads or changes; AP_ROWS names the
+    // loaded row (AP_CARRIED) for the rest, read again at emission.  The timer
+    // candidates follow loadActivityTimers (timerBuilder.go:249-312) on loaded values.
+    hw_act = cr.n_activity;
+    for (uint32_t j = 0; j < hw_act; j++) {
+      const cdr_activity_info a = gget(gp(CY->state.act) + cc.act_off + j);
+      const bool started = a.started_id != CDR_EMPTY_EVENT_ID;
+      const int64_t s2c = a.scheduled_time + (int64_t)a.s2c * NS_PER_S;
+      // StartedTime / LastHeartBeatUpdatedTime are Go zero times unless the flag is set
+      const bool tset = (a.flags & CDR_AI_STARTED_TIME_SET) != 0;
+      const int64_t st = tset ? a.started_time : 0, hb0 = tset ? a.last_heartbeat_time : 0;
+      const int64_t lhb = hb0 > st ? hb0 : st;
+      bool map = true;  // byActivityID: the largest scheduleID of an activityID holds it (Load's map order)
+      for (uint32_t i = 0; i < hw_act; i++) {
+        const cdr_activity_info b = gget(gp(CY->state.act) + cc.act_off + i);
+        map = map && !(i != j && b.activity_id == a.activity_id && b.schedule_id > a.schedule_id);
+      }
+      A.st(j, AP_SID, a.schedule_id);
+      A.st(j, AP_TS2C, a.expiration_time < s2c ? a.expiration_time : s2c);
+      A.st(j, AP_TALT, started ? st + (int64_t)a.stc * NS_PER_S
+                               : a.scheduled_time + (int64_t)a.s2s * NS_PER_S);
+      A.st(j, AP_THB, started && a.hb > 0 ? lhb + (int64_t)a.hb * NS_PER_S : T_NONE);
+      A.st(j, AP_META, (int64_t)(a.activity_id | (map ? META_FLAG(AF_AIDMAP) : 0ull) |
+                                 (started ? META_FLAG(AF_STARTED) : 0ull) |
+                                 ((a.flags & CDR_AI_CANCEL_REQUESTED) ? META_FLAG(AF_CANCEL) : 0ull) |
+                                 ((uint64_t)(a.timer_task_status & 0xFF) << META_TTS_SHIFT)));
+      A.st(j, AP_VER, a.version);
+      A.st(j, AP_STARTED_ID, a.started_id);
+      A.st(j, AP_STARTED_TIME, st);
+      A.st(j, AP_CANCEL_ID, a.cancel_request_id);
+      A.st(j, AP_ROWS, (int64_t)(AP_CARRIED | j));
+      A.st(j, AP_STC_HB, (int64_t)((uint32_t)a.stc | ((uint64_t)(uint32_t)a.hb << 32)));
+      A.st(j, AP_REQ, (int64_t)a.request_id);
+    }
+  }
 
   // ---- software pipeline: operands of event k+CDR_DEPTH and the type of event
   // k+CDR_DEPTH+2 are issued while event k is processed
@@ -1246,6 +1347,26 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
       const int64_t sid = A.ld(j, AP_SID);
       if (sid == DEAD_KEY) continue;
       const uint64_t rows = (uint64_t)A.ld(j, AP_ROWS);
+      if (rows & AP_CARRIED) {  // a loaded activity: its row, with what the replay changed
+        const GAS cdr_carry* CY = gp(B_.carry);
+        const uint32_t ci = (uint32_t)rows;
+        cdr_activity_info o = gget(gp(CY->state.act) + gget(gp(CY->caps) + csrc).act_off + ci);
+        const uint64_t m = (uint64_t)A.ld(j, AP_META);
+        const int64_t st_id = A.ld(j, AP_STARTED_ID);
+        if (st_id != o.started_id) {  // ActivityTaskStarted replayed onto it (:2083-2098)
+          o.started_time = A.ld(j, AP_STARTED_TIME);
+          o.last_heartbeat_time = o.started_time;
+          o.flags |= CDR_AI_STARTED_TIME_SET;
+        }
+        o.version = A.ld(j, AP_VER);
+        o.started_id = st_id;
+        o.cancel_request_id = A.ld(j, AP_CANCEL_ID);
+        o.request_id = (uint32_t)A.ld(j, AP_REQ);
+        o.timer_task_status = (int32_t)((m >> META_TTS_SHIFT) & 0xFFu);
+        o.flags = (o.flags & ~CDR_AI_CANCEL_REQUESTED) | ((m & META_FLAG(AF_CANCEL)) ? CDR_AI_CANCEL_REQUESTED : 0u);
+        gput(act + n++, o);
+        continue;
+      }
       const uint32_t o_s = el8((uint32_t)rows, len, lane), o_b = el8((uint32_t)(rows >> 32), len, lane);
       const int64_t sched_ts = bld64(S.r, o_s, S.col(CDR_COL_TIMESTAMP));
       const uint32_t arec = (uint32_t)bld64(S.r, o_s, S.col(CDR_COL_AUX));
@@ -1301,7 +1422,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   gput(gp(O_.result) + w, r);
   if (err != CDR_OK) return;
   if (n_vh) gput(vh + (n_vh - 1), cdr_vh_item{vh_last_id, vh_last_ver});
-  if (!(x_flags & CDR_XI_STARTED)) {  // no WorkflowExecutionStarted: its fields keep their zero values
+  if (!(x_flags & CDR_XI_STARTED) && csrc < 0) {  // no WorkflowExecutionStarted: its fields keep their zero values
     X->domain_id = X->workflow_id = X->run_id = X->create_request_id = 0;
     X->parent_domain_id = X->parent_workflow_id = X->parent_run_id = X->task_list = 0;
     X->workflow_type = X->cron_schedule = X->memo = X->nonretriable = X->branch_tree_id = 0;
@@ -1339,7 +1460,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   X->search_attr_len = n_sa;
   if (isRS) {
     RS->current_version = prev_ver;
-    if (!(x_flags & CDR_XI_STARTED)) RS->start_version = D.failover_version;
+    if (!(x_flags & CDR_XI_STARTED) && csrc < 0) RS->start_version = D.failover_version;
     RS->last_write_version = prev_ver;
     RS->last_write_event_id = prev_id;
     for (int c = 0; c < CDR_MAX_CLUSTERS; c++)

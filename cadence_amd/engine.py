@@ -36,6 +36,7 @@ class Batch:
     uuid_seed: int = 1
     empty_uuid: int = 1
     strings: list = field(default_factory=list)  # handle -> string (fixture batches)
+    carry: "Carry | None" = None  # loaded mutable states (cdr_carry), None = fresh builders
 
     @property
     def n_wfs(self):
@@ -55,8 +56,88 @@ class Batch:
         b.cluster = self.cluster
         b.now_ns = self.now_ns
         b.uuid_seed = self.uuid_seed
+        if self.carry is not None:
+            b.carry = C.addressof(self.carry.cstruct())
         self._keep = b
         return b
+
+
+@dataclass
+class Carry:
+    """Loaded mutable states for a batch (cdr_carry): entry w replays onto record
+    src[w] of `state` (the Outputs of an earlier replay), -1 = fresh builder — the
+    mutableStateBuilder.Load + applyEvents path (mutableStateBuilder.go:272-295)."""
+    src: np.ndarray
+    state: "Outputs"
+
+    def cstruct(self) -> abi.CdrCarry:
+        self.src = np.ascontiguousarray(self.src, dtype=np.int32)
+        c = abi.CdrCarry()
+        c.src = self.src.ctypes.data
+        c.caps = C.addressof(self.state.plan.caps)
+        c.n_src = self.state.n_wfs
+        c.totals = self.state.plan.totals
+        c.state = self.state.cstruct()
+        self._keep = c
+        return c
+
+
+def _calls(batch: Batch, w: int) -> list:
+    """Event offsets (within entry w) where each applyEvents call starts."""
+    d = batch.wfs[w]
+    return [k for k in range(d.ev_len) if k == 0 or batch.events[d.ev_off + k].flags & abi.EVF_BATCH_FIRST]
+
+
+def _entry_batch(batch: Batch, wfs, carry=None) -> Batch:
+    return Batch(events=batch.events, wfs=wfs, kvs=batch.kvs, rps=batch.rps, cluster=batch.cluster,
+                 now_ns=batch.now_ns, uuid_seed=batch.uuid_seed, empty_uuid=batch.empty_uuid,
+                 strings=batch.strings, carry=carry)
+
+
+def split_batch(batch: Batch, seed: int = 1):
+    """Cut every top-level entry with two or more calls after a random number of its
+    calls (before its continue-as-new call, if any).  Returns (prefix batch, cut) where
+    cut[w] is the event offset of the cut (0 = entry not split; its prefix is the whole
+    entry).  suffix_batch() builds the rest as a carry-in batch."""
+    rng = np.random.default_rng(seed)
+    wfs = (abi.CdrWfDesc * batch.n_wfs)()
+    C.memmove(wfs, batch.wfs, C.sizeof(wfs))
+    cut = np.zeros(batch.n_wfs, np.int64)
+    for w in range(batch.n_wfs):
+        d = wfs[w]
+        if d.parent >= 0:
+            continue
+        calls = _calls(batch, w)
+        hi = len(calls) - 1
+        if d.newrun >= 0:
+            hi = min(hi, d.newrun_call)
+        if hi < 1:
+            continue
+        c = int(rng.integers(1, hi + 1))
+        cut[w] = calls[c]
+        d.ev_len = calls[c]  # the prefix never reaches a newrun call: its new run is not applied
+    return _entry_batch(batch, wfs), cut
+
+
+def suffix_batch(batch: Batch, cut, prefix: Batch, prefix_out: "Outputs") -> Batch:
+    """The remainder of split_batch's cut as a batch replaying onto the prefix's
+    persisted states; entries whose prefix failed (or were not cut) replay whole on a
+    fresh builder."""
+    wfs = (abi.CdrWfDesc * batch.n_wfs)()
+    C.memmove(wfs, batch.wfs, C.sizeof(wfs))
+    src = np.full(batch.n_wfs, -1, np.int32)
+    for w in range(batch.n_wfs):
+        c = int(cut[w])
+        if c == 0 or prefix_out.result[w].code != abi.OK:
+            continue
+        d = wfs[w]
+        calls_before = len(_calls(prefix, w))
+        d.ev_off += c
+        d.ev_len -= c
+        if d.newrun >= 0:
+            d.newrun_call -= calls_before
+        src[w] = w
+    return _entry_batch(batch, wfs, Carry(src=src, state=prefix_out))
 
 
 def default_cluster() -> abi.CdrClusterMeta:

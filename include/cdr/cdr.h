@@ -200,6 +200,9 @@ typedef struct cdr_dev_batch {
   cdr_cluster_meta cluster;
   int64_t now_ns;
   uint64_t uuid_seed;
+  /* device copy of the batch's cdr_carry (pointers into device memory), or NULL; its
+   * entries replay with the general kernel (cdr_plan_caps clears CDR_CAP_FAST/WAVE) */
+  const cdr_carry* carry;
 } cdr_dev_batch;
 
 /* ------------------------------------------------------------ host planning */

@@ -365,6 +365,9 @@ typedef struct cdr_batch {
   cdr_cluster_meta cluster;
   int64_t now_ns;     /* injected timeSource.Now() */
   uint64_t uuid_seed; /* injected uuid.New() */
+  /* loaded mutable states (nullable): entries it names replay onto a loaded state
+   * instead of a fresh builder (cdr_carry below) */
+  const struct cdr_carry* carry;
 } cdr_batch;
 
 /* =========================================================== OUTPUT =======
@@ -515,6 +518,26 @@ typedef struct cdr_out {
   cdr_reset_point* rp;     /* [totals.rp] */
   cdr_kv* sa;              /* [totals.sa] */
 } cdr_out;
+
+/* Carry-in: replay onto a LOADED mutable state, the analogue of
+ * mutableStateBuilder.Load (mutableStateBuilder.go:272-295) followed by applyEvents —
+ * the NDC replicator's apply-to-current-branch path (nDCHistoryReplicator.go:330-398)
+ * and the 2DC historyReplicator.  The loaded states are the persisted records of an
+ * earlier replay in cdr_out form (per-entry slices at `caps`' offsets, counts in
+ * state.result).  Entry w of the batch loads record src[w] (-1: fresh builder, as
+ * without carry).  A loaded entry must have state.result[src].code == CDR_OK.
+ * Load's non-persisted effects are restated: currentVersion = EmptyVersion,
+ * pendingActivityInfoByActivityID rebuilt from the activity rows (ascending
+ * scheduleID, the last duplicate activityID wins).  The caller keeps the fields the
+ * records omit (schema.h OUTPUT); applyEvents clears stickiness, so a drop-in shim
+ * zeroes Sticky* / Client* after the call. */
+typedef struct cdr_carry {
+  const int32_t* src;      /* [n_wfs of the batch] */
+  const cdr_wf_caps* caps; /* [n_src] row offsets of the loaded states' tables */
+  uint32_t n_src, _pad;    /* entries in `state` */
+  cdr_totals totals;       /* rows in each table of `state` */
+  cdr_out state;           /* read only */
+} cdr_carry;
 
 #ifdef __cplusplus
 }

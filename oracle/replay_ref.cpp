@@ -1054,11 +1054,166 @@ bool write_state(const MutableState& ms, const cdr_batch* b, uint32_t w, const c
   return true;
 }
 
+// mutableStateBuilder.Load (mutableStateBuilder.go:272-295) from the persisted records
+// of an earlier replay (cdr_carry): the inverse of write_state, plus Load's own
+// effects — byActivityID rebuilt from the activity rows (ascending scheduleID, so the
+// last duplicate activityID wins) and currentVersion = EmptyVersion
+void load_state(MutableState& ms, const cdr_carry& cy, uint32_t src) {
+  const cdr_exec_info& x = cy.state.exec[src];
+  const cdr_wf_result& r = cy.state.result[src];
+  const cdr_wf_caps& cp = cy.caps[src];
+  ExecutionInfo& ei = ms.ei;
+  ei.DomainID = x.domain_id;
+  ei.WorkflowID = x.workflow_id;
+  ei.RunID = x.run_id;
+  ei.CreateRequestID = x.create_request_id;
+  ei.ParentDomainID = x.parent_domain_id;
+  ei.ParentWorkflowID = x.parent_workflow_id;
+  ei.ParentRunID = x.parent_run_id;
+  ei.TaskList = x.task_list;
+  ei.WorkflowTypeName = x.workflow_type;
+  ei.DecisionRequestID = x.decision_request_id;
+  ei.CronSchedule = x.cron_schedule;
+  ei.HasMemo = (x.flags & CDR_XI_HAS_MEMO) != 0;
+  ei.Memo = x.memo;
+  ei.NonRetriableErrors = x.nonretriable;
+  ei.InitiatedID = x.initiated_id;
+  ei.CompletionEventBatchID = x.completion_event_batch_id;
+  ei.WorkflowTimeout = x.workflow_timeout;
+  ei.DecisionTimeoutValue = x.decision_timeout_value;
+  ei.State = x.state;
+  ei.CloseStatus = x.close_status;
+  ei.LastFirstEventID = x.last_first_event_id;
+  ei.LastEventTaskID = x.last_event_task_id;
+  ei.NextEventID = x.next_event_id;
+  ei.LastProcessedEvent = x.last_processed_event;
+  ei.SignalCount = x.signal_count;
+  ei.DecisionTimeout = x.decision_timeout;
+  ei.DecisionVersion = x.decision_version;
+  ei.DecisionScheduleID = x.decision_schedule_id;
+  ei.DecisionStartedID = x.decision_started_id;
+  ei.DecisionAttempt = x.decision_attempt;
+  ei.DecisionStartedTimestamp = x.decision_started_ts;
+  ei.DecisionScheduledTimestamp = x.decision_scheduled_ts;
+  ei.DecisionOriginalScheduledTimestamp = x.decision_original_scheduled_ts;
+  ei.Attempt = x.attempt;
+  ei.InitialInterval = x.initial_interval;
+  ei.BackoffCoefficient = x.backoff_coefficient;
+  ei.MaximumInterval = x.maximum_interval;
+  ei.MaximumAttempts = x.maximum_attempts;
+  ei.ExpirationSet = (x.flags & CDR_XI_HAS_EXPIRATION) != 0;
+  ei.ExpirationTime = x.expiration_time;
+  ei.ExpirationSeconds = x.expiration_seconds;
+  ei.CancelRequested = (x.flags & CDR_XI_CANCEL_REQUESTED) != 0;
+  ei.HasRetryPolicy = (x.flags & CDR_XI_HAS_RETRY) != 0;
+  ei.HasSearchAttr = (x.flags & CDR_XI_HAS_SEARCH_ATTR) != 0;
+  ei.HasResetPoints = (x.flags & CDR_XI_HAS_RESET_POINTS) != 0;
+  ei.Started = (x.flags & CDR_XI_STARTED) != 0;
+  ei.HasBranchToken = (x.flags & CDR_XI_HAS_BRANCH) != 0;
+  if (ei.HasBranchToken) {
+    ei.BranchTree = x.branch_tree_id;
+    ei.BranchLo = x.branch_id_lo;
+    ei.BranchHi = x.branch_id_hi;
+  }
+  ei.ResetPoints.assign(cy.state.rp + cp.rp_off, cy.state.rp + cp.rp_off + r.n_reset_points);
+  ei.SearchAttributes.assign(cy.state.sa + cp.sa_off, cy.state.sa + cp.sa_off + r.n_search_attr);
+  if (ms.hasRS) {
+    const cdr_repl_state& rs = cy.state.repl[src];
+    ms.rs.CurrentVersion = rs.current_version;
+    ms.rs.StartVersion = rs.start_version;
+    ms.rs.LastWriteVersion = rs.last_write_version;
+    ms.rs.LastWriteEventID = rs.last_write_event_id;
+    ms.rs.LastReplicationInfo.clear();
+    for (int c = 0; c < CDR_MAX_CLUSTERS; c++)
+      if (rs.lri_mask & (1u << c)) ms.rs.LastReplicationInfo[c] = {rs.lri_version[c], rs.lri_last_event_id[c]};
+  }
+  if (ms.hasVH) {
+    ms.vh.items.clear();
+    for (uint32_t k = 0; k < r.n_vh; k++) {
+      const cdr_vh_item& it = cy.state.vh[cp.vh_off + k];
+      ms.vh.items.push_back({it.event_id, it.version});
+    }
+    ms.vh.has_token = (x.flags & CDR_XI_VH_BRANCH) != 0;
+    if (ms.vh.has_token) {
+      ms.vh.tree = x.branch_tree_id;
+      ms.vh.br_lo = x.branch_id_lo;
+      ms.vh.br_hi = x.branch_id_hi;
+    }
+  }
+  ms.currentVersion = CDR_EMPTY_VERSION;  // :291
+  for (uint32_t k = 0; k < r.n_activity; k++) {
+    const cdr_activity_info& o = cy.state.act[cp.act_off + k];
+    ActivityInfo a{};
+    a.Version = o.version;
+    a.ScheduleID = o.schedule_id;
+    a.ScheduledEventBatchID = o.scheduled_event_batch_id;
+    a.ScheduledTime = o.scheduled_time;
+    a.StartedID = o.started_id;
+    a.StartedTimeSet = (o.flags & CDR_AI_STARTED_TIME_SET) != 0;
+    a.StartedTime = o.started_time;
+    a.LastHeartBeatSet = (o.flags & CDR_AI_STARTED_TIME_SET) != 0;
+    a.LastHeartBeatUpdatedTime = o.last_heartbeat_time;
+    a.ExpirationSet = true;
+    a.ExpirationTime = o.expiration_time;
+    a.CancelRequestID = o.cancel_request_id;
+    a.CancelRequested = (o.flags & CDR_AI_CANCEL_REQUESTED) != 0;
+    a.ActivityID = o.activity_id;
+    a.RequestID = o.request_id;
+    a.TaskList = o.task_list;
+    a.NonRetriableErrors = o.nonretriable;
+    a.ScheduleToStartTimeout = o.s2s;
+    a.ScheduleToCloseTimeout = o.s2c;
+    a.StartToCloseTimeout = o.stc;
+    a.HeartbeatTimeout = o.hb;
+    a.TimerTaskStatus = o.timer_task_status;
+    a.Attempt = o.attempt;
+    a.HasRetryPolicy = (o.flags & CDR_AI_HAS_RETRY) != 0;
+    a.InitialInterval = o.initial_interval;
+    a.MaximumInterval = o.maximum_interval;
+    a.MaximumAttempts = o.maximum_attempts;
+    a.BackoffCoefficient = o.backoff_coefficient;
+    ms.pendingActivityInfoIDs[a.ScheduleID] = a;
+  }
+  for (auto& kv : ms.pendingActivityInfoIDs) ms.pendingActivityInfoByActivityID[kv.second.ActivityID] = kv.first;
+  for (uint32_t k = 0; k < r.n_timer; k++) {
+    const cdr_timer_info& o = cy.state.timer[cp.timer_off + k];
+    ms.pendingTimerInfoIDs[o.timer_id] = TimerInfo{o.version, o.timer_id, o.started_id, o.expiry_time, o.task_id};
+  }
+  for (uint32_t k = 0; k < r.n_child; k++) {
+    const cdr_child_info& o = cy.state.child[cp.child_off + k];
+    ChildInfo c{};
+    c.Version = o.version;
+    c.InitiatedID = o.initiated_id;
+    c.InitiatedEventBatchID = o.initiated_event_batch_id;
+    c.StartedID = o.started_id;
+    c.StartedWorkflowID = o.started_workflow_id;
+    c.StartedRunID = o.started_run_id;
+    c.CreateReqLo = o.create_request_lo;
+    c.CreateReqHi = o.create_request_hi;
+    c.DomainName = o.domain_name;
+    c.WorkflowTypeName = o.workflow_type;
+    c.ParentClosePolicy = o.parent_close_policy;
+    ms.pendingChildExecutionInfoIDs[c.InitiatedID] = c;
+  }
+  for (uint32_t k = 0; k < r.n_cancel; k++) {
+    const cdr_cancel_info& o = cy.state.cancel[cp.cancel_off + k];
+    ms.pendingRequestCancelInfoIDs[o.initiated_id] =
+        CancelInfo{o.version, o.initiated_event_batch_id, o.initiated_id, o.cancel_request_lo, o.cancel_request_hi};
+  }
+  for (uint32_t k = 0; k < r.n_signal; k++) {
+    const cdr_signal_info& o = cy.state.signal[cp.signal_off + k];
+    ms.pendingSignalInfoIDs[o.initiated_id] =
+        SignalInfo{o.version,         o.initiated_event_batch_id, o.initiated_id, o.signal_request_lo,
+                   o.signal_request_hi, o.signal_name,             o.input,        o.control};
+  }
+}
+
 void replay_one(const cdr_batch* b, const Ctx* ctx, uint32_t w, const cdr_wf_caps* caps, cdr_out* out) {
   const cdr_wf_desc& d = b->wfs[w];
   cdr_wf_result& r = out->result[w];
   r = cdr_wf_result{};
   MutableState ms(ctx, (int)d.builder, d.failover_version, d.wf_key, d.retention_days);
+  if (b->carry && b->carry->src && b->carry->src[w] >= 0) load_state(ms, *b->carry, (uint32_t)b->carry->src[w]);
   StateBuilder sb{ctx, b, &ms};
   const cdr_event* ev = b->events + d.ev_off;
   const cdr_event* nr = nullptr;
