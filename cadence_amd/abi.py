@@ -101,7 +101,8 @@ AttrTimer = _S("cdr_attr_timer", [("timer_id", u32), ("_pad", u32), ("start_to_f
                                   ("started_event_id", i64)])
 AttrExternal = _S("cdr_attr_external", [
     ("domain", u32), ("workflow_id", u32), ("run_id", u32), ("workflow_type", u32), ("signal_name", u32),
-    ("input", u32), ("control", u32), ("flags", u32), ("parent_close_policy", i32), ("_pad", i32)])
+    ("input", u32), ("control", u32), ("flags", u32), ("parent_close_policy", i32),
+    ("target_domain_id", u32)])
 AttrRef = _S("cdr_attr_initiated_ref", [("initiated_event_id", i64), ("run_id", u32), ("_pad", u32)])
 AttrCAN = _S("cdr_attr_can", [("new_execution_run_id", u32), ("_pad", u32)])
 AttrUpsert = _S("cdr_attr_upsert", [("search_attr_off", u32), ("search_attr_len", u32)])
@@ -174,10 +175,20 @@ CdrWfCaps = _S("cdr_wf_caps", [
     ("act_off", u64), ("timer_off", u64), ("child_off", u64), ("cancel_off", u64), ("signal_off", u64),
     ("vh_off", u64), ("rp_off", u64), ("sa_off", u64), ("act_cap", u32), ("timer_cap", u32), ("child_cap", u32),
     ("cancel_cap", u32), ("signal_cap", u32), ("vh_cap", u32), ("rp_cap", u32), ("sa_cap", u32),
-    ("act_live", u32), ("timer_live", u32), ("flags", u32), ("_pad", u32)])
-CdrTotals = _S("cdr_totals", [(n, u64) for n in ("act", "timer", "child", "cancel", "signal", "vh", "rp", "sa")])
+    ("act_live", u32), ("timer_live", u32), ("flags", u32), ("_pad", u32), ("xfer_off", u64), ("ttask_off", u64),
+    ("xfer_cap", u32), ("ttask_cap", u32)])
+CdrTotals = _S("cdr_totals", [(n, u64) for n in ("act", "timer", "child", "cancel", "signal", "vh", "rp", "sa",
+                                                 "xfer", "ttask")])
 CdrOut = _S("cdr_out", [(n, C.c_void_p) for n in (
-    "result", "exec", "repl", "vh", "act", "timer", "child", "cancel", "signal", "rp", "sa")])
+    "result", "exec", "repl", "vh", "act", "timer", "child", "cancel", "signal", "rp", "sa", "transfer",
+    "timer_tasks", "n_tasks")])
+CdrTask = _S("cdr_task", [("type", u32), ("timeout_type", i32), ("event_id", i64), ("visibility_ts", i64),
+                          ("attempt", i64), ("domain_id", u32), ("task_list", u32), ("target_workflow_id", u32),
+                          ("target_run_id", u32), ("flags", u32), ("_pad", u32)])
+TASK_TYPES = {0: "DecisionTask", 1: "ActivityTask", 2: "CloseExecution", 3: "CancelExecution",
+              4: "StartChildExecution", 5: "SignalExecution", 6: "RecordWorkflowStarted",
+              8: "UpsertWorkflowSearchAttributes", 16: "DecisionTimeout", 17: "ActivityTimeout", 18: "UserTimer",
+              19: "WorkflowTimeout", 20: "DeleteHistoryEvent", 22: "WorkflowBackoffTimer"}
 CdrCarry = _S("cdr_carry", [("src", C.c_void_p), ("caps", C.c_void_p), ("n_src", u32), ("_pad", u32),
                             ("totals", CdrTotals), ("state", CdrOut)])
 CdrSlices = _S("cdr_slices", [
@@ -238,6 +249,7 @@ MIRRORS = {
     "cdr_child_info": CdrChildInfo, "cdr_cancel_info": CdrCancelInfo, "cdr_signal_info": CdrSignalInfo,
     "cdr_wf_result": CdrWfResult, "cdr_wf_caps": CdrWfCaps, "cdr_totals": CdrTotals, "cdr_out": CdrOut,
     "cdr_slices": CdrSlices, "cdr_dev_batch": CdrDevBatch, "cdr_carry": CdrCarry,
+    "cdr_task": CdrTask,
 }
 
 # C ABI entry points declared in include/cdr/cdr.h and include/cdr/synth.h

@@ -178,7 +178,8 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   // ---- plan + pack on the host
   uint32_t ns = 0, n_wave = 0;
   uint64_t rows = 0;
-  const uint32_t mode = cdr_get_plan_mode(ctx);
+  const bool tasks = out->transfer != nullptr;  // emitted by the general kernel only: no wave slices
+  const uint32_t mode = tasks ? 0u : cdr_get_plan_mode(ctx);
   int rc = cdr_plan_slices_ex(b->wfs, caps, b->n_wfs, mode, nullptr, nullptr, nullptr, nullptr, &ns, &rows, &n_wave);
   if (rc) return rc;
   std::vector<int32_t> lane(ns * (size_t)CDR_SLICE_WIDTH);
@@ -291,6 +292,11 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   dout.signal = (cdr_signal_info*)dz(tot->signal * sizeof(cdr_signal_info));
   dout.rp = (cdr_reset_point*)dz(tot->rp * sizeof(cdr_reset_point));
   dout.sa = (cdr_kv*)dz(tot->sa * sizeof(cdr_kv));
+  if (tasks) {
+    dout.transfer = (cdr_task*)dz(tot->xfer * sizeof(cdr_task));
+    dout.timer_tasks = (cdr_task*)dz(tot->ttask * sizeof(cdr_task));
+    dout.n_tasks = (uint32_t*)dz((uint64_t)b->n_wfs * 2 * sizeof(uint32_t));
+  }
   for (void* p : allocs)
     if (!p) {
       free_all();
@@ -313,6 +319,11 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   down(out->signal, dout.signal, tot->signal * sizeof(cdr_signal_info));
   down(out->rp, dout.rp, tot->rp * sizeof(cdr_reset_point));
   down(out->sa, dout.sa, tot->sa * sizeof(cdr_kv));
+  if (tasks) {
+    down(out->transfer, dout.transfer, tot->xfer * sizeof(cdr_task));
+    down(out->timer_tasks, dout.timer_tasks, tot->ttask * sizeof(cdr_task));
+    down(out->n_tasks, dout.n_tasks, (uint64_t)b->n_wfs * 2 * sizeof(uint32_t));
+  }
   free_all();
   return rc;
 }

@@ -25,6 +25,10 @@ inline uint32_t arena_words_for(uint32_t type) {
       return (sizeof(cdr_attr_wf_started) + 7) / 8;
     case CDR_EV_AT_SCHEDULED:
       return (sizeof(cdr_attr_at_scheduled) + 7) / 8;
+    case CDR_EV_CHILD_INITIATED:  // read only by task emission (target execution)
+    case CDR_EV_RCE_INITIATED:
+    case CDR_EV_SE_INITIATED:
+      return (sizeof(cdr_attr_external) + 7) / 8;
     default:
       return 0;
   }
@@ -162,6 +166,55 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   *out = c;
 }
 
+// upper bounds of the transfer / timer tasks an entry's events append
+// (stateBuilder.go:157-595: at most one of each kind per event, two timer tasks for
+// WorkflowExecutionStarted — backoff + timeout)
+void task_caps(const cdr_event* ev, uint64_t n, uint32_t* xfer, uint32_t* ttask) {
+  uint32_t x = 0, t = 0;
+  for (uint64_t k = 0; k < n; k++) {
+    switch (ev[k].type) {
+      case CDR_EV_WF_STARTED:
+        x += 1;
+        t += 2;
+        break;
+      case CDR_EV_DT_SCHEDULED:
+      case CDR_EV_DT_TIMED_OUT:
+      case CDR_EV_DT_FAILED:
+      case CDR_EV_CHILD_INITIATED:
+      case CDR_EV_RCE_INITIATED:
+      case CDR_EV_SE_INITIATED:
+      case CDR_EV_UPSERT_SA:
+        x += 1;
+        break;
+      case CDR_EV_AT_SCHEDULED:
+      case CDR_EV_WF_COMPLETED:
+      case CDR_EV_WF_FAILED:
+      case CDR_EV_WF_TIMED_OUT:
+      case CDR_EV_WF_CANCELED:
+      case CDR_EV_WF_TERMINATED:
+      case CDR_EV_WF_CONTINUED_AS_NEW:
+        x += 1;
+        t += 1;
+        break;
+      case CDR_EV_DT_STARTED:
+      case CDR_EV_AT_STARTED:
+      case CDR_EV_AT_COMPLETED:
+      case CDR_EV_AT_FAILED:
+      case CDR_EV_AT_TIMED_OUT:
+      case CDR_EV_AT_CANCELED:
+      case CDR_EV_TIMER_STARTED:
+      case CDR_EV_TIMER_FIRED:
+      case CDR_EV_TIMER_CANCELED:
+        t += 1;
+        break;
+      default:
+        break;
+    }
+  }
+  *xfer = x;
+  *ttask = t;
+}
+
 // one event (or padding when e == nullptr) into element i of the slab row `row`;
 // attribute records go to the arena at *apos
 void put_event(uint8_t* row, uint32_t i, const cdr_event* ep, bool first, uint64_t* apos_p, uint64_t* arena) {
@@ -250,18 +303,24 @@ void put_event(uint8_t* row, uint32_t i, const cdr_event* ep, bool first, uint64
         kk = e.a.timer.timer_id;
         break;
       case CDR_EV_CHILD_INITIATED:
-        kk = e.a.ext.domain;
+        kk = e.a.ext.domain | ((uint64_t)(apos & 0xFFFFFFFFull) << 32);
+        std::memcpy(arena + apos, &e.a.ext, sizeof(cdr_attr_external));
+        apos += arena_words_for(e.type);
         ax = e.a.ext.workflow_type;
         h = e.a.ext.workflow_id;
         n = e.a.ext.parent_close_policy;
         if (e.a.ext.flags & CDR_XF_DOMAIN_MISSING) flags |= CDR_SEF_DOMAIN_MISSING;
         break;
       case CDR_EV_RCE_INITIATED:
-        kk = e.a.ext.domain;
+        kk = e.a.ext.domain | ((uint64_t)(apos & 0xFFFFFFFFull) << 32);
+        std::memcpy(arena + apos, &e.a.ext, sizeof(cdr_attr_external));
+        apos += arena_words_for(e.type);
         if (e.a.ext.flags & CDR_XF_DOMAIN_MISSING) flags |= CDR_SEF_DOMAIN_MISSING;
         break;
       case CDR_EV_SE_INITIATED:
-        kk = e.a.ext.domain;
+        kk = e.a.ext.domain | ((uint64_t)(apos & 0xFFFFFFFFull) << 32);
+        std::memcpy(arena + apos, &e.a.ext, sizeof(cdr_attr_external));
+        apos += arena_words_for(e.type);
         ax = (int64_t)(((uint64_t)e.a.ext.input << 32) | e.a.ext.control);
         h = e.a.ext.signal_name;
         if (e.a.ext.flags & CDR_XF_DOMAIN_MISSING) flags |= CDR_SEF_DOMAIN_MISSING;
@@ -372,6 +431,11 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
       c.timer_live += r.n_timer;
       c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE);
     }
+    cdr_internal::task_caps(b->events + d.ev_off, d.ev_len, &c.xfer_cap, &c.ttask_cap);
+    c.xfer_off = t.xfer;
+    t.xfer += c.xfer_cap;
+    c.ttask_off = t.ttask;
+    t.ttask += c.ttask_cap;
     c.act_off = t.act;
     t.act += c.act_cap;
     c.timer_off = t.timer;
@@ -683,6 +747,7 @@ uint64_t cdr_struct_size(const char* name) {
       {"cdr_slices", sizeof(cdr_slices)},
       {"cdr_dev_batch", sizeof(cdr_dev_batch)},
       {"cdr_carry", sizeof(cdr_carry)},
+      {"cdr_task", sizeof(cdr_task)},
   };
   for (const E& e : table)
     if (std::strcmp(e.n, name) == 0) return e.s;

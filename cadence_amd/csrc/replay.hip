@@ -383,8 +383,14 @@ __device__ __forceinline__ void tim_pick(const T& S, uint32_t hw) {
 // slice's uniform slot count `cap` (slots past the lane's high-water mark `hw` are
 // ignored), state is carried in selects, and only the final status-bit store is
 // lane-masked.  `on` = the lane's event asked for a pick.
+// what a pick created (the timer task createNewTask returns, timerBuilder.go:391-408)
+struct Pick {
+  bool made;
+  int32_t timeout_type, slot;
+  int64_t vis, event_id;
+};
 template <class A>
-__device__ __forceinline__ void act_pick_p(const A& S, uint32_t hw, uint32_t cap, bool on) {
+__device__ __forceinline__ Pick act_pick_p(const A& S, uint32_t hw, uint32_t cap, bool on) {
   int best = -1;
   int64_t bt = 0, bs = 0;
   int bo = 0;
@@ -413,10 +419,13 @@ __device__ __forceinline__ void act_pick_p(const A& S, uint32_t hw, uint32_t cap
     bm = better ? meta : bm;
   }
   const uint64_t b = (uint64_t)bbit << META_TTS_SHIFT;
-  if (best >= 0 && !(bm & b)) S.st((uint32_t)best, AP_META, (int64_t)(bm | b));
+  const bool made = best >= 0 && !(bm & b);
+  if (made) S.st((uint32_t)best, AP_META, (int64_t)(bm | b));
+  // TimerTaskStatus bit -> shared.TimeoutType (StartToClose 0 ... Heartbeat 3)
+  return Pick{made, (int32_t)__builtin_ctz(bbit | 16u), best, bt, bs};
 }
 template <class T>
-__device__ __forceinline__ void tim_pick_p(const T& S, uint32_t hw, uint32_t cap, bool on) {
+__device__ __forceinline__ Pick tim_pick_p(const T& S, uint32_t hw, uint32_t cap, bool on) {
   int best = -1;
   int64_t be = 0, bs = 0;
   uint64_t bv = 0;
@@ -430,8 +439,10 @@ __device__ __forceinline__ void tim_pick_p(const T& S, uint32_t hw, uint32_t cap
     bs = better ? sid : bs;
     bv = better ? v : bv;
   }
-  if (best >= 0 && (bv >> 32) != CDR_TIMER_TASK_STATUS_CREATED)
+  const bool made = best >= 0 && (bv >> 32) != CDR_TIMER_TASK_STATUS_CREATED;
+  if (made)
     S.st((uint32_t)best, TP_TID_TASK, (int64_t)((bv & 0xFFFFFFFFull) | ((uint64_t)CDR_TIMER_TASK_STATUS_CREATED << 32)));
+  return Pick{made, 0, best, be, bs};
 }
 
 }  // namespace
@@ -470,7 +481,7 @@ __device__ __forceinline__ const GAS cdr_reset_point* carry_rp(const GAS cdr_car
 __device__ __forceinline__ const GAS cdr_kv* carry_sa(const GAS cdr_carry* c) { return gp(c->state.sa); }
 __device__ __forceinline__ const GAS cdr_vh_item* carry_vh(const GAS cdr_carry* c) { return gp(c->state.vh); }
 
-template <bool LDS>
+template <bool LDS, bool TASKS>
 __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu(CDR_WPE, 8))) void k_replay(
     cdr_launch L) {
   (void)L;  // read through KA()
@@ -664,6 +675,68 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
       A.st(j, AP_REQ, (int64_t)a.request_id);
     }
   }
+
+  // ---- transfer / timer tasks (stateBuilder.go:613-804), when the caller asks for
+  // them (cdr_out.transfer != NULL): appended in generation order to the entry's slices
+  constexpr bool TK = TASKS;  // instantiated without task code for the common case
+  uint32_t n_xt = 0, n_tt = 0, xt_cap = 0, tt_cap = 0;
+  if (TK) {
+    xt_cap = CP.xfer_cap;
+    tt_cap = CP.ttask_cap;
+  }
+  auto task_x = [&](bool c, uint32_t type, int64_t eid, uint32_t dom, uint32_t tl, uint32_t twf, uint32_t trun,
+                    uint32_t fl) {
+    c = c && n_xt < xt_cap;
+    if (c) {
+      cdr_task t;
+      t.type = type;
+      t.timeout_type = 0;
+      t.event_id = eid;
+      t.visibility_ts = 0;
+      t.attempt = 0;
+      t.domain_id = dom;
+      t.task_list = tl;
+      t.target_workflow_id = twf;
+      t.target_run_id = trun;
+      t.flags = fl;
+      t._pad = 0;
+      gput(gp(O_.transfer) + CP.xfer_off + n_xt, t);
+    }
+    n_xt += c ? 1u : 0u;
+  };
+  auto task_t = [&](bool c, uint32_t type, int32_t tt, int64_t eid, int64_t vis, int64_t att) {
+    c = c && n_tt < tt_cap;
+    if (c) {
+      cdr_task t;
+      t.type = type;
+      t.timeout_type = tt;
+      t.event_id = eid;
+      t.visibility_ts = vis;
+      t.attempt = att;
+      t.domain_id = t.task_list = t.target_workflow_id = t.target_run_id = t.flags = t._pad = 0;
+      gput(gp(O_.timer_tasks) + CP.ttask_off + n_tt, t);
+    }
+    n_tt += c ? 1u : 0u;
+  };
+  // ExecutionInfo.TaskList as of now (getTaskList, stateBuilder.go:789-794)
+  auto task_list_now = [&]() -> uint32_t { return ((x_flags & CDR_XI_STARTED) || csrc >= 0) ? X->task_list : 0u; };
+  // ActivityTimeoutTask: the activity timer pick's task (Attempt: 0 unless loaded)
+  auto act_task = [&](const Pick& p) {
+    if (!(TK && p.made)) return;
+    int64_t att = 0;
+    const uint64_t rows = (uint64_t)A.ld((uint32_t)p.slot, AP_ROWS);
+    if (rows & AP_CARRIED) {
+      const GAS cdr_carry* CY = gp(B_.carry);
+      att = gget(gp(CY->state.act) + gget(gp(CY->caps) + csrc).act_off + (uint32_t)rows).attempt;
+    }
+    task_t(true, CDR_TT_ACTIVITY_TIMEOUT, p.timeout_type, p.event_id, p.vis, att);
+  };
+  auto tim_task = [&](const Pick& p) { task_t(TK && p.made, CDR_TT_USER_TIMER, 0, p.event_id, p.vis, 0); };
+  // appendTasksForFinishedExecutions (:775-787)
+  auto close_tasks = [&](bool c, int64_t ts) {
+    task_x(TK && c, CDR_TT_CLOSE_EXECUTION, 0, 0, 0, 0, 0, 0);
+    task_t(TK && c, CDR_TT_DELETE_HISTORY, 0, 0, ts + (int64_t)D.retention_days * 86400ll * NS_PER_S, 0);
+  };
 
   // ---- software pipeline: operands of event k+CDR_DEPTH and the type of event
   // k+CDR_DEPTH+2 are issued while event k is processed
@@ -873,6 +946,12 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           n_rp = SEL(ok, nrp, n_rp);
           n_sa = SEL(ok, nsa, n_sa);
           x_flags = SEL(ok, xf, x_flags);
+          if (TK && ok) {  // scheduleWorkflowTimerTask (:706-735) + RecordWorkflowStartedTask (:614-616)
+            const int64_t backoff = (int64_t)a->first_decision_backoff_s * NS_PER_S;
+            task_t(backoff != 0, CDR_TT_WORKFLOW_BACKOFF, (af & CDR_SF_CRON_INITIATOR) ? 1 : 0, 0, e.ts + backoff, 0);
+            task_t(true, CDR_TT_WORKFLOW_TIMEOUT, 0, 0, e.ts + (int64_t)a->exec_timeout_s * NS_PER_S + backoff, 0);
+            task_x(true, CDR_TT_RECORD_STARTED, 0, 0, 0, 0, 0, 0);
+          }
           cks_ok = SEL(ok, 0u, cks_ok);
           x_dt_timeout_value = SEL(ok, a->task_timeout_s, x_dt_timeout_value);
           x_state = SEL(ok, (int32_t)CDR_STATE_CREATED, x_state);
@@ -895,6 +974,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           dsc_ts = SEL(mine, e.ts, dsc_ts);
           dst_ts = SEL(mine, (int64_t)0, dst_ts);
           dorig_ts = SEL(mine, e.ts, dorig_ts);
+          task_x(TK && mine, CDR_TT_DECISION, e.id, D.domain_id, task_list_now(), 0, 0, 0);  // :196-197
           break;
         case CDR_EV_DT_STARTED: {  // :202-213 -> :200-253
           const bool f = mine && e.key != dsched;
@@ -906,6 +986,8 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           dreq = SEL(ok, e.h, dreq);
           datt = SEL(ok, (int64_t)0, datt);
           dst_ts = SEL(ok, e.ts, dst_ts);
+          // scheduleDecisionTimerTask (:210-211; timerBuilder.go:322-331)
+          task_t(TK && ok, CDR_TT_DECISION_TIMEOUT, CDR_TIMEOUT_START_TO_CLOSE, e.key, e.ts + (int64_t)dto * NS_PER_S, 0);
           break;
         }
         case CDR_EV_DT_COMPLETED: {  // :215-219 -> :255-262,659-674,789-800
@@ -964,6 +1046,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           dorig_ts = SEL(mine, (int64_t)0, dorig_ts);
           dsc_ts = SEL(mine, (tr || inc) ? now : (int64_t)0, dsc_ts);
           datt = SEL(mine, na, datt);
+          task_x(TK && mine && tr, CDR_TT_DECISION, x_next_event, D.domain_id, task_list_now(), 0, 0, 0);  // :235,253
           break;
         }
         case CDR_EV_AT_SCHEDULED: {  // :259-269 -> mutableStateBuilder.go:1982-2028
@@ -1000,7 +1083,8 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
             A.st(j, AP_STC_HB, (int64_t)(((uint64_t)e.key >> 32) | ((uint64_t)e.aux & 0xFFFFFFFF00000000ull)));
             A.st(j, AP_REQ, 0);
           }
-          act_pick_p(A, hw_act, act_cap, ok);
+          task_x(TK && ok, CDR_TT_ACTIVITY, e.id, D.domain_id, task_list_now(), 0, 0, 0);  // :265-266
+          act_task(act_pick_p(A, hw_act, act_cap, ok));
           break;
         }
         case CDR_EV_AT_STARTED: {  // :271-278 -> :2083-2098
@@ -1021,7 +1105,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
             A.st(j, AP_TALT, e.ts + (int64_t)stc * NS_PER_S);
             A.st(j, AP_THB, hb > 0 ? e.ts + (int64_t)hb * NS_PER_S : T_NONE);
           }
-          act_pick_p(A, hw_act, act_cap, ok);
+          act_task(act_pick_p(A, hw_act, act_cap, ok));
           break;
         }
         case CDR_EV_AT_COMPLETED:  // :280-305,312-319 -> DeleteActivity :1247-1269
@@ -1053,7 +1137,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           const bool f2 = ok && !found;
           PFAIL(f2, CDR_E_ACTIVITY_ID_NOT_FOUND);
           ok = ok && !f2;
-          act_pick_p(A, hw_act, act_cap, ok);
+          act_task(act_pick_p(A, hw_act, act_cap, ok));
           break;
         }
         case CDR_EV_AT_CANCEL_REQUESTED: {  // :307-310 -> :2264-2285
@@ -1099,7 +1183,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
             T.st(j, TP_EXPIRY, e.ts + e.aux * NS_PER_S);
             T.st(j, TP_VER, e.ver);
           }
-          tim_pick_p(T, hw_tim, tim_cap, ok);
+          tim_task(tim_pick_p(T, hw_tim, tim_cap, ok));
           break;
         }
         case CDR_EV_TIMER_FIRED:       // :334-341
@@ -1109,7 +1193,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
             const bool hit = mine && j < hw_tim && T.ld(j, TP_SID) != DEAD_KEY && (uint32_t)T.ld(j, TP_TID_TASK) == tid;
             if (hit) T.st(j, TP_SID, DEAD_KEY);
           }
-          tim_pick_p(T, hw_tim, tim_cap, mine);
+          tim_task(tim_pick_p(T, hw_tim, tim_cap, mine));
           break;
         }
         case CDR_EV_CHILD_INITIATED: {  // :355-371 -> :3256-3280
@@ -1138,6 +1222,10 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           }
           live_chi += ok ? 1u : 0u;
           PFAIL(ok && (e.tf & CDR_SEF_DOMAIN_MISSING), CDR_E_DOMAIN_NOT_FOUND);
+          if (TK && ok && !(e.tf & CDR_SEF_DOMAIN_MISSING)) {  // scheduleStartChildWorkflowTransferTask (:370-371)
+            const cdr_attr_external xa = gget(gp((const cdr_attr_external*)(B_.ev.arena + ((uint64_t)e.key >> 32))));
+            task_x(true, CDR_TT_START_CHILD, e.id, xa.target_domain_id, 0, xa.workflow_id, 0, 0);
+          }
           break;
         }
         case CDR_EV_CHILD_STARTED: {  // :378-381 -> :3312-3325
@@ -1182,6 +1270,11 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           }
           live_can += ok ? 1u : 0u;
           PFAIL(ok && (e.tf & CDR_SEF_DOMAIN_MISSING), CDR_E_DOMAIN_NOT_FOUND);
+          if (TK && ok && !(e.tf & CDR_SEF_DOMAIN_MISSING)) {  // scheduleCancelExternalWorkflowTransferTask (:421-427)
+            const cdr_attr_external xa = gget(gp((const cdr_attr_external*)(B_.ev.arena + ((uint64_t)e.key >> 32))));
+            task_x(true, CDR_TT_CANCEL_EXECUTION, e.id, xa.target_domain_id, 0, xa.workflow_id, xa.run_id,
+                   (xa.flags & CDR_XF_CHILD_ONLY) ? CDR_TF_CHILD_ONLY : 0u);
+          }
           break;
         }
         case CDR_EV_RCE_FAILED:
@@ -1215,6 +1308,11 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           }
           live_sig += ok ? 1u : 0u;
           PFAIL(ok && (e.tf & CDR_SEF_DOMAIN_MISSING), CDR_E_DOMAIN_NOT_FOUND);
+          if (TK && ok && !(e.tf & CDR_SEF_DOMAIN_MISSING)) {  // scheduleSignalWorkflowTransferTask (:452-458)
+            const cdr_attr_external xa = gget(gp((const cdr_attr_external*)(B_.ev.arena + ((uint64_t)e.key >> 32))));
+            task_x(true, CDR_TT_SIGNAL_EXECUTION, e.id, xa.target_domain_id, 0, xa.workflow_id, xa.run_id,
+                   (xa.flags & CDR_XF_CHILD_ONLY) ? CDR_TF_CHILD_ONLY : 0u);
+          }
           break;
         }
         case CDR_EV_SE_FAILED:
@@ -1251,6 +1349,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           x_state = SEL(ok, (int32_t)CDR_STATE_COMPLETED, x_state);
           x_close = SEL(ok, (int32_t)cs, x_close);
           x_completion_batch = SEL(ok, call_first_id, x_completion_batch);
+          close_tasks(ok, e.ts);
           break;
         }
         case CDR_EV_UPSERT_SA: {  // :533-535 -> :2746-2768
@@ -1271,6 +1370,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           }
           n_sa = SEL(mine, nsa, n_sa);
           x_flags |= mine ? CDR_XI_HAS_SEARCH_ATTR : 0u;
+          task_x(TK && mine, CDR_TT_UPSERT_SA, 0, 0, 0, 0, 0, 0);  // :535
           break;
         }
         case CDR_EV_WF_CONTINUED_AS_NEW: {  // :537-595
@@ -1289,6 +1389,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           x_state = SEL(ok, (int32_t)CDR_STATE_COMPLETED, x_state);
           x_close = SEL(ok, (int32_t)CDR_CLOSE_CONTINUED_AS_NEW, x_close);
           x_completion_batch = SEL(ok, call_first_id, x_completion_batch);
+          close_tasks(ok, e.ts);  // :592
           break;
         }
         default:
@@ -1328,7 +1429,11 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   r.fail_index = err_k;
   // table high-water marks; k_tables compacts them to live counts (a failed
   // workflow reports no state)
-  if (err != CDR_OK) hw_act = hw_tim = hw_chi = hw_can = hw_sig = n_vh = n_rp = n_sa = 0;
+  if (err != CDR_OK) hw_act = hw_tim = hw_chi = hw_can = hw_sig = n_vh = n_rp = n_sa = n_xt = n_tt = 0;
+  if (TK) {
+    gp(O_.n_tasks)[2 * (uint64_t)w] = n_xt;
+    gp(O_.n_tasks)[2 * (uint64_t)w + 1] = n_tt;
+  }
   r.n_activity = 0;  // set by the emission below
   r.n_timer = 0;
   r.n_child = hw_chi;
@@ -1614,7 +1719,11 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const size_t lds = (size_t)(la * CDR_ACT_PLANES + lt * CDR_TIM_PLANES) * CDR_SLICE_WIDTH * sizeof(uint64_t);
   const bool spill = in->max_act_slots > la || in->max_tim_slots > lt;
   const uint32_t blocks = in->ev.n_slices;
-  const bool fast = c->fast && in->n_fast_slices > 0;
+  // task emission lives in the general kernel only: every slice goes there (a plan
+  // without wave slices is required, cdr_plan_slices_ex mode 0)
+  const bool tasks = out->transfer != nullptr;
+  if (tasks && (in->n_wave_slices > 0 || !out->timer_tasks || !out->n_tasks)) return CDR_API_EINVAL;
+  const bool fast = c->fast && in->n_fast_slices > 0 && !tasks;
   const bool wave = in->n_wave_slices > 0;
   const bool general = (fast ? in->n_fast_slices : 0u) + in->n_wave_slices < in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
@@ -1625,10 +1734,19 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   HIPCHK(hipGetLastError());
   if (blocks && wave) hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
   HIPCHK(hipGetLastError());
-  if (blocks && general) hipLaunchKernelGGL(k_replay<true>, dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, L);
+  if (blocks && general) {
+    if (tasks)
+      hipLaunchKernelGGL((k_replay<true, true>), dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, L);
+    else
+      hipLaunchKernelGGL((k_replay<true, false>), dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, L);
+  }
   HIPCHK(hipGetLastError());
-  if (blocks && general && spill)
-    hipLaunchKernelGGL(k_replay<false>, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
+  if (blocks && general && spill) {
+    if (tasks)
+      hipLaunchKernelGGL((k_replay<false, true>), dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
+    else
+      hipLaunchKernelGGL((k_replay<false, false>), dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used + 1] : c->ev[1], st));
   if (ring) {

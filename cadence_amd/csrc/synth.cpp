@@ -38,6 +38,7 @@ enum : uint32_t {
   H_MEMO = 6,
   H_NONRETRY = 7,
   H_DOMAIN0 = 16,      // +k target domains
+  H_DOMAINID0 = 24,    // +k their domain IDs
   H_CHECKSUM0 = 32,    // +k binary checksums
   H_SIGNAME0 = 48,
   H_CHILDTYPE0 = 64,
@@ -262,6 +263,7 @@ struct Gen {
           e.a.ext.workflow_id = wf_handle(wf, 24 + r.below(4));
           e.a.ext.workflow_type = H_CHILDTYPE0 + r.below(4);
           e.a.ext.parent_close_policy = (int32_t)r.below(3);
+          e.a.ext.target_domain_id = H_DOMAINID0 + (e.a.ext.domain - H_DOMAIN0);
           children.push_back(Pend{e.event_id, 0, 0});
         } else if (kind == 1 && signals.size() < 4) {
           cdr_event& e = emit(CDR_EV_SE_INITIATED, false);
@@ -269,10 +271,20 @@ struct Gen {
           e.a.ext.signal_name = H_SIGNAME0 + r.below(4);
           e.a.ext.input = H_BLOB0 + r.below(100);
           e.a.ext.control = r.p(0.5) ? H_BLOB0 + r.below(100) : 0u;
+          // target execution / domain ID / child-only: derived, so the generator's random
+          // stream (and every committed digest) is unchanged
+          e.a.ext.target_domain_id = H_DOMAINID0 + (e.a.ext.domain - H_DOMAIN0);
+          e.a.ext.workflow_id = wf_handle(wf, 28 + (uint32_t)(e.event_id & 1));
+          e.a.ext.run_id = (e.event_id & 2) ? wf_handle(wf, 30) : 0u;
+          e.a.ext.flags |= (e.event_id & 4) ? CDR_XF_CHILD_ONLY : 0u;
           signals.push_back(Pend{e.event_id, 0, 0});
         } else if (kind == 2 && cancels.size() < 4) {
           cdr_event& e = emit(CDR_EV_RCE_INITIATED, false);
           e.a.ext.domain = H_DOMAIN0 + r.below(4);
+          e.a.ext.target_domain_id = H_DOMAINID0 + (e.a.ext.domain - H_DOMAIN0);
+          e.a.ext.workflow_id = wf_handle(wf, 28 + (uint32_t)(e.event_id & 1));
+          e.a.ext.run_id = (e.event_id & 2) ? wf_handle(wf, 30) : 0u;
+          e.a.ext.flags |= (e.event_id & 4) ? CDR_XF_CHILD_ONLY : 0u;
           cancels.push_back(Pend{e.event_id, 0, 0});
         } else if (!acts.empty()) {
           size_t k = r.below((uint32_t)acts.size());

@@ -226,7 +226,7 @@ def plan(batch: Batch) -> Plan:
 class Outputs:
     """Host buffers for one batch's persisted mutable states (zero-initialised)."""
 
-    def __init__(self, batch: Batch, pl: Plan):
+    def __init__(self, batch: Batch, pl: Plan, tasks: bool = False):
         n = max(1, batch.n_wfs)
         self.n_wfs = batch.n_wfs
         self.plan = pl
@@ -234,6 +234,11 @@ class Outputs:
         self.exec = (abi.CdrExecInfo * n)()
         self.repl = (abi.CdrReplState * n)()
         self.tables = {t: (TABLE_TYPES[t] * max(1, getattr(pl.totals, t)))() for t in TABLES}
+        self.tasks = None
+        if tasks:  # stateBuilder transfer / timer task lists (cdr_task)
+            self.tasks = {"xfer": (abi.CdrTask * max(1, pl.totals.xfer))(),
+                          "ttask": (abi.CdrTask * max(1, pl.totals.ttask))(),
+                          "n": (C.c_uint32 * (2 * n))()}
 
     def cstruct(self) -> abi.CdrOut:
         o = abi.CdrOut()
@@ -242,8 +247,19 @@ class Outputs:
         o.repl = C.addressof(self.repl)
         for t in TABLES:
             setattr(o, t, C.addressof(self.tables[t]))
+        if self.tasks is not None:
+            o.transfer = C.addressof(self.tasks["xfer"])
+            o.timer_tasks = C.addressof(self.tasks["ttask"])
+            o.n_tasks = C.addressof(self.tasks["n"])
         self._keep = o
         return o
+
+    def task_rows(self, w: int, kind: str):
+        """Transfer ("xfer") or timer ("ttask") tasks of entry w, in generation order."""
+        c = self.plan.caps[w]
+        off = c.xfer_off if kind == "xfer" else c.ttask_off
+        n = self.tasks["n"][2 * w + (0 if kind == "xfer" else 1)]
+        return [self.tasks[kind][off + j] for j in range(n)]
 
     # ---- per-workflow accessors
     def rows(self, w: int, table: str):
@@ -288,9 +304,11 @@ class Engine:
         except Exception:
             pass
 
-    def replay(self, batch: Batch, pl: Plan | None = None) -> Outputs:
+    def replay(self, batch: Batch, pl: Plan | None = None, tasks: bool = False) -> Outputs:
+        """Replay through cdr_replay_batch; `tasks` also emits the transfer / timer
+        task lists (general kernel only)."""
         pl = pl or plan(batch)
-        out = Outputs(batch, pl)
+        out = Outputs(batch, pl, tasks)
         rc = abi.lib().cdr_replay_batch(self.ctx, C.byref(batch.cstruct()), pl.caps, C.byref(pl.totals),
                                        C.byref(out.cstruct()))
         if rc:
@@ -328,13 +346,33 @@ def compare(batch: Batch, a: Outputs, b: Outputs, limit: int = 10):
                 xa = b"".join(_bytes(r) for r in a.rows(w, t))
                 xb = b"".join(_bytes(r) for r in b.rows(w, t))
                 if xa != xb:
-                    rows_a, rows_b = a.rows(w, t), b.rows(w, t)
+                    rows_a, rows_b = a.rows(w, t), b.rows(w, t)  # noqa: F841
                     for j, (p, q) in enumerate(zip(rows_a, rows_b)):
                         fd = [f for f, _ in type(p)._fields_ if _bytes(p) != _bytes(q) and
                               getattr(p, f) != getattr(q, f)]
                         if fd:
                             bad.append(f"wf {w}: {t}[{j}] differs in {fd}")
                             break
+        if len(bad) >= limit:
+            break
+    return bad
+
+
+def compare_tasks(batch: Batch, a: Outputs, b: Outputs, limit: int = 10):
+    """Task lists of every entry that is OK in both outputs, field by field."""
+    bad = []
+    for w in range(batch.n_wfs):
+        if a.result[w].code != abi.OK or b.result[w].code != abi.OK:
+            continue
+        for kind in ("xfer", "ttask"):
+            ra, rb = a.task_rows(w, kind), b.task_rows(w, kind)
+            if len(ra) != len(rb):
+                bad.append(f"wf {w}: {kind} count {len(ra)} != {len(rb)}")
+                continue
+            for j, (p, q) in enumerate(zip(ra, rb)):
+                if _bytes(p) != _bytes(q):
+                    bad.append(f"wf {w}: {kind}[{j}] {_rec(p, None)} != {_rec(q, None)}")
+                    break
         if len(bad) >= limit:
             break
     return bad

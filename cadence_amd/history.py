@@ -94,6 +94,7 @@ class HistoryBuilder:
             s.cron_schedule = I(x.get("cronSchedule", ""))
             s.attempt = int(x.get("attempt", 0))
             s.first_decision_backoff_s = int(x.get("firstDecisionTaskBackoffSeconds", 0))
+            cron_init = x.get("initiator") in ("CronSchedule", "CRON_SCHEDULE", 2)  # ContinueAsNewInitiator
             s.expiration_ts = int(x.get("expirationTimestamp", 0))
             f = 0
             if x.get("parentWorkflowDomain") is not None:
@@ -109,6 +110,8 @@ class HistoryBuilder:
             if x.get("parentInitiatedEventId") is not None:
                 f |= abi.SF_HAS_PARENT_INITIATED
                 s.parent_initiated_id = int(x["parentInitiatedEventId"])
+            if cron_init:
+                f |= abi.SF_CRON_INITIATOR
             rp = x.get("retryPolicy")
             if rp is not None:
                 f |= abi.SF_HAS_RETRY
@@ -207,6 +210,9 @@ class HistoryBuilder:
             ex = a.ext
             ex.domain = I(x.get("domain", ""))
             ex.flags = abi.XF_DOMAIN_MISSING if x.get("domain", "") in self.domains_missing else 0
+            ex.flags |= abi.XF_CHILD_ONLY if x.get("childWorkflowOnly") else 0
+            dom = x.get("domain", "")
+            ex.target_domain_id = I(self.domain_ids.get(dom, "id-of-" + dom))  # the domain cache's ID
             we = x.get("workflowExecution") or {}
             ex.workflow_id = I(x.get("workflowId", we.get("workflowId", "")))
             ex.run_id = I(we.get("runId", ""))

@@ -69,6 +69,8 @@ extern "C" {
  *                             n = parentClosePolicy
  *   SignalExternalWorkflowExecutionInitiated  key = domain, aux = input << 32 | control, h = signalName
  *   RequestCancelExternalWorkflowExecutionInitiated  key = domain
+ *                             (these three: key |= arena word offset (< 2^32) of their
+ *                             cdr_attr_external << 32, read only when tasks are emitted)
  *   ChildWorkflowExecutionStarted  key = initiatedEventId, h = runId
  *   other child / external closes  key = initiatedEventId
  *   UpsertWorkflowSearchAttributes  aux = kv offset, h = kv count
@@ -150,7 +152,9 @@ typedef struct cdr_slices {
 #define CDR_TB(t) (1ull << (t))
 #define CDR_NEED_TS                                                                                  \
   (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_DT_SCHEDULED) | CDR_TB(CDR_EV_DT_STARTED) |              \
-   CDR_TB(CDR_EV_AT_SCHEDULED) | CDR_TB(CDR_EV_AT_STARTED) | CDR_TB(CDR_EV_TIMER_STARTED))
+   CDR_TB(CDR_EV_AT_SCHEDULED) | CDR_TB(CDR_EV_AT_STARTED) | CDR_TB(CDR_EV_TIMER_STARTED) |            \
+   CDR_TB(CDR_EV_WF_COMPLETED) | CDR_TB(CDR_EV_WF_FAILED) | CDR_TB(CDR_EV_WF_TIMED_OUT) |              \
+   CDR_TB(CDR_EV_WF_CANCELED) | CDR_TB(CDR_EV_WF_TERMINATED) | CDR_TB(CDR_EV_WF_CONTINUED_AS_NEW))
 #define CDR_NEED_KEY                                                                                 \
   (CDR_TB(CDR_EV_DT_STARTED) | CDR_TB(CDR_EV_AT_SCHEDULED) | CDR_TB(CDR_EV_AT_STARTED) |              \
    CDR_TB(CDR_EV_AT_COMPLETED) | CDR_TB(CDR_EV_AT_FAILED) | CDR_TB(CDR_EV_AT_TIMED_OUT) |              \
@@ -159,7 +163,8 @@ typedef struct cdr_slices {
    CDR_TB(CDR_EV_CHILD_STARTED) | CDR_TB(CDR_EV_CHILD_START_FAILED) | CDR_TB(CDR_EV_CHILD_COMPLETED) | \
    CDR_TB(CDR_EV_CHILD_FAILED) | CDR_TB(CDR_EV_CHILD_CANCELED) | CDR_TB(CDR_EV_CHILD_TIMED_OUT) |      \
    CDR_TB(CDR_EV_CHILD_TERMINATED) | CDR_TB(CDR_EV_RCE_FAILED) | CDR_TB(CDR_EV_EXT_CANCEL_REQUESTED) | \
-   CDR_TB(CDR_EV_SE_FAILED) | CDR_TB(CDR_EV_EXT_SIGNALED))
+   CDR_TB(CDR_EV_SE_FAILED) | CDR_TB(CDR_EV_EXT_SIGNALED) | CDR_TB(CDR_EV_RCE_INITIATED) |                 \
+   CDR_TB(CDR_EV_SE_INITIATED))
 #define CDR_NEED_AUX                                                                                 \
   (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_DT_SCHEDULED) | CDR_TB(CDR_EV_DT_COMPLETED) |            \
    CDR_TB(CDR_EV_AT_SCHEDULED) | CDR_TB(CDR_EV_TIMER_STARTED) | CDR_TB(CDR_EV_CHILD_INITIATED) |       \

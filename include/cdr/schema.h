@@ -286,7 +286,8 @@ typedef struct cdr_attr_timer { /* Timer{Started,Fired,Canceled}, CancelTimerFai
 typedef struct cdr_attr_external { /* StartChild/SignalExternal/RequestCancelExternal ...Initiated */
   uint32_t domain, workflow_id, run_id, workflow_type;
   uint32_t signal_name, input, control, flags;
-  int32_t parent_close_policy, _pad;
+  int32_t parent_close_policy;
+  uint32_t target_domain_id; /* the domain cache's ID for `domain` (transfer tasks only) */
 } cdr_attr_external;
 
 typedef struct cdr_attr_initiated_ref { /* every event that closes an external/child entity */
@@ -470,6 +471,40 @@ typedef struct cdr_signal_info { /* SignalInfo dataInterfaces.go:698-706 */
   uint32_t signal_name, input, control, _pad;
 } cdr_signal_info;
 
+/* Transfer and timer tasks applyEvents appends (stateBuilder.go:613-804; the
+ * persistence.Task types of dataInterfaces.go:121-155).  Emitted only when the caller
+ * asks for them (cdr_out.transfer != NULL): in emission order, per entry, at the
+ * caps.xfer_off / ttask_off slices, counts in cdr_out.n_tasks. */
+enum cdr_task_type {
+  /* transfer tasks (TransferTaskType*) */
+  CDR_TT_DECISION = 0,        /* DomainID, TaskList, ScheduleID (event_id) */
+  CDR_TT_ACTIVITY = 1,        /* DomainID, TaskList, ScheduleID */
+  CDR_TT_CLOSE_EXECUTION = 2,
+  CDR_TT_CANCEL_EXECUTION = 3, /* TargetDomainID, TargetWorkflowID, TargetRunID, child-only, InitiatedID */
+  CDR_TT_START_CHILD = 4,      /* TargetDomainID, TargetWorkflowID, InitiatedID */
+  CDR_TT_SIGNAL_EXECUTION = 5, /* as CANCEL_EXECUTION */
+  CDR_TT_RECORD_STARTED = 6,
+  CDR_TT_UPSERT_SA = 8,
+  /* timer tasks (TaskType*) */
+  CDR_TT_DECISION_TIMEOUT = 16 + 0, /* visibility, TimeoutType, EventID = ScheduleID, ScheduleAttempt */
+  CDR_TT_ACTIVITY_TIMEOUT = 16 + 1, /* visibility, TimeoutType, EventID = ScheduleID, Attempt */
+  CDR_TT_USER_TIMER = 16 + 2,       /* visibility, EventID = StartedID */
+  CDR_TT_WORKFLOW_TIMEOUT = 16 + 3, /* visibility */
+  CDR_TT_DELETE_HISTORY = 16 + 4,   /* visibility */
+  CDR_TT_WORKFLOW_BACKOFF = 16 + 6  /* visibility, TimeoutType = WorkflowBackoffTimeoutType */
+};
+#define CDR_TF_CHILD_ONLY 0x1u /* TargetChildWorkflowOnly */
+typedef struct cdr_task {
+  uint32_t type; /* cdr_task_type */
+  int32_t timeout_type;
+  int64_t event_id;      /* ScheduleID / InitiatedID / EventID, 0 when the type has none */
+  int64_t visibility_ts; /* timer tasks (ns); 0 for transfer tasks */
+  int64_t attempt;
+  uint32_t domain_id, task_list; /* handles: DomainID or TargetDomainID; TaskList */
+  uint32_t target_workflow_id, target_run_id;
+  uint32_t flags, _pad; /* CDR_TF_* */
+} cdr_task;
+
 /* per-workflow result: status + where each variable-length table lives */
 typedef struct cdr_wf_result {
   int32_t code;   /* cdr_status */
@@ -489,6 +524,9 @@ typedef struct cdr_wf_caps {
    * (#scheduled - #closed), timers = #TimerStarted */
   uint32_t act_live, timer_live;
   uint32_t flags, _pad; /* CDR_CAP_* */
+  /* task slices (bounds from the event types; used only when tasks are emitted) */
+  uint64_t xfer_off, ttask_off;
+  uint32_t xfer_cap, ttask_cap;
 } cdr_wf_caps;
 /* the history fits the fast-path replay kernel (replay_fast.inc): Started first and
  * only there, event types in CDR_FAST_TYPES, at most one pending activity, builder
@@ -502,6 +540,7 @@ typedef struct cdr_wf_caps {
 
 typedef struct cdr_totals {
   uint64_t act, timer, child, cancel, signal, vh, rp, sa;
+  uint64_t xfer, ttask; /* task rows (cdr_task) */
 } cdr_totals;
 
 /* Caller-allocated output buffers (host or device memory, per the entry point). */
@@ -517,6 +556,10 @@ typedef struct cdr_out {
   cdr_signal_info* signal; /* [totals.signal] */
   cdr_reset_point* rp;     /* [totals.rp] */
   cdr_kv* sa;              /* [totals.sa] */
+  /* tasks (nullable: NULL = not emitted, the default; rebuild discards them) */
+  cdr_task* transfer;      /* [totals.xfer] */
+  cdr_task* timer_tasks;   /* [totals.ttask] */
+  uint32_t* n_tasks;       /* [2 * n_wfs]: transfer, timer count of entry w */
 } cdr_out;
 
 /* Carry-in: replay onto a LOADED mutable state, the analogue of

@@ -37,11 +37,12 @@ def lib():
     return _lib
 
 
-def replay(batch, pl=None, threads: int = 1):
-    """Oracle replay of a cadence_amd.engine.Batch into host Outputs."""
+def replay(batch, pl=None, threads: int = 1, tasks: bool = False):
+    """Oracle replay of a cadence_amd.engine.Batch into host Outputs (`tasks`: also
+    the transfer / timer task lists)."""
     from cadence_amd import engine
     pl = pl or engine.plan(batch)
-    out = engine.Outputs(batch, pl)
+    out = engine.Outputs(batch, pl, tasks)
     rc = lib().cdro_replay_batch(C.byref(batch.cstruct()), pl.caps, C.byref(out.cstruct()), threads)
     if rc:
         raise RuntimeError(f"cdro_replay_batch rc={rc}")

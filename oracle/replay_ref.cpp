@@ -262,6 +262,26 @@ struct MutableState {
   std::map<int64_t, ChildInfo> pendingChildExecutionInfoIDs;
   std::map<int64_t, CancelInfo> pendingRequestCancelInfoIDs;
   std::map<int64_t, SignalInfo> pendingSignalInfoIDs;
+  // stateBuilder.transferTasks / timerTasks (stateBuilder.go:613-804), each task once
+  // in generation order (getTransferTasks / getTimerTasks)
+  std::vector<cdr_task> transferTasks, timerTasks;
+  void AddXfer(uint32_t type, int64_t eventID, uint32_t domain, uint32_t taskList) {
+    cdr_task t{};
+    t.type = type;
+    t.event_id = eventID;
+    t.domain_id = domain;
+    t.task_list = taskList;
+    transferTasks.push_back(t);
+  }
+  void AddTimer(uint32_t type, int32_t timeoutType, int64_t eventID, int64_t vis, int64_t attempt) {
+    cdr_task t{};
+    t.type = type;
+    t.timeout_type = timeoutType;
+    t.event_id = eventID;
+    t.visibility_ts = vis;
+    t.attempt = attempt;
+    timerTasks.push_back(t);
+  }
 
   // newMutableStateBuilder (mutableStateBuilder.go:137-231)
   MutableState(const Ctx* c, int kind, int64_t failover, uint64_t key, int32_t retention)
@@ -279,6 +299,12 @@ struct MutableState {
     }
   }
 
+  // appendTasksForFinishedExecutions (stateBuilder.go:775-787): CloseExecutionTask +
+  // DeleteHistoryEventTask at the event time + the domain's retention
+  void AppendTasksForFinishedExecution(int64_t ts) {
+    AddXfer(CDR_TT_CLOSE_EXECUTION, 0, 0, 0);
+    AddTimer(CDR_TT_DELETE_HISTORY, 0, 0, ts + (int64_t)retention_days * 24LL * 3600LL * 1000000000LL, 0);
+  }
   bool IsWorkflowExecutionRunning() const {  // :1422-1435
     return ei.State == CDR_STATE_CREATED || ei.State == CDR_STATE_RUNNING;
   }
@@ -352,11 +378,12 @@ struct MutableState {
     UpdateDecision(r);
   }
   // ReplicateTransientDecisionTaskScheduled (:169-198)
-  void ReplicateTransientDecisionTaskScheduled() {
-    if (HasPendingDecision() || ei.DecisionAttempt == 0) return;
+  bool ReplicateTransientDecisionTaskScheduled() {
+    if (HasPendingDecision() || ei.DecisionAttempt == 0) return false;
     DecisionInfo d{GetCurrentVersion(), ei.NextEventID, CDR_EMPTY_EVENT_ID, ctx->empty_uuid,
                    ei.DecisionTimeoutValue, ei.DecisionAttempt, 0, ctx->b->now_ns, 0};
     UpdateDecision(d);
+    return true;
   }
 
   // DeleteActivity (:1247-1269)
@@ -412,6 +439,8 @@ struct MutableState {
     const Cand& h = c[0];
     if (h.created) return;  // firstActivityTimerTask (:384-389)
     ActivityInfo& ai = pendingActivityInfoIDs[h.sched];
+    // createNewTask (timerBuilder.go:391-408): ActivityTimeoutTask
+    AddTimer(CDR_TT_ACTIVITY_TIMEOUT, h.type, h.sched, h.t, ai.Attempt);
     int32_t bit = h.type == CDR_TIMEOUT_HEARTBEAT        ? CDR_TTS_HEARTBEAT
                   : h.type == CDR_TIMEOUT_SCHEDULE_TO_START ? CDR_TTS_SCHEDULE_TO_START
                   : h.type == CDR_TIMEOUT_SCHEDULE_TO_CLOSE ? CDR_TTS_SCHEDULE_TO_CLOSE
@@ -435,6 +464,7 @@ struct MutableState {
     }
     if (!head) return;
     if (head->TaskID == CDR_TIMER_TASK_STATUS_CREATED) return;  // firstTimerTask (:370-375)
+    AddTimer(CDR_TT_USER_TIMER, 0, head->StartedID, head->ExpiryTime, 0);  // createNewTask: UserTimerTask
     pendingTimerInfoIDs[head->TimerID].TaskID = CDR_TIMER_TASK_STATUS_CREATED;
   }
 };
@@ -578,6 +608,17 @@ struct StateBuilder {
             }
           }
           if (ms->hasRS) ms->rs.StartVersion = ev.version;  // :182-184
+          {  // scheduleWorkflowTimerTask (:706-735) + RecordWorkflowStartedTask (:614-616)
+            const int64_t backoff = (int64_t)a.first_decision_backoff_s * 1000000000LL;
+            int64_t timeout = ev.timestamp + (int64_t)ei.WorkflowTimeout * 1000000000LL;
+            if (backoff != 0) {
+              timeout += backoff;
+              ms->AddTimer(CDR_TT_WORKFLOW_BACKOFF, (a.flags & CDR_SF_CRON_INITIATOR) ? 1 : 0, 0,
+                           ev.timestamp + backoff, 0);
+            }
+            ms->AddTimer(CDR_TT_WORKFLOW_TIMEOUT, 0, 0, timeout, 0);
+            ms->AddXfer(CDR_TT_RECORD_STARTED, 0, 0, 0);
+          }
           break;
         }
         case CDR_EV_DT_SCHEDULED: {  // :186-200 -> decision manager :143-167
@@ -585,6 +626,7 @@ struct StateBuilder {
                                        ev.a.dt_sched.start_to_close_s, ev.a.dt_sched.attempt, 0,
                                        ev.timestamp, ev.timestamp};
           ms->UpdateDecision(d);
+          ms->AddXfer(CDR_TT_DECISION, ev.event_id, domainID, ei.TaskList);  // :196-197
           break;
         }
         case CDR_EV_DT_STARTED: {  // :202-213 -> :200-253
@@ -600,6 +642,9 @@ struct StateBuilder {
                                         d.DecisionTimeout, d.Attempt, ev.timestamp, d.ScheduledTimestamp,
                                         d.OriginalScheduledTimestamp};
           ms->UpdateDecision(nd);
+          // scheduleDecisionTimerTask (:210-211, timerBuilder.go:322-331)
+          ms->AddTimer(CDR_TT_DECISION_TIMEOUT, CDR_TIMEOUT_START_TO_CLOSE, scheduleID,
+                       ev.timestamp + (int64_t)nd.DecisionTimeout * 1000000000LL, nd.Attempt);
           break;
         }
         case CDR_EV_DT_COMPLETED: {  // :215-219 -> :255-262, :789-800
@@ -631,11 +676,13 @@ struct StateBuilder {
         }
         case CDR_EV_DT_TIMED_OUT:  // :221-239
           ms->FailDecision(ev.a.dt.timeout_type != CDR_TIMEOUT_SCHEDULE_TO_START);
-          ms->ReplicateTransientDecisionTaskScheduled();
+          if (ms->ReplicateTransientDecisionTaskScheduled())
+            ms->AddXfer(CDR_TT_DECISION, ei.DecisionScheduleID, domainID, ei.TaskList);  // :235-236
           break;
         case CDR_EV_DT_FAILED:  // :241-257
           ms->FailDecision(true);
-          ms->ReplicateTransientDecisionTaskScheduled();
+          if (ms->ReplicateTransientDecisionTaskScheduled())
+            ms->AddXfer(CDR_TT_DECISION, ei.DecisionScheduleID, domainID, ei.TaskList);  // :253-254
           break;
         case CDR_EV_AT_SCHEDULED: {  // :259-269 -> mutableStateBuilder.go:1982-2028
           const cdr_attr_at_scheduled& a = ev.a.at_sched;
@@ -667,6 +714,7 @@ struct StateBuilder {
           }
           ms->pendingActivityInfoIDs[ai.ScheduleID] = ai;
           ms->pendingActivityInfoByActivityID[ai.ActivityID] = ai.ScheduleID;
+          ms->AddXfer(CDR_TT_ACTIVITY, ai.ScheduleID, domainID, ei.TaskList);  // :265-266
           ms->ActivityTimerPick();
           break;
         }
@@ -733,6 +781,14 @@ struct StateBuilder {
           ci.ParentClosePolicy = a.parent_close_policy;
           ms->pendingChildExecutionInfoIDs[ci.InitiatedID] = ci;
           if (a.flags & CDR_XF_DOMAIN_MISSING) return fail(CDR_E_DOMAIN_NOT_FOUND, i);  // :365-368
+          {  // scheduleStartChildWorkflowTransferTask (:370-371)
+            cdr_task t{};
+            t.type = CDR_TT_START_CHILD;
+            t.event_id = ci.InitiatedID;
+            t.domain_id = a.target_domain_id;
+            t.target_workflow_id = a.workflow_id;
+            ms->transferTasks.push_back(t);
+          }
           break;
         }
         case CDR_EV_CHILD_START_FAILED:  // :373-376
@@ -758,6 +814,16 @@ struct StateBuilder {
           cdr_uuid(b->uuid_seed, ms->wf_key, CDR_UUID_CANCEL_REQ, ev.event_id, &rci.ReqLo, &rci.ReqHi);
           ms->pendingRequestCancelInfoIDs[rci.InitiatedID] = rci;
           if (ev.a.ext.flags & CDR_XF_DOMAIN_MISSING) return fail(CDR_E_DOMAIN_NOT_FOUND, i);
+          {  // scheduleCancelExternalWorkflowTransferTask (:421-427)
+            cdr_task t{};
+            t.type = CDR_TT_CANCEL_EXECUTION;
+            t.event_id = rci.InitiatedID;
+            t.domain_id = ev.a.ext.target_domain_id;
+            t.target_workflow_id = ev.a.ext.workflow_id;
+            t.target_run_id = ev.a.ext.run_id;
+            t.flags = (ev.a.ext.flags & CDR_XF_CHILD_ONLY) ? CDR_TF_CHILD_ONLY : 0u;
+            ms->transferTasks.push_back(t);
+          }
           break;
         }
         case CDR_EV_RCE_FAILED:            // :429-432
@@ -776,6 +842,16 @@ struct StateBuilder {
           si.Control = a.control;
           ms->pendingSignalInfoIDs[si.InitiatedID] = si;
           if (a.flags & CDR_XF_DOMAIN_MISSING) return fail(CDR_E_DOMAIN_NOT_FOUND, i);
+          {  // scheduleSignalWorkflowTransferTask (:452-458)
+            cdr_task t{};
+            t.type = CDR_TT_SIGNAL_EXECUTION;
+            t.event_id = si.InitiatedID;
+            t.domain_id = a.target_domain_id;
+            t.target_workflow_id = a.workflow_id;
+            t.target_run_id = a.run_id;
+            t.flags = (a.flags & CDR_XF_CHILD_ONLY) ? CDR_TF_CHILD_ONLY : 0u;
+            ms->transferTasks.push_back(t);
+          }
           break;
         }
         case CDR_EV_SE_FAILED:    // :460-463
@@ -804,6 +880,7 @@ struct StateBuilder {
             return fail(CDR_E_INVALID_STATE_TRANSITION, i);
           ei.CompletionEventBatchID = first.event_id;
           ms->ClearStickyness();
+          ms->AppendTasksForFinishedExecution(ev.timestamp);  // :757-787
           break;
         }
         case CDR_EV_UPSERT_SA: {  // :533-535 -> :2746-2768
@@ -819,6 +896,7 @@ struct StateBuilder {
             if (!found) ei.SearchAttributes.push_back(kv);
           }
           ei.HasSearchAttr = true;  // mergeMapOfByteArray makes a map if nil
+          ms->AddXfer(CDR_TT_UPSERT_SA, 0, 0, 0);  // :535
           break;
         }
         case CDR_EV_WF_CONTINUED_AS_NEW: {  // :537-595
@@ -848,6 +926,7 @@ struct StateBuilder {
             return fail(CDR_E_INVALID_STATE_TRANSITION, i);
           ei.CompletionEventBatchID = first.event_id;
           ms->ClearStickyness();
+          ms->AppendTasksForFinishedExecution(ev.timestamp);  // :592
           break;
         }
         default:
@@ -1051,6 +1130,13 @@ bool write_state(const MutableState& ms, const cdr_batch* b, uint32_t w, const c
   r.n_reset_points = (uint32_t)ei.ResetPoints.size();
   for (size_t j = 0; j < sa.size(); j++) out->sa[cp.sa_off + j] = sa[j];
   r.n_search_attr = (uint32_t)sa.size();
+  if (out->transfer) {
+    if (ms.transferTasks.size() > cp.xfer_cap || ms.timerTasks.size() > cp.ttask_cap) return false;
+    for (size_t j = 0; j < ms.transferTasks.size(); j++) out->transfer[cp.xfer_off + j] = ms.transferTasks[j];
+    for (size_t j = 0; j < ms.timerTasks.size(); j++) out->timer_tasks[cp.ttask_off + j] = ms.timerTasks[j];
+    out->n_tasks[2 * w] = (uint32_t)ms.transferTasks.size();
+    out->n_tasks[2 * w + 1] = (uint32_t)ms.timerTasks.size();
+  }
   return true;
 }
 

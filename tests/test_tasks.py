@@ -1,0 +1,218 @@
+"""Transfer / timer task emission (stateBuilder.go:613-804).
+
+CPU: the oracle's task lists against the reference's own expectations in
+stateBuilder_test.go (restated through small hand-written histories): the Started
+event's WorkflowTimeout / WorkflowBackoffTimer / RecordWorkflowStarted tasks
+(:153-220), the transient decision's DecisionTask (:1180-1230), the close tasks
+(:251), the child / signal / cancel transfer tasks (:818, :913, :1006) and the
+timer-builder tasks.  GPU (-m gpu): the general kernel's task lists == the oracle's,
+field by field, for every config, builder and carried-in state.
+"""
+import pytest
+
+from cadence_amd import abi, engine
+from cadence_amd.history import HistoryBuilder
+
+NS = 10 ** 9
+T0 = 1_600_000_000 * NS
+
+
+def _ev(i, ty, ts=None, **a):
+    return dict(eventId=i, version=1, timestamp=T0 + i * NS if ts is None else ts, eventType=ty, **a)
+
+
+def _started(i=1, backoff=0, cron=False, timeout=100):
+    x = {"workflowType": {"name": "wt"}, "taskList": {"name": "tl"},
+         "executionStartToCloseTimeoutSeconds": timeout, "taskStartToCloseTimeoutSeconds": 10}
+    if backoff:
+        x["firstDecisionTaskBackoffSeconds"] = backoff
+    if cron:
+        x["initiator"] = "CronSchedule"
+        x["cronSchedule"] = "* * * * *"
+    return _ev(i, "WorkflowExecutionStarted", workflowExecutionStartedEventAttributes=x)
+
+
+def _dt_sched(i, att=0):
+    return _ev(i, "DecisionTaskScheduled", decisionTaskScheduledEventAttributes={
+        "taskList": {"name": "tl"}, "startToCloseTimeoutSeconds": 10, "attempt": att})
+
+
+def _replay(calls, retention=1, **kw):
+    import oracle
+    hb = HistoryBuilder()
+    w = hb.workflow(workflow_id="wf", run_id="run", request_id="req", retention_days=retention, **kw)
+    w.calls = calls
+    b = hb.build()
+    out = oracle.replay(b, tasks=True)
+    assert out.result[0].code == abi.OK, out.result[0].code
+    I = hb.intern
+    return out, I
+
+
+def _types(rows):
+    return [abi.TASK_TYPES[r.type] for r in rows]
+
+
+@pytest.mark.parametrize("backoff,cron", [(0, False), (60, True), (30, False)])
+def test_started_tasks(backoff, cron):
+    """stateBuilder_test.go:153-220: WorkflowTimeoutTask at now + WorkflowTimeout (+
+    backoff), a WorkflowBackoffTimerTask at now + backoff when there is one (timeout
+    type Cron for a cron initiator), one RecordWorkflowStartedTask."""
+    out, I = _replay([[_started(backoff=backoff, cron=cron)]])
+    tt, xt = out.task_rows(0, "ttask"), out.task_rows(0, "xfer")
+    assert _types(xt) == ["RecordWorkflowStarted"]
+    ts = T0 + NS
+    if backoff:
+        assert _types(tt) == ["WorkflowBackoffTimer", "WorkflowTimeout"]
+        assert tt[0].visibility_ts == ts + backoff * NS
+        assert tt[0].timeout_type == (1 if cron else 0)  # WorkflowBackoffTimeoutType{Retry,Cron}
+        assert tt[1].visibility_ts == ts + (100 + backoff) * NS
+    else:
+        assert _types(tt) == ["WorkflowTimeout"]
+        assert tt[0].visibility_ts == ts + 100 * NS
+
+
+def test_decision_tasks_and_transient():
+    """DecisionTask per scheduled decision (DomainID, TaskList, ScheduleID); a
+    DecisionTimeoutTask at Started + StartToClose; a timed-out decision schedules a
+    transient DecisionTask at the call's NextEventID (stateBuilder_test.go:1180-1230)."""
+    calls = [[_started(), _dt_sched(2)],
+             [_ev(3, "DecisionTaskStarted", decisionTaskStartedEventAttributes={"scheduledEventId": 2,
+                                                                                 "requestId": "r"})],
+             [_ev(4, "DecisionTaskTimedOut", decisionTaskTimedOutEventAttributes={
+                 "scheduledEventId": 2, "startedEventId": 3, "timeoutType": 0})]]
+    out, I = _replay(calls)
+    xt, tt = out.task_rows(0, "xfer"), out.task_rows(0, "ttask")
+    assert _types(xt) == ["RecordWorkflowStarted", "DecisionTask", "DecisionTask"]
+    assert (xt[1].event_id, xt[1].domain_id, xt[1].task_list) == (2, I("domain-id"), I("tl"))
+    assert xt[2].event_id == 4  # NextEventID as of the call's start (transient ScheduleID)
+    assert _types(tt) == ["WorkflowTimeout", "DecisionTimeout"]
+    d = tt[1]
+    assert (d.event_id, d.visibility_ts, d.timeout_type, d.attempt) == (2, T0 + 3 * NS + 10 * NS, 0, 0)
+
+
+def test_close_tasks_retention():
+    """appendTasksForFinishedExecutions: CloseExecutionTask + DeleteHistoryEventTask at
+    the close event's time + retention days (stateBuilder_test.go:251)."""
+    calls = [[_started(), _dt_sched(2)],
+             [_ev(3, "DecisionTaskStarted", decisionTaskStartedEventAttributes={"scheduledEventId": 2})],
+             [_ev(4, "DecisionTaskCompleted", decisionTaskCompletedEventAttributes={"scheduledEventId": 2,
+                                                                                    "startedEventId": 3}),
+              _ev(5, "WorkflowExecutionCompleted", workflowExecutionCompletedEventAttributes={})]]
+    out, _ = _replay(calls, retention=3)
+    xt, tt = out.task_rows(0, "xfer"), out.task_rows(0, "ttask")
+    assert _types(xt)[-1] == "CloseExecution"
+    assert _types(tt)[-1] == "DeleteHistoryEvent"
+    assert tt[-1].visibility_ts == T0 + 5 * NS + 3 * 86400 * NS
+
+
+def test_external_tasks():
+    """StartChildExecutionTask / SignalExecutionTask / CancelExecutionTask carry the
+    target domain's ID, workflow, run and child-only flag (stateBuilder_test.go:818,
+    :913, :1006) and the initiated event ID."""
+    we = {"workflowId": "target-wf", "runId": "target-run"}
+    calls = [[_started(), _dt_sched(2)],
+             [_ev(3, "DecisionTaskStarted", decisionTaskStartedEventAttributes={"scheduledEventId": 2})],
+             [_ev(4, "DecisionTaskCompleted", decisionTaskCompletedEventAttributes={"scheduledEventId": 2,
+                                                                                    "startedEventId": 3}),
+              _ev(5, "StartChildWorkflowExecutionInitiated", startChildWorkflowExecutionInitiatedEventAttributes={
+                  "domain": "child-dom", "workflowId": "child-wf", "workflowType": {"name": "ct"}}),
+              _ev(6, "SignalExternalWorkflowExecutionInitiated",
+                  signalExternalWorkflowExecutionInitiatedEventAttributes={
+                      "domain": "sig-dom", "workflowExecution": we, "signalName": "s", "childWorkflowOnly": True}),
+              _ev(7, "RequestCancelExternalWorkflowExecutionInitiated",
+                  requestCancelExternalWorkflowExecutionInitiatedEventAttributes={
+                      "domain": "can-dom", "workflowExecution": we})]]
+    out, I = _replay(calls)
+    xt = out.task_rows(0, "xfer")
+    assert _types(xt)[-3:] == ["StartChildExecution", "SignalExecution", "CancelExecution"]
+    c, s, k = xt[-3:]
+    assert (c.event_id, c.domain_id, c.target_workflow_id) == (5, I("id-of-child-dom"), I("child-wf"))
+    assert (s.event_id, s.domain_id, s.target_workflow_id, s.target_run_id, s.flags) == (
+        6, I("id-of-sig-dom"), I("target-wf"), I("target-run"), 1)
+    assert (k.event_id, k.domain_id, k.target_run_id, k.flags) == (7, I("id-of-can-dom"), I("target-run"), 0)
+
+
+def test_timer_builder_tasks():
+    """UserTimerTask for the earliest timer when it is first picked (EventID = its
+    StartedID, visibility = its expiry); ActivityTimeoutTask for the earliest activity
+    candidate (ScheduleToStart before start, timerBuilder_test.go:85-215)."""
+    calls = [[_started(), _dt_sched(2)],
+             [_ev(3, "DecisionTaskStarted", decisionTaskStartedEventAttributes={"scheduledEventId": 2})],
+             [_ev(4, "DecisionTaskCompleted", decisionTaskCompletedEventAttributes={"scheduledEventId": 2,
+                                                                                    "startedEventId": 3}),
+              _ev(5, "TimerStarted", timerStartedEventAttributes={"timerId": "t1", "startToFireTimeoutSeconds": 50}),
+              _ev(6, "TimerStarted", timerStartedEventAttributes={"timerId": "t2", "startToFireTimeoutSeconds": 20}),
+              _ev(7, "ActivityTaskScheduled", activityTaskScheduledEventAttributes={
+                  "activityId": "a", "taskList": {"name": "atl"}, "scheduleToStartTimeoutSeconds": 5,
+                  "scheduleToCloseTimeoutSeconds": 60, "startToCloseTimeoutSeconds": 30,
+                  "heartbeatTimeoutSeconds": 0})]]
+    out, I = _replay(calls)
+    tt = out.task_rows(0, "ttask")
+    ut = [t for t in tt if abi.TASK_TYPES[t.type] == "UserTimer"]
+    at = [t for t in tt if abi.TASK_TYPES[t.type] == "ActivityTimeout"]
+    assert [(t.event_id, t.visibility_ts) for t in ut] == [(5, T0 + 5 * NS + 50 * NS), (6, T0 + 6 * NS + 20 * NS)]
+    assert [(t.event_id, t.timeout_type, t.visibility_ts) for t in at] == [(7, 1, T0 + 7 * NS + 5 * NS)]
+    assert _types(out.task_rows(0, "xfer"))[-1] == "ActivityTask"
+
+
+def test_task_caps_bound_oracle():
+    """The planner's task capacities bound what the oracle emits on every config."""
+    import oracle
+    for cfg in range(6):
+        b = engine.synth_batch(cfg, 120, seed=cfg + 11, error_rate=0.1)
+        out = oracle.replay(b, tasks=True)
+        for w in range(b.n_wfs):
+            if out.result[w].code == abi.OK:
+                c = out.plan.caps[w]
+                assert out.tasks["n"][2 * w] <= c.xfer_cap and out.tasks["n"][2 * w + 1] <= c.ttask_cap
+
+
+# ------------------------------------------------------------------ GPU
+def _check_tasks(eng, b):
+    import oracle
+    ref = oracle.replay(b, tasks=True)
+    got = eng.replay(b, tasks=True)
+    bad = engine.compare(b, got, ref) + engine.compare_tasks(b, got, ref)
+    assert not bad, "\n".join(bad[:10])
+    return ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
+def test_gpu_tasks_configs(engine_gpu, cfg):
+    b = engine.synth_batch(cfg, 300, seed=0x5EED0300 + cfg, error_rate=0.1 if cfg in (0, 3, 4) else 0.0)
+    ref = _check_tasks(engine_gpu, b)
+    assert sum(ref.tasks["n"][:2 * b.n_wfs]) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("builder", [abi.BUILDER_LOCAL, abi.BUILDER_2DC, abi.BUILDER_NDC])
+def test_gpu_tasks_builders(engine_gpu, builder):
+    _check_tasks(engine_gpu, engine.synth_batch(0, 300, seed=51 + builder, builder=builder, error_rate=0.2))
+
+
+@pytest.mark.gpu
+def test_gpu_tasks_carry(engine_gpu):
+    """Tasks of a replay onto loaded state (ActivityTimeoutTask.Attempt from the row)."""
+    b = engine.synth_batch(3, 300, seed=61)
+    pre, cut = engine.split_batch(b, 2)
+    sb = engine.suffix_batch(b, cut, pre, engine_gpu.replay(pre))
+    _check_tasks(engine_gpu, sb)
+
+
+@pytest.mark.gpu
+def test_gpu_tasks_fixture_histories(engine_gpu):
+    """The hand-written KAT histories above, on the GPU."""
+    import oracle
+    hb = HistoryBuilder()
+    w = hb.workflow(workflow_id="wf", run_id="run", request_id="req")
+    w.calls = [[_started(backoff=60, cron=True), _dt_sched(2)],
+               [_ev(3, "DecisionTaskStarted", decisionTaskStartedEventAttributes={"scheduledEventId": 2})],
+               [_ev(4, "DecisionTaskTimedOut", decisionTaskTimedOutEventAttributes={
+                   "scheduledEventId": 2, "startedEventId": 3, "timeoutType": 0})]]
+    b = hb.build()
+    ref = oracle.replay(b, tasks=True)
+    got = engine_gpu.replay(b, tasks=True)
+    assert not engine.compare_tasks(b, got, ref)
+    assert _types(got.task_rows(0, "xfer")) == ["RecordWorkflowStarted", "DecisionTask", "DecisionTask"]
