@@ -269,6 +269,7 @@ def main():
     ap.add_argument("--no-stream-peak", action="store_true")
     ap.add_argument("--no-fast-path", action="store_true", help="replay every slice with the general kernel")
     ap.add_argument("--no-wave", action="store_true", help="no wave slices: divergent histories in lane slices")
+    ap.add_argument("--wave-all", action="store_true", help="every divergent history on a wave slice")
     args = ap.parse_args()
 
     import torch
@@ -290,7 +291,7 @@ def main():
     total = args.wfs * world
     mine, _ = assign_shards(total, world, rank)
     log(f"[rank {rank}] {len(mine)} of {total} workflows (shard->GPU greedy over {NUM_SHARDS} shards)")
-    db = DeviceBatch(torch, args.config, mine, args.seed, plan_mode=0 if args.no_wave else abi.PLAN_WAVE)
+    db = DeviceBatch(torch, args.config, mine, args.seed, plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0))
     log(f"[rank {rank}] {db.n_fast} of {db.info.n_slices} slices on the fast-path kernel, {db.n_wave} wave slices")
     log(f"[rank {rank}] packed {db.n_events:,} events in {db.pack_s:.2f}s (host SoA), H2D {db.h2d_s:.2f}s "
         f"({db.in_bytes / 1e9:.2f} GB in, {db.out_bytes / 1e9:.2f} GB out buffers)")

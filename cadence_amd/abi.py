@@ -200,6 +200,8 @@ SLICE_WAVE = 0x2
 CAP_FAST = 0x1
 CAP_WAVE = 0x2
 PLAN_WAVE = 0x1
+PLAN_WAVE_ALL = 0x2  # with PLAN_WAVE: lane-friendly (CAP_LANE) entries on the wave kernel too
+CAP_LANE = 0x4
 
 # slice-major slab of event columns (cdr.h enum cdr_col): name, dtype, in order
 SLAB_COLS = (("event_id", np.int64), ("version", np.int64), ("timestamp", np.int64), ("task_id", np.int64),

@@ -6,7 +6,10 @@
 // wavefront replays 64 workflows in lockstep with coalesced loads, and sizes the
 // per-workflow output regions the kernels write into.
 #include <algorithm>
+#include <cmath>
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <system_error>
@@ -155,7 +158,7 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   }
   c.vh_cap = vh;
   c.act_live = (uint32_t)live_max;
-  c.timer_live = c.timer_cap;
+  c.timer_live = (uint32_t)lv_max[0];  // peak live user timers: the kernels reuse freed slots first
   c.flags = (fast && live_max <= 1) ? CDR_CAP_FAST : 0u;
   const uint32_t W = CDR_WAVE_SLOTS;
   // the wave kernel keeps one slot per lane and reuses freed slots first, so its
@@ -163,6 +166,20 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   if (!(c.flags & CDR_CAP_FAST) && live_max <= (int64_t)W && lv_max[0] <= W && lv_max[1] <= W && lv_max[2] <= W &&
       lv_max[3] <= W)
     c.flags |= CDR_CAP_WAVE;
+  // small working sets and a moderate length: cheaper in a lane slice than on a wave of
+  // its own (the lane kernel's slot scans are short; the wave kernel pays its scalar
+  // per-event cost regardless) — measured on C3/C5 shapes, DESIGN.md §3
+  {
+    static const uint32_t* lim = [] {
+      static uint32_t v[4] = {CDR_LANE_MAX_ACT, CDR_LANE_MAX_TIMERS, CDR_LANE_MAX_EXT, CDR_LANE_MAX_LEN};
+      if (const char* e = std::getenv("CDR_LANE_MAX"))  // tuning override "act,timers,ext,len"
+        std::sscanf(e, "%u,%u,%u,%u", &v[0], &v[1], &v[2], &v[3]);
+      return v;
+    }();
+    if ((c.flags & CDR_CAP_WAVE) && live_max <= (int64_t)lim[0] && lv_max[0] <= lim[1] &&
+        lv_max[1] + lv_max[2] + lv_max[3] <= lim[2] && n <= lim[3])
+      c.flags |= CDR_CAP_LANE;
+  }
   *out = c;
 }
 
@@ -466,18 +483,36 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   std::vector<uint32_t> lanes, waves;
   lanes.reserve(n_wfs);
   for (uint32_t w = 0; w < n_wfs; w++)
-    ((mode & CDR_PLAN_WAVE) && (caps[w].flags & CDR_CAP_WAVE) ? waves : lanes).push_back(w);
+    ((mode & CDR_PLAN_WAVE) && (caps[w].flags & CDR_CAP_WAVE) &&
+             ((mode & CDR_PLAN_WAVE_ALL) || !(caps[w].flags & CDR_CAP_LANE))
+         ? waves
+         : lanes)
+        .push_back(w);
   // longest first: a slice's rows = its longest lane, so neighbours in length
   // share slices and padding stays small (SELL-C-sigma with sigma = batch); wave
   // slices longest first too, so the longest histories start first
   auto longer = [&](uint32_t a, uint32_t c) { return wfs[a].ev_len > wfs[c].ev_len; };
-  std::stable_sort(lanes.begin(), lanes.end(), longer);
+  // lane slices: within a length class (~4% wide, so padding stays small) order by the
+  // working-slot footprint, so that a slice's slot count (max over its lanes) is close
+  // to its lanes' own and more slices fit the LDS tier of the general kernel
+  auto lclass = [&](uint32_t a) { return (uint32_t)(std::log2((double)wfs[a].ev_len + 1.0) * 16.0); };
+  auto slots = [&](uint32_t a) { return caps ? caps[a].act_live * CDR_ACT_PLANES + caps[a].timer_live * CDR_TIM_PLANES : 0u; };
+  auto lane_order = [&](uint32_t a, uint32_t c) {
+    const uint32_t ka = lclass(a), kc = lclass(c);
+    if (ka != kc) return ka > kc;
+    const uint32_t sa = slots(a), sc = slots(c);
+    if (sa != sc) return sa > sc;
+    return wfs[a].ev_len > wfs[c].ev_len;
+  };
+  std::stable_sort(lanes.begin(), lanes.end(), lane_order);
   std::stable_sort(waves.begin(), waves.end(), longer);
   const uint32_t nl = (uint32_t)((lanes.size() + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
   const uint32_t nw = (uint32_t)waves.size();
   uint64_t rows = 0;
   for (uint32_t s = 0; s < nl; s++) {
-    const uint32_t len = (uint32_t)wfs[lanes[(size_t)s * CDR_SLICE_WIDTH]].ev_len;
+    uint32_t len = 0;  // the slice's longest lane
+    for (uint32_t l = 0; l < CDR_SLICE_WIDTH && (size_t)s * CDR_SLICE_WIDTH + l < lanes.size(); l++)
+      len = std::max(len, (uint32_t)wfs[lanes[(size_t)s * CDR_SLICE_WIDTH + l]].ev_len);
     if (slice_len) slice_len[s] = len;
     if (slice_row0) slice_row0[s] = rows;
     if (slice_flags) slice_flags[s] = 0;

@@ -1658,6 +1658,11 @@ struct cdr_ctx {
   // optional per-launch timing ring (bench): event pairs around every replay kernel
   std::vector<hipEvent_t> ring;
   uint32_t ring_used = 0;
+  // side stream for the wave kernel: its scalar-unit-bound waves co-run with the
+  // VALU-bound lane kernels instead of after them (fork/join by events)
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  int concurrent = 1;
 };
 
 #define HIPCHK(x)                                                                      \
@@ -1683,6 +1688,11 @@ cdr_ctx* cdr_create(int device) {
       return nullptr;
     }
   c->timed = false;
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess)
+    c->concurrent = 0;
+  if (const char* e = std::getenv("CDR_SERIAL_KERNELS")) c->concurrent = c->concurrent && e[0] == '0';
   return c;
 }
 
@@ -1705,6 +1715,9 @@ void cdr_destroy(cdr_ctx* c) {
   if (!c) return;
   for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
   for (hipEvent_t e : c->ring) (void)hipEventDestroy(e);
+  if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->fork) (void)hipEventDestroy(c->fork);
+  if (c->join) (void)hipEventDestroy(c->join);
   delete c;
 }
 
@@ -1732,7 +1745,18 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   if (blocks && fast)
     hipLaunchKernelGGL(k_replay_fast, dim3(blocks), dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, st, L);
   HIPCHK(hipGetLastError());
-  if (blocks && wave) hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
+  // the wave kernel on the side stream when lane slices also run: both kernels' waves
+  // share the CUs (wave slices: scalar unit; lane slices: VALU)
+  const bool fork = c->concurrent && blocks && wave && general;
+  if (fork) {
+    HIPCHK(hipEventRecord(c->fork, st));
+    HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
+    hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, c->side, L);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->join, c->side));
+  } else if (blocks && wave) {
+    hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
+  }
   HIPCHK(hipGetLastError());
   if (blocks && general) {
     if (tasks)
@@ -1748,6 +1772,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       hipLaunchKernelGGL((k_replay<false, false>), dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
   }
   HIPCHK(hipGetLastError());
+  if (fork) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used + 1] : c->ev[1], st));
   if (ring) {
     // keep ev[0..1] meaningful for cdr_last_kernel_ms as well

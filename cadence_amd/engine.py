@@ -288,6 +288,10 @@ class Engine:
         the previous setting."""
         return bool(abi.lib().cdr_set_plan_mode(self.ctx, abi.PLAN_WAVE if enable else 0))
 
+    def set_plan_mode(self, mode: int) -> int:
+        """CDR_PLAN_* bits of cdr_replay_batch's slicing; returns the previous mode."""
+        return int(abi.lib().cdr_set_plan_mode(self.ctx, mode))
+
     def set_fast_path(self, enable: bool) -> bool:
         """Route sequential-activity slices to the fast-path kernel (default) or replay
         everything with the general kernel; returns the previous setting."""

@@ -229,6 +229,9 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
  * marks it in slice_flags (nullable; the other slices get 0).  `caps` may be NULL
  * when mode is 0.  Returns the number of wave slices via *n_wave (nullable). */
 #define CDR_PLAN_WAVE 0x1u
+/* with CDR_PLAN_WAVE: also the CDR_CAP_LANE entries get wave slices (by default they
+ * stay in lane slices, where they replay cheaper) */
+#define CDR_PLAN_WAVE_ALL 0x2u
 int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
                        int32_t* lane_wf, uint32_t* slice_len, uint64_t* slice_row0, uint32_t* slice_flags,
                        uint32_t* n_slices, uint64_t* n_rows, uint32_t* n_wave);

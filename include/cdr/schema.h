@@ -536,6 +536,14 @@ typedef struct cdr_wf_caps {
  * activities, user timers, children, request-cancels and signals at any time; not
  * CDR_CAP_FAST */
 #define CDR_CAP_WAVE 0x2u
+/* a CDR_CAP_WAVE history small enough that a lane slice replays it cheaper
+ * (cdr_plan_slices_ex keeps it in the lane slices): peak live activities, user timers,
+ * children + request-cancels + signals and the event count within these bounds */
+#define CDR_CAP_LANE 0x4u
+#define CDR_LANE_MAX_ACT 6u
+#define CDR_LANE_MAX_TIMERS 10u
+#define CDR_LANE_MAX_EXT 8u
+#define CDR_LANE_MAX_LEN 512u
 #define CDR_WAVE_SLOTS 64u
 
 typedef struct cdr_totals {

@@ -178,13 +178,14 @@ def test_wave_slices_plan_and_pack():
     pl = engine.plan(b)
     L = abi.lib()
     ns, rows, nw = C.c_uint32(), C.c_uint64(), C.c_uint32()
-    L.cdr_plan_slices_ex(b.wfs, pl.caps, b.n_wfs, abi.PLAN_WAVE, None, None, None, None, C.byref(ns),
+    mode = abi.PLAN_WAVE | abi.PLAN_WAVE_ALL  # also the lane-friendly (CAP_LANE) entries
+    L.cdr_plan_slices_ex(b.wfs, pl.caps, b.n_wfs, mode, None, None, None, None, C.byref(ns),
                          C.byref(rows), C.byref(nw))
     lane = np.zeros(ns.value * 64, np.int32)
     slen = np.zeros(ns.value, np.uint32)
     row0 = np.zeros(ns.value, np.uint64)
     flags = np.zeros(ns.value, np.uint32)
-    L.cdr_plan_slices_ex(b.wfs, pl.caps, b.n_wfs, abi.PLAN_WAVE, lane.ctypes.data, slen.ctypes.data,
+    L.cdr_plan_slices_ex(b.wfs, pl.caps, b.n_wfs, mode, lane.ctypes.data, slen.ctypes.data,
                          row0.ctypes.data, flags.ctypes.data, C.byref(ns), C.byref(rows), C.byref(nw))
     waves = np.nonzero(flags & abi.SLICE_WAVE)[0]
     assert len(waves) == nw.value > 0
@@ -221,3 +222,18 @@ def test_wave_slices_plan_and_pack():
     tf = cols["type_flags"][r0 * 64:(r0 + int(slen[s])) * 64]
     assert [int(x) & 0xFF for x in tf[:n]] == [b.events[d.ev_off + k].type for k in range(n)]
     assert all((int(x) & 0xFF) == 0xFF for x in tf[n:])
+
+
+def test_lane_friendly_entries_stay_in_lane_slices():
+    """CDR_CAP_LANE (small working sets, moderate length) keeps a divergent history in a
+    lane slice under CDR_PLAN_WAVE; PLAN_WAVE_ALL sends it to a wave slice."""
+    b = engine.synth_batch(3, 300, seed=12)
+    pl = engine.plan(b)
+    lane_ok = [w for w in range(b.n_wfs) if pl.caps[w].flags & abi.CAP_LANE]
+    assert lane_ok and all(pl.caps[w].flags & abi.CAP_WAVE for w in lane_ok)
+    for w in lane_ok:
+        c = pl.caps[w]
+        assert c.act_live <= 6 and c.timer_live <= 10 and b.wfs[w].ev_len <= 512
+    n_all = engine.slice_kinds(b, pl, abi.PLAN_WAVE | abi.PLAN_WAVE_ALL)[1]
+    n_def = engine.slice_kinds(b, pl, abi.PLAN_WAVE)[1]
+    assert n_def == n_all - len(lane_ok)

@@ -21,6 +21,13 @@ def _check(batch, eng, both_paths=False, lanes=True):
     got = eng.replay(batch)
     bad = engine.compare(batch, got, ref)
     assert not bad, "default routing: " + "\n".join(bad[:10])
+    old = eng.set_plan_mode(abi.PLAN_WAVE | abi.PLAN_WAVE_ALL)  # every divergent history on a wave
+    try:
+        got = eng.replay(batch)
+    finally:
+        eng.set_plan_mode(old)
+    bad = engine.compare(batch, got, ref)
+    assert not bad, "all divergent on the wave kernel: " + "\n".join(bad[:10])
     if lanes:
         old = eng.set_wave(False)
         try:
@@ -45,7 +52,7 @@ def _check(batch, eng, both_paths=False, lanes=True):
 def test_synth_configs_clean(engine_gpu, cfg):
     b = engine.synth_batch(cfg, 300, seed=0x5EED0000 + cfg)
     if cfg in (3, 4, 5, 0):  # divergent shapes: the wave kernel must be exercised
-        assert engine.slice_kinds(b)[1] > 0
+        assert engine.slice_kinds(b, mode=abi.PLAN_WAVE | abi.PLAN_WAVE_ALL)[1] > 0
     ref = _check(b, engine_gpu)
     assert engine.status_histogram(ref).get("OK", 0) > 0
 
@@ -80,7 +87,7 @@ def test_wave_kernel_configs(engine_gpu, cfg):
     """Larger divergent batches (every entry that fits the wave kernel gets a wave
     slice), checked against the oracle only."""
     b = engine.synth_batch(cfg, 1500, seed=0x5EED0100 + cfg, error_rate=0.1)
-    nf, nw, ns = engine.slice_kinds(b)
+    nf, nw, ns = engine.slice_kinds(b, mode=abi.PLAN_WAVE | abi.PLAN_WAVE_ALL)
     assert nw > 0, (nf, nw, ns)
     _check(b, engine_gpu, lanes=False)
 
@@ -150,7 +157,7 @@ def test_wave_kernel_table_overflow(engine_gpu, n):
     for j, bld in enumerate([abi.BUILDER_NDC, abi.BUILDER_2DC, abi.BUILDER_LOCAL]):
         _overflow_history(hb, f"wf-{j}", n, n, bld)
     b = hb.build()
-    nf, nw, ns = engine.slice_kinds(b)
+    nf, nw, ns = engine.slice_kinds(b, mode=abi.PLAN_WAVE | abi.PLAN_WAVE_ALL)
     assert nw == 3, (nf, nw, ns)
     ref = _check(b, engine_gpu)
     assert engine.status_histogram(ref) == {"OK": 3}
