@@ -289,6 +289,11 @@ static_assert(TP_VER + 1 == CDR_TIM_PLANES, "timer planes");
 #define AF_CANCEL 0x4ull
 #define META_FLAG(f) ((f) << 32)
 #define META_TTS_SHIFT 40
+// event types whose replay only updates registers (one shared dispatch pass)
+#define SIMPLE_TYPES                                                                                         \
+  (CDR_TB(CDR_EV_WF_SIGNALED) | CDR_TB(CDR_EV_DT_SCHEDULED) | CDR_TB(CDR_EV_DT_STARTED) |                    \
+   CDR_TB(CDR_EV_MARKER_RECORDED) | CDR_TB(CDR_EV_CANCEL_TIMER_FAILED) | CDR_TB(CDR_EV_AT_REQ_CANCEL_FAILED) | \
+   CDR_TB(CDR_EV_WF_CANCEL_REQUESTED))
 #define AP_CARRIED ((int64_t)1 << 62) /* AP_ROWS: row j of the loaded activity table (cdr_carry) */
 
 extern __shared__ uint64_t cdr_lds[];
@@ -846,8 +851,38 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     for (uint64_t pend = __builtin_amdgcn_ballot_w64(go); pend;) {
       uint32_t ut = __builtin_amdgcn_readlane(type, __builtin_ctzll(pend));
       asm volatile("" : "+s"(ut));  // keep the switch on the SGPR copy
-      const bool mine = go && type == ut;
+      // register-only types (signals, the decision schedule/start, no-ops, cancel
+      // request) share one pass: each lane applies its own type's selects
+      const bool simple = ((SIMPLE_TYPES >> ut) & 1ull) != 0;
+      const bool mine = go && (simple ? ((SIMPLE_TYPES >> type) & 1ull) != 0 : type == ut);
       pend &= ~__builtin_amdgcn_ballot_w64(mine);
+      if (simple) {
+        const bool ms = mine && type == CDR_EV_DT_SCHEDULED;  // :186-200 -> :143-167
+        dv = SEL(ms, e.ver, dv);
+        dsched = SEL(ms, e.id, dsched);
+        dstart = SEL(ms, CDR_EMPTY_EVENT_ID, dstart);
+        dreq = SEL(ms, EU, dreq);
+        dto = SEL(ms, e.n, dto);
+        datt = SEL(ms, e.aux, datt);
+        dsc_ts = SEL(ms, e.ts, dsc_ts);
+        dst_ts = SEL(ms, (int64_t)0, dst_ts);
+        dorig_ts = SEL(ms, e.ts, dorig_ts);
+        task_x(TK && ms, CDR_TT_DECISION, e.id, D.domain_id, task_list_now(), 0, 0, 0);  // :196-197
+        const bool mt = mine && type == CDR_EV_DT_STARTED;  // :202-213 -> :200-253
+        const bool f = mt && e.key != dsched;
+        PFAIL(f, CDR_E_DECISION_NOT_FOUND);
+        const bool ok = mt && !f;
+        x_state = SEL(ok && x_state == CDR_STATE_CREATED, (int32_t)CDR_STATE_RUNNING, x_state);  // (:56-60)
+        dv = SEL(ok, e.ver, dv);
+        dstart = SEL(ok, e.id, dstart);
+        dreq = SEL(ok, e.h, dreq);
+        datt = SEL(ok, (int64_t)0, datt);
+        dst_ts = SEL(ok, e.ts, dst_ts);
+        task_t(TK && ok, CDR_TT_DECISION_TIMEOUT, CDR_TIMEOUT_START_TO_CLOSE, e.key, e.ts + (int64_t)dto * NS_PER_S, 0);
+        x_signals += (mine && type == CDR_EV_WF_SIGNALED) ? 1 : 0;                           // :473-476
+        x_flags |= (mine && type == CDR_EV_WF_CANCEL_REQUESTED) ? CDR_XI_CANCEL_REQUESTED : 0u;  // :478-481
+        continue;  // MarkerRecorded, CancelTimerFailed, RequestCancelActivityTaskFailed: no-ops
+      }
       switch (ut) {
         case CDR_EV_WF_STARTED: {  // stateBuilder.go:158-184 -> mutableStateBuilder.go:1639-1716
           // every lane reads a valid record (the first one for lanes of other types)
