@@ -50,7 +50,8 @@ STATUS = {
     4: "E_INVALID_STATE_TRANSITION", 5: "E_VH_LOWER_VERSION", 6: "E_VH_LOWER_EVENT_ID",
     7: "E_DECISION_NOT_FOUND", 8: "E_ACTIVITY_NOT_FOUND", 9: "E_ACTIVITY_ID_NOT_FOUND",
     10: "E_MISSING_ACTIVITY_INFO", 11: "E_DOMAIN_NOT_FOUND", 12: "E_REBUILD_NEXT_EVENT_ID",
-    13: "E_BAD_INPUT", 32: "P_ACTIVITY_STARTED_NIL", 33: "P_CHILD_STARTED_NIL",
+    13: "E_BAD_INPUT", 14: "E_REFRESH_EVENT_NOT_FOUND", 15: "E_REFRESH_BACKOFF_INITIATOR",
+    16: "E_REFRESH_CAPACITY", 32: "P_ACTIVITY_STARTED_NIL", 33: "P_CHILD_STARTED_NIL",
     34: "P_VH_ITEM_INVALID", 35: "P_UNKNOWN_CLUSTER", 64: "NOT_APPLIED",
 }
 OK = 0
@@ -59,6 +60,8 @@ RF_IN_NEWRUN, RF_IS_NEWRUN, RF_NEWRUN_APPLIED = 1, 2, 4
 SF_HAS_PARENT_DOMAIN, SF_PARENT_DOMAIN_MISSING, SF_HAS_PARENT_EXEC = 0x1, 0x2, 0x4
 SF_HAS_PARENT_INITIATED, SF_HAS_RETRY, SF_HAS_MEMO, SF_HAS_SEARCH_ATTR = 0x8, 0x10, 0x20, 0x40
 SF_HAS_RESET_POINTS, SF_CRON_INITIATOR = 0x80, 0x100
+SF_HAS_INITIATOR, SF_RETRY_INITIATOR, SF_DECIDER_INITIATOR = 0x200, 0x400, 0x800
+REFRESH_ADVANCED_VISIBILITY = 0x1
 AF_HAS_RETRY = 0x1
 XF_DOMAIN_MISSING, XF_CHILD_ONLY = 0x1, 0x2
 RP_HAS_CHECKSUM, RP_HAS_RUN_ID, RP_HAS_FIRST_DC_ID, RP_HAS_CREATED = 0x1, 0x2, 0x4, 0x8
@@ -184,7 +187,8 @@ CdrOut = _S("cdr_out", [(n, C.c_void_p) for n in (
     "timer_tasks", "n_tasks")])
 CdrTask = _S("cdr_task", [("type", u32), ("timeout_type", i32), ("event_id", i64), ("visibility_ts", i64),
                           ("attempt", i64), ("domain_id", u32), ("task_list", u32), ("target_workflow_id", u32),
-                          ("target_run_id", u32), ("flags", u32), ("_pad", u32)])
+                          ("target_run_id", u32), ("flags", u32), ("_pad", u32),
+                          ("version", i64)])
 TASK_TYPES = {0: "DecisionTask", 1: "ActivityTask", 2: "CloseExecution", 3: "CancelExecution",
               4: "StartChildExecution", 5: "SignalExecution", 6: "RecordWorkflowStarted",
               8: "UpsertWorkflowSearchAttributes", 16: "DecisionTimeout", 17: "ActivityTimeout", 18: "UserTimer",
@@ -272,6 +276,10 @@ EXPORTS = {
     "cdr_replay_sliced_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p]),
     "cdr_replay_batch": (i32, [C.c_void_p, C.POINTER(CdrBatch), C.POINTER(CdrWfCaps), C.POINTER(CdrTotals),
                                C.POINTER(CdrOut)]),
+    "cdr_refresh_tasks_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), i64, u32,
+                                      C.c_void_p]),
+    "cdr_rebuild_batch": (i32, [C.c_void_p, C.POINTER(CdrBatch), C.POINTER(CdrWfCaps), C.POINTER(CdrTotals),
+                                C.POINTER(CdrOut), u32]),
     "cdr_compact_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
                                 C.c_void_p, C.c_void_p]),
     "cdr_checksum_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p, C.c_void_p]),

@@ -126,6 +126,9 @@ int dmalloc(T** p, uint64_t n) {
 
 }  // namespace
 
+static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot,
+                       cdr_out* out, bool refresh, uint32_t rflags);
+
 extern "C" {
 
 int cdr_compact_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out, void* dense,
@@ -174,11 +177,27 @@ int cdr_checksum_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out
 }
 
 int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot, cdr_out* out) {
+  return replay_host(ctx, b, caps, tot, out, false, 0);
+}
+
+int cdr_rebuild_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot, cdr_out* out,
+                      uint32_t flags) {
+  if (!out || !out->transfer || !out->timer_tasks || !out->n_tasks) return CDR_API_EINVAL;
+  return replay_host(ctx, b, caps, tot, out, true, flags);
+}
+
+}  // extern "C"
+
+// plan + pack + H2D + replay (+ refreshTasks) + D2H
+static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot,
+                       cdr_out* out, bool refresh, uint32_t rflags) {
   if (!ctx || !b || !caps || !tot || !out) return CDR_API_EINVAL;
   // ---- plan + pack on the host
   uint32_t ns = 0, n_wave = 0;
   uint64_t rows = 0;
-  const bool tasks = out->transfer != nullptr;  // emitted by the general kernel only: no wave slices
+  // stateBuilder task lists are emitted by the general kernel only (no wave slices);
+  // the refresher's come from their own kernel after any replay
+  const bool tasks = out->transfer != nullptr && !refresh;
   const uint32_t mode = tasks ? 0u : cdr_get_plan_mode(ctx);
   int rc = cdr_plan_slices_ex(b->wfs, caps, b->n_wfs, mode, nullptr, nullptr, nullptr, nullptr, &ns, &rows, &n_wave);
   if (rc) return rc;
@@ -292,7 +311,7 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   dout.signal = (cdr_signal_info*)dz(tot->signal * sizeof(cdr_signal_info));
   dout.rp = (cdr_reset_point*)dz(tot->rp * sizeof(cdr_reset_point));
   dout.sa = (cdr_kv*)dz(tot->sa * sizeof(cdr_kv));
-  if (tasks) {
+  if (tasks || refresh) {
     dout.transfer = (cdr_task*)dz(tot->xfer * sizeof(cdr_task));
     dout.timer_tasks = (cdr_task*)dz(tot->ttask * sizeof(cdr_task));
     dout.n_tasks = (uint32_t*)dz((uint64_t)b->n_wfs * 2 * sizeof(uint32_t));
@@ -302,7 +321,15 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
       free_all();
       return CDR_API_ENOMEM;
     }
-  rc = cdr_replay_sliced_async(ctx, &db, &dout, nullptr);
+  if (refresh) {  // the replay itself emits no stateBuilder tasks
+    cdr_out rout = dout;
+    rout.transfer = rout.timer_tasks = nullptr;
+    rout.n_tasks = nullptr;
+    rc = cdr_replay_sliced_async(ctx, &db, &rout, nullptr);
+    if (rc == CDR_API_OK) rc = cdr_refresh_tasks_async(ctx, &db, &dout, b->now_ns, rflags, nullptr);
+  } else {
+    rc = cdr_replay_sliced_async(ctx, &db, &dout, nullptr);
+  }
   if (rc == CDR_API_OK && hipDeviceSynchronize() != hipSuccess) rc = CDR_API_EDEVICE;
   auto down = [&](void* dst, const void* src, uint64_t bytes) {
     if (rc == CDR_API_OK && dst && bytes && hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) != hipSuccess)
@@ -319,7 +346,7 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   down(out->signal, dout.signal, tot->signal * sizeof(cdr_signal_info));
   down(out->rp, dout.rp, tot->rp * sizeof(cdr_reset_point));
   down(out->sa, dout.sa, tot->sa * sizeof(cdr_kv));
-  if (tasks) {
+  if (tasks || refresh) {
     down(out->transfer, dout.transfer, tot->xfer * sizeof(cdr_task));
     down(out->timer_tasks, dout.timer_tasks, tot->ttask * sizeof(cdr_task));
     down(out->n_tasks, dout.n_tasks, (uint64_t)b->n_wfs * 2 * sizeof(uint32_t));
@@ -327,5 +354,3 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
   free_all();
   return rc;
 }
-
-}  // extern "C"

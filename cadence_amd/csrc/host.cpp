@@ -228,7 +228,11 @@ void task_caps(const cdr_event* ev, uint64_t n, uint32_t* xfer, uint32_t* ttask)
         break;
     }
   }
-  *xfer = x;
+  // refreshTasks (mutableStateTaskRefresher.go:66-160) writes into the same slices: its
+  // transfer tasks are bounded by the same events plus one UpsertWorkflowSearchAttributes
+  // task; its timer tasks (at most one per kind) by Started's two, a close event's, a
+  // DecisionTaskStarted's, an ActivityTaskScheduled's and a TimerStarted's
+  *xfer = x + 1;
   *ttask = t;
 }
 

@@ -236,9 +236,13 @@ class Outputs:
         self.tables = {t: (TABLE_TYPES[t] * max(1, getattr(pl.totals, t)))() for t in TABLES}
         self.tasks = None
         if tasks:  # stateBuilder transfer / timer task lists (cdr_task)
-            self.tasks = {"xfer": (abi.CdrTask * max(1, pl.totals.xfer))(),
-                          "ttask": (abi.CdrTask * max(1, pl.totals.ttask))(),
-                          "n": (C.c_uint32 * (2 * n))()}
+            self.alloc_tasks(pl)
+
+    def alloc_tasks(self, pl: Plan):
+        """(Re)allocate zeroed task lists (cdr_task) sized by the plan's totals."""
+        self.tasks = {"xfer": (abi.CdrTask * max(1, pl.totals.xfer))(),
+                      "ttask": (abi.CdrTask * max(1, pl.totals.ttask))(),
+                      "n": (C.c_uint32 * (2 * max(1, self.n_wfs)))()}
 
     def cstruct(self) -> abi.CdrOut:
         o = abi.CdrOut()
@@ -317,6 +321,19 @@ class Engine:
                                        C.byref(out.cstruct()))
         if rc:
             raise RuntimeError(f"cdr_replay_batch rc={rc}")
+        return out
+
+    def rebuild(self, batch: Batch, pl: Plan | None = None, advanced_visibility: bool = True) -> Outputs:
+        """nDCStateRebuilder.rebuild's device half through cdr_rebuild_batch: replay
+        (every kernel) then refreshTasks (refresh.hip) with now = batch.now_ns; the
+        task lists are the refresher's."""
+        pl = pl or plan(batch)
+        out = Outputs(batch, pl, tasks=True)
+        flags = abi.REFRESH_ADVANCED_VISIBILITY if advanced_visibility else 0
+        rc = abi.lib().cdr_rebuild_batch(self.ctx, C.byref(batch.cstruct()), pl.caps, C.byref(pl.totals),
+                                        C.byref(out.cstruct()), flags)
+        if rc:
+            raise RuntimeError(f"cdr_rebuild_batch rc={rc}")
         return out
 
 

@@ -94,7 +94,8 @@ class HistoryBuilder:
             s.cron_schedule = I(x.get("cronSchedule", ""))
             s.attempt = int(x.get("attempt", 0))
             s.first_decision_backoff_s = int(x.get("firstDecisionTaskBackoffSeconds", 0))
-            cron_init = x.get("initiator") in ("CronSchedule", "CRON_SCHEDULE", 2)  # ContinueAsNewInitiator
+            init = x.get("initiator")  # ContinueAsNewInitiator: Decider 0, RetryPolicy 1, CronSchedule 2
+            cron_init = init in ("CronSchedule", "CRON_SCHEDULE", 2)
             s.expiration_ts = int(x.get("expirationTimestamp", 0))
             f = 0
             if x.get("parentWorkflowDomain") is not None:
@@ -112,6 +113,12 @@ class HistoryBuilder:
                 s.parent_initiated_id = int(x["parentInitiatedEventId"])
             if cron_init:
                 f |= abi.SF_CRON_INITIATOR
+            if init is not None:
+                f |= abi.SF_HAS_INITIATOR
+                if init in ("RetryPolicy", "RETRY_POLICY", 1):
+                    f |= abi.SF_RETRY_INITIATOR
+                elif init in ("Decider", "DECIDER", 0):
+                    f |= abi.SF_DECIDER_INITIATOR
             rp = x.get("retryPolicy")
             if rp is not None:
                 f |= abi.SF_HAS_RETRY

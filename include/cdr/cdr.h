@@ -13,6 +13,10 @@
  *     -> cdr_create / cdr_destroy (one context per goroutine-equivalent / stream)
  *   nDCStateRebuilder.rebuild batch loop service/history/nDCStateRebuilder.go:92-160
  *     -> cdr_replay_batch with cdr_wf_desc.expected_next_event_id set
+ *   mutableStateTaskRefresher.refreshTasks (after nDCStateRebuilder.rebuild's replay)
+ *                                       service/history/mutableStateTaskRefresher.go:66-160
+ *                                       service/history/nDCStateRebuilder.go:154-157
+ *     -> cdr_refresh_tasks_async (device-resident) / cdr_rebuild_batch (host buffers)
  *   common.WorkflowIDToHistoryShard     common/util.go:249-252
  *     -> cdr_workflow_id_to_shard (farmhash Fingerprint32 % numShards)
  *
@@ -277,6 +281,30 @@ int cdr_replay_sliced_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out
  * buffers sized by its totals.  Synchronous. */
 int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* totals,
                      cdr_out* out);
+
+/* refreshTasks (mutableStateTaskRefresher.go:66-160) over the rebuilt states of a
+ * replay: run after cdr_replay_sliced_async on the same `in` / `out` (same stream).
+ * For every entry whose result is CDR_OK it regenerates the transfer and timer tasks
+ * of the rebuilt state at time `now_ns` into out->transfer / out->timer_tasks (the
+ * entry's caps.xfer_off / ttask_off slices, counts in out->n_tasks — the stateBuilder
+ * lists, if any, are replaced), clears every pending activity's TimerTaskStatus and
+ * every user timer's TaskID and sets the ones the activity / user-timer picks created
+ * (:264-342).  Events the refresher reads (WorkflowExecutionStarted, the scheduled /
+ * initiated events of pending entities — the reference's events cache) are looked up
+ * among the entry's own events in `in`; a miss, a Decider initiator with a first-decision
+ * backoff, an unknown target domain or an overflowing task slice set the entry's
+ * result.code (CDR_E_REFRESH_*, CDR_E_DOMAIN_NOT_FOUND) and leave its tables unchanged
+ * with no tasks.  `flags`: CDR_REFRESH_ADVANCED_VISIBILITY adds the
+ * UpsertWorkflowSearchAttributes task (:148-156).  Asynchronous. */
+#define CDR_REFRESH_ADVANCED_VISIBILITY 0x1u
+int cdr_refresh_tasks_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, int64_t now_ns,
+                            uint32_t flags, void* stream);
+
+/* nDCStateRebuilder.rebuild's replay + refreshTasks for host-resident data: as
+ * cdr_replay_batch, then cdr_refresh_tasks_async at b->now_ns.  out->transfer,
+ * timer_tasks and n_tasks are required (sized by `totals`).  Synchronous. */
+int cdr_rebuild_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* totals,
+                      cdr_out* out, uint32_t flags);
 
 /* Stream compaction of the per-workflow pending tables into dense tables
  * (device pointers): for each table, rows [caps.off, caps.off + result.n) of every

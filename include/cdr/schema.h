@@ -156,6 +156,12 @@ enum cdr_status {
   CDR_E_DOMAIN_NOT_FOUND = 11,      /* domain cache lookups stateBuilder.go:162,365,417,448 */
   CDR_E_REBUILD_NEXT_EVENT_ID = 12, /* nDCStateRebuilder.go:139-143 */
   CDR_E_BAD_INPUT = 13,             /* malformed batch (host validation) */
+  /* refreshTasks (cdr_refresh_tasks_async; mutableStateTaskRefresher.go:66-160) */
+  CDR_E_REFRESH_EVENT_NOT_FOUND = 14, /* GetStartEvent / eventsCache.getEvent miss: the event is not
+                                         among the entry's own events (e.g. a carried-in entry) */
+  CDR_E_REFRESH_BACKOFF_INITIATOR = 15, /* generateDelayedDecisionTasks InternalServiceError
+                                           mutableStateTaskGenerator.go:197-205 */
+  CDR_E_REFRESH_CAPACITY = 16,      /* task slice of the entry too small (caller sized it) */
   CDR_P_ACTIVITY_STARTED_NIL = 32,  /* nil deref mutableStateBuilder.go:2089-2091 */
   CDR_P_CHILD_STARTED_NIL = 33,     /* nil deref mutableStateBuilder.go:3319-3320 */
   CDR_P_VH_ITEM_INVALID = 34,       /* NewVersionHistoryItem panic versionHistory.go:36-42 */
@@ -229,6 +235,9 @@ typedef struct cdr_reset_point { /* shared.ResetPointInfo */
 #define CDR_SF_HAS_SEARCH_ATTR 0x040u      /* SearchAttributes != nil */
 #define CDR_SF_HAS_RESET_POINTS 0x080u     /* PrevAutoResetPoints != nil && Points != nil */
 #define CDR_SF_CRON_INITIATOR 0x100u       /* Initiator == CronSchedule (tasks only) */
+#define CDR_SF_HAS_INITIATOR 0x200u        /* Initiator != nil (refreshTasks only) */
+#define CDR_SF_RETRY_INITIATOR 0x400u      /* Initiator == RetryPolicy (refreshTasks only) */
+#define CDR_SF_DECIDER_INITIATOR 0x800u    /* Initiator == Decider (refreshTasks only) */
 typedef struct cdr_attr_wf_started {
   uint32_t workflow_type, task_list, cron_schedule, flags;
   uint32_t parent_domain_id, parent_workflow_id, parent_run_id, continued_run_id;
@@ -503,7 +512,13 @@ typedef struct cdr_task {
   uint32_t domain_id, task_list; /* handles: DomainID or TargetDomainID; TaskList */
   uint32_t target_workflow_id, target_run_id;
   uint32_t flags, _pad; /* CDR_TF_* */
+  /* Version: set by refreshTasks (mutableStateTaskGenerator.go); stateBuilder's tasks
+   * leave it to the caller (0) */
+  int64_t version;
 } cdr_task;
+#ifdef __cplusplus
+static_assert(sizeof(cdr_task) == 64, "cdr_task");
+#endif
 
 /* per-workflow result: status + where each variable-length table lives */
 typedef struct cdr_wf_result {

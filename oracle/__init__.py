@@ -28,6 +28,9 @@ def lib():
         L.cdro_replay_batch.restype = C.c_int
         L.cdro_replay_batch.argtypes = [C.POINTER(abi.CdrBatch), C.POINTER(abi.CdrWfCaps), C.POINTER(abi.CdrOut),
                                         C.c_int]
+        L.cdro_refresh_tasks.restype = C.c_int
+        L.cdro_refresh_tasks.argtypes = [C.POINTER(abi.CdrBatch), C.POINTER(abi.CdrWfCaps), C.POINTER(abi.CdrOut),
+                                         C.c_int64, C.c_uint32]
         L.cdro_vh_add_or_update.restype = C.c_int
         L.cdro_vh_add_or_update.argtypes = [C.POINTER(abi.CdrVHItem), C.POINTER(C.c_uint32), C.c_uint32,
                                             C.c_int64, C.c_int64]
@@ -46,4 +49,19 @@ def replay(batch, pl=None, threads: int = 1, tasks: bool = False):
     rc = lib().cdro_replay_batch(C.byref(batch.cstruct()), pl.caps, C.byref(out.cstruct()), threads)
     if rc:
         raise RuntimeError(f"cdro_replay_batch rc={rc}")
+    return out
+
+
+def rebuild(batch, pl=None, advanced_visibility: bool = True):
+    """Oracle of nDCStateRebuilder's replay + refreshTasks (refresh_ref.cpp): the
+    rebuilt state with the refresher's task lists (now = batch.now_ns)."""
+    from cadence_amd import abi, engine
+    pl = pl or engine.plan(batch)
+    out = replay(batch, pl)
+    out.alloc_tasks(pl)
+    flags = abi.REFRESH_ADVANCED_VISIBILITY if advanced_visibility else 0
+    bs = batch.cstruct()
+    rc = lib().cdro_refresh_tasks(C.byref(bs), pl.caps, C.byref(out.cstruct()), bs.now_ns, flags)
+    if rc:
+        raise RuntimeError(f"cdro_refresh_tasks rc={rc}")
     return out
