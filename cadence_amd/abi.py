@@ -61,7 +61,7 @@ SF_HAS_PARENT_DOMAIN, SF_PARENT_DOMAIN_MISSING, SF_HAS_PARENT_EXEC = 0x1, 0x2, 0
 SF_HAS_PARENT_INITIATED, SF_HAS_RETRY, SF_HAS_MEMO, SF_HAS_SEARCH_ATTR = 0x8, 0x10, 0x20, 0x40
 SF_HAS_RESET_POINTS, SF_CRON_INITIATOR = 0x80, 0x100
 SF_HAS_INITIATOR, SF_RETRY_INITIATOR, SF_DECIDER_INITIATOR = 0x200, 0x400, 0x800
-REFRESH_ADVANCED_VISIBILITY = 0x1
+REFRESH_ADVANCED_VISIBILITY, REFRESH_SNAPSHOT_PASSIVE = 0x1, 0x2
 AF_HAS_RETRY = 0x1
 XF_DOMAIN_MISSING, XF_CHILD_ONLY = 0x1, 0x2
 RP_HAS_CHECKSUM, RP_HAS_RUN_ID, RP_HAS_FIRST_DC_ID, RP_HAS_CREATED = 0x1, 0x2, 0x4, 0x8

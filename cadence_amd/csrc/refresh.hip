@@ -124,9 +124,9 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
   int32_t code = CDR_OK;
   int best = -1, head = -1;
   int32_t best_bit = 0;
+  // GetCurrentVersion (mutableStateBuilder.go:491-502) of the rebuilt in-memory state
+  int64_t curVer = CDR_EMPTY_VERSION;
   do {
-    // GetCurrentVersion (mutableStateBuilder.go:491-502) of the rebuilt in-memory state
-    int64_t curVer = CDR_EMPTY_VERSION;
     if (d.builder == CDR_BUILDER_2DC) {
       curVer = O.repl[w].current_version;
     } else if (d.builder == CDR_BUILDER_NDC && E.n > 0) {
@@ -301,6 +301,10 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
   }
   O.n_tasks[2 * (uint64_t)w] = nx;
   O.n_tasks[2 * (uint64_t)w + 1] = nt;
+  if (flags & CDR_REFRESH_SNAPSHOT_PASSIVE) {  // setTaskInfo (historyEngine.go:2383-2397)
+    for (uint32_t j = 0; j < nx; j++) XT[j].version = curVer;
+    for (uint32_t j = 0; j < nt; j++) TT[j].version = curVer;
+  }
   // the refreshed masks: every status / TaskID cleared, the picks' set
   cdr_activity_info* act = O.act + cp.act_off;
   for (uint32_t j = 0; j < r.n_activity; j++) act[j].timer_task_status = (int)j == best ? best_bit : 0;

@@ -323,13 +323,14 @@ class Engine:
             raise RuntimeError(f"cdr_replay_batch rc={rc}")
         return out
 
-    def rebuild(self, batch: Batch, pl: Plan | None = None, advanced_visibility: bool = True) -> Outputs:
+    def rebuild(self, batch: Batch, pl: Plan | None = None, advanced_visibility: bool = True, snapshot: bool = False) -> Outputs:
         """nDCStateRebuilder.rebuild's device half through cdr_rebuild_batch: replay
         (every kernel) then refreshTasks (refresh.hip) with now = batch.now_ns; the
         task lists are the refresher's."""
         pl = pl or plan(batch)
         out = Outputs(batch, pl, tasks=True)
-        flags = abi.REFRESH_ADVANCED_VISIBILITY if advanced_visibility else 0
+        flags = (abi.REFRESH_ADVANCED_VISIBILITY if advanced_visibility else 0) | (
+        abi.REFRESH_SNAPSHOT_PASSIVE if snapshot else 0)
         rc = abi.lib().cdr_rebuild_batch(self.ctx, C.byref(batch.cstruct()), pl.caps, C.byref(pl.totals),
                                         C.byref(out.cstruct()), flags)
         if rc:

@@ -295,8 +295,15 @@ int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, 
  * backoff, an unknown target domain or an overflowing task slice set the entry's
  * result.code (CDR_E_REFRESH_*, CDR_E_DOMAIN_NOT_FOUND) and leave its tables unchanged
  * with no tasks.  `flags`: CDR_REFRESH_ADVANCED_VISIBILITY adds the
- * UpsertWorkflowSearchAttributes task (:148-156).  Asynchronous. */
+ * UpsertWorkflowSearchAttributes task (:148-156); CDR_REFRESH_SNAPSHOT_PASSIVE below.
+ * Asynchronous. */
 #define CDR_REFRESH_ADVANCED_VISIBILITY 0x1u
+/* then CloseTransactionAsSnapshot(now, transactionPolicyPassive)
+ * (mutableStateBuilder.go:3787-3855): with the passive policy and no new events its only
+ * effect on the outputs is setTaskInfo (historyEngine.go:2383-2397) — every task's Version
+ * becomes GetCurrentVersion() (LastUpdatedTimestamp = now is the caller's: the record
+ * omits it) */
+#define CDR_REFRESH_SNAPSHOT_PASSIVE 0x2u
 int cdr_refresh_tasks_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, int64_t now_ns,
                             uint32_t flags, void* stream);
 

@@ -52,14 +52,15 @@ def replay(batch, pl=None, threads: int = 1, tasks: bool = False):
     return out
 
 
-def rebuild(batch, pl=None, advanced_visibility: bool = True):
+def rebuild(batch, pl=None, advanced_visibility: bool = True, snapshot: bool = False):
     """Oracle of nDCStateRebuilder's replay + refreshTasks (refresh_ref.cpp): the
     rebuilt state with the refresher's task lists (now = batch.now_ns)."""
     from cadence_amd import abi, engine
     pl = pl or engine.plan(batch)
     out = replay(batch, pl)
     out.alloc_tasks(pl)
-    flags = abi.REFRESH_ADVANCED_VISIBILITY if advanced_visibility else 0
+    flags = (abi.REFRESH_ADVANCED_VISIBILITY if advanced_visibility else 0) | (
+        abi.REFRESH_SNAPSHOT_PASSIVE if snapshot else 0)
     bs = batch.cstruct()
     rc = lib().cdro_refresh_tasks(C.byref(bs), pl.caps, C.byref(out.cstruct()), bs.now_ns, flags)
     if rc:

@@ -11,6 +11,10 @@
 //   the task generator                       service/history/mutableStateTaskGenerator.go:122-545
 //   timerBuilder picks                       service/history/timerBuilder.go:171-230,233-312
 //   nDCStateRebuilder.rebuild's call         service/history/nDCStateRebuilder.go:154-157
+//   CloseTransactionAsSnapshot(passive)     service/history/mutableStateBuilder.go:3787-3855: with
+//     the passive policy every close-transaction step is a no-op (:4240-4355), a replayed
+//     state has no new events, so what remains is setTaskInfo (historyEngine.go:2383-2397):
+//     every task's Version = GetCurrentVersion() (flag 2)
 //
 // It runs on the replay's outputs (cdr_out, the rebuilt mutable state) plus the entry's
 // own events (the events cache).  Parity pinning: the reference has no unit test for
@@ -251,6 +255,10 @@ struct Refresh {
 
     if (xt.size() > cp.xfer_cap || tt.size() > cp.ttask_cap) return CDR_E_REFRESH_CAPACITY;
     // commit: task lists and the refreshed timer-task masks
+    if (flags & 2u) {  // CloseTransactionAsSnapshot(passive): setTaskInfo (historyEngine.go:2383-2397)
+      for (auto& t : xt) t.version = curVer;
+      for (auto& t : tt) t.version = curVer;
+    }
     for (size_t j = 0; j < xt.size(); j++) out->transfer[cp.xfer_off + j] = xt[j];
     for (size_t j = 0; j < tt.size(); j++) out->timer_tasks[cp.ttask_off + j] = tt[j];
     out->n_tasks[2 * w] = (uint32_t)xt.size();

@@ -170,6 +170,23 @@ def test_external_tasks():
     assert (s.event_id, s.domain_id, s.target_run_id, s.flags) == (6, I("domain-id"), I("target-run"), 1)
 
 
+def test_snapshot_passive_task_versions():
+    """CloseTransactionAsSnapshot(passive): setTaskInfo sets every task's Version to the
+    current version (historyEngine.go:2383-2397) — timer picks included."""
+    import oracle
+    calls = [[_started()] + _dt(2)[:1], _dt(2)[1:2], _dt(2)[2:] + [
+        dict(_ev(5, "TimerStarted", timerStartedEventAttributes={"timerId": "t", "startToFireTimeoutSeconds": 9}),
+             version=9)]]
+    _, b = _hb(calls)
+    plain, snap = oracle.rebuild(b), oracle.rebuild(b, snapshot=True)
+    for kind in ("xfer", "ttask"):
+        p, q = plain.task_rows(0, kind), snap.task_rows(0, kind)
+        assert len(p) == len(q) > 0
+        assert all(t.version == 9 for t in q)
+        assert [t.type for t in p] == [t.type for t in q]
+    assert [t.version for t in plain.task_rows(0, "ttask")] == [7, 0]  # start version; user timer unset
+
+
 def test_refresh_caps_bound_oracle():
     """The planner's task capacities bound what the refresher emits on every config."""
     import oracle
@@ -193,10 +210,10 @@ def test_carry_entries_miss_the_start_event():
 
 
 # ------------------------------------------------------------------ GPU
-def _check(eng, b, adv=True):
+def _check(eng, b, adv=True, snapshot=False):
     import oracle
-    ref = oracle.rebuild(b, advanced_visibility=adv)
-    got = eng.rebuild(b, advanced_visibility=adv)
+    ref = oracle.rebuild(b, advanced_visibility=adv, snapshot=snapshot)
+    got = eng.rebuild(b, advanced_visibility=adv, snapshot=snapshot)
     bad = engine.compare(b, got, ref) + engine.compare_tasks(b, got, ref)
     for w in range(b.n_wfs):
         if got.result[w].code != ref.result[w].code:
@@ -217,7 +234,9 @@ def test_gpu_refresh_configs(engine_gpu, cfg):
 @pytest.mark.gpu
 @pytest.mark.parametrize("builder", [abi.BUILDER_LOCAL, abi.BUILDER_2DC, abi.BUILDER_NDC])
 def test_gpu_refresh_builders(engine_gpu, builder):
-    _check(engine_gpu, engine.synth_batch(0, 300, seed=71 + builder, builder=builder, error_rate=0.2), adv=False)
+    b = engine.synth_batch(0, 300, seed=71 + builder, builder=builder, error_rate=0.2)
+    _check(engine_gpu, b, adv=False)
+    _check(engine_gpu, b, snapshot=True)
 
 
 @pytest.mark.gpu
