@@ -206,6 +206,72 @@ class DeviceBatch:
         return ev_bytes + wf_bytes + rows, n_ok, ev_bytes, wf_bytes, rows
 
 
+def _np_dtype(ty, names):
+    fmt = {C.c_uint32: "<u4", C.c_int32: "<i4", C.c_uint64: "<u8", C.c_int64: "<i8"}
+    types = dict(ty._fields_)
+    return np.dtype({"names": list(names), "formats": [fmt[types[n]] for n in names],
+                     "offsets": [getattr(ty, n).offset for n in names], "itemsize": C.sizeof(ty)})
+
+
+def refresh_measure(torch, L, ctx, db, stream, steps):
+    """refreshTasks (refresh.hip, cdr_refresh_tasks_async) over the rebuilt states of the
+    timed replay: K launches timed with HIP events on the launch stream, after the
+    headline's timed region (it is not part of `value`).  Task slices per entry: the
+    refresher's bound (3 + pending activity / child / cancel / signal capacities transfer
+    tasks, 6 timer tasks)."""
+    n = db.info.n_entries
+    caps = np.frombuffer(db.h_caps, dtype=_np_dtype(abi.CdrWfCaps, (
+        "act_cap", "child_cap", "cancel_cap", "signal_cap", "xfer_off", "ttask_off", "xfer_cap", "ttask_cap")))
+    caps = caps.copy()
+    xcap = 3 + caps["act_cap"].astype(np.uint64) + caps["child_cap"] + caps["cancel_cap"] + caps["signal_cap"]
+    caps["xfer_cap"] = xcap.astype(np.uint32)
+    caps["ttask_cap"] = 6
+    caps["xfer_off"] = np.concatenate([[0], np.cumsum(xcap)[:-1]]).astype(np.uint64)
+    caps["ttask_off"] = np.arange(n, dtype=np.uint64) * 6
+    dev = torch.device("cuda", torch.cuda.current_device())
+    caps_t = torch.from_numpy(caps.view(np.uint8)).to(dev)
+    dbr = abi.CdrDevBatch.from_buffer_copy(db.db)
+    dbr.caps = caps_t.data_ptr()
+    xt = torch.zeros(int(xcap.sum()) * C.sizeof(abi.CdrTask), dtype=torch.uint8, device=dev)
+    tt = torch.zeros(n * 6 * C.sizeof(abi.CdrTask), dtype=torch.uint8, device=dev)
+    nt = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+    out = abi.CdrOut.from_buffer_copy(db.out)
+    out.transfer, out.timer_tasks, out.n_tasks = xt.data_ptr(), tt.data_ptr(), nt.data_ptr()
+    now = int(db.meta.now_ns)
+
+    def launch():
+        rc = L.cdr_refresh_tasks_async(ctx, C.byref(dbr), C.byref(out), now, abi.REFRESH_ADVANCED_VISIBILITY,
+                                       C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"cdr_refresh_tasks_async rc={rc}")
+
+    launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    counts = nt.view(-1, 2).sum(dim=0).tolist()
+    res = np.frombuffer(db.results(), dtype=np.dtype([("code", "<i4"), ("flags", "<u4"), ("fid", "<i8"),
+                                                      ("fix", "<i8"), ("n_activity", "<u4"), ("n_timer", "<u4"),
+                                                      ("n_child", "<u4"), ("n_cancel", "<u4"), ("n_signal", "<u4"),
+                                                      ("n_vh", "<u4"), ("n_rp", "<u4"), ("n_sa", "<u4")]))
+    ok = res["code"] == 0
+    rows = sum(int(res[f][ok].sum()) * b for f, b in ROW_BYTES.items() if f in (
+        "n_activity", "n_timer", "n_child", "n_cancel", "n_signal"))
+    # per entry: lane_wf, result, caps, desc, ExecutionInfo, the start event's columns and
+    # attribute words, the closing event's type/version, n_tasks; + pending rows + tasks
+    per_entry = 4 + C.sizeof(abi.CdrWfResult) + C.sizeof(abi.CdrWfCaps) + C.sizeof(abi.CdrWfDesc) + 256 + 44 + 12 + 8
+    alg = n * per_entry + rows + (counts[0] + counts[1]) * C.sizeof(abi.CdrTask)
+    return {"kernel": "k_refresh", "kernel_ms": ms, "entries": n, "ok_entries": int(ok.sum()),
+            "transfer_tasks": int(counts[0]), "timer_tasks": int(counts[1]),
+            "entries_per_s": n / (ms / 1e3), "algorithmic_bytes_per_launch": alg,
+            "achieved_gbs": alg / (ms / 1e3) / 1e9, "frac": alg / (ms / 1e3) / 1e9 / PEAK_HBM_GBS}
+
+
 def stream_peak_gbs(torch, nbytes=4 << 30, reps=5):
     a = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
     b = torch.empty_like(a)
@@ -270,6 +336,7 @@ def main():
     ap.add_argument("--no-fast-path", action="store_true", help="replay every slice with the general kernel")
     ap.add_argument("--no-wave", action="store_true", help="no wave slices: divergent histories in lane slices")
     ap.add_argument("--wave-all", action="store_true", help="every divergent history on a wave slice")
+    ap.add_argument("--no-refresh", action="store_true", help="skip the refreshTasks side measurement")
     args = ap.parse_args()
 
     import torch
@@ -338,6 +405,7 @@ def main():
     if tot_ok != tot_wfs:
         log(f"WARNING: {tot_wfs - tot_ok} workflows did not replay OK")
 
+    refresh = None if args.no_refresh else refresh_measure(torch, L, ctx, db, stream, max(1, args.steps))
     if rank != 0:
         if dist:
             dist.barrier()
@@ -371,6 +439,7 @@ def main():
                      "bytes_breakdown": {"events": ev_b, "per_workflow": wf_b, "pending_rows": row_b},
                      "stream_copy_peak_gbs": peak_meas},
         "cpu_baseline": cpu,
+        "refresh": refresh,
         "host": {"soa_pack_s": db.pack_s, "h2d_s": db.h2d_s,
                  "h2d_gbs": db.in_bytes / max(db.h2d_s, 1e-9) / 1e9},
         "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_workflows": tot_ok,
