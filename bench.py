@@ -220,16 +220,18 @@ def refresh_measure(torch, L, ctx, db, stream, steps):
     refresher's bound (3 + pending activity / child / cancel / signal capacities transfer
     tasks, 6 timer tasks)."""
     n = db.info.n_entries
-    caps = np.frombuffer(db.h_caps, dtype=_np_dtype(abi.CdrWfCaps, (
+    # a byte copy viewed through the partial dtype: the table offsets between the named
+    # fields must survive (a structured copy would not keep the gaps)
+    raw = np.frombuffer(db.h_caps, np.uint8).copy()
+    caps = raw.view(_np_dtype(abi.CdrWfCaps, (
         "act_cap", "child_cap", "cancel_cap", "signal_cap", "xfer_off", "ttask_off", "xfer_cap", "ttask_cap")))
-    caps = caps.copy()
     xcap = 3 + caps["act_cap"].astype(np.uint64) + caps["child_cap"] + caps["cancel_cap"] + caps["signal_cap"]
     caps["xfer_cap"] = xcap.astype(np.uint32)
     caps["ttask_cap"] = 6
     caps["xfer_off"] = np.concatenate([[0], np.cumsum(xcap)[:-1]]).astype(np.uint64)
     caps["ttask_off"] = np.arange(n, dtype=np.uint64) * 6
     dev = torch.device("cuda", torch.cuda.current_device())
-    caps_t = torch.from_numpy(caps.view(np.uint8)).to(dev)
+    caps_t = torch.from_numpy(raw).to(dev)
     dbr = abi.CdrDevBatch.from_buffer_copy(db.db)
     dbr.caps = caps_t.data_ptr()
     xt = torch.zeros(int(xcap.sum()) * C.sizeof(abi.CdrTask), dtype=torch.uint8, device=dev)

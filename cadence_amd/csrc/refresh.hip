@@ -74,13 +74,26 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
   if (wi < 0) return;
   const uint32_t w = (uint32_t)wi;
   const uint32_t s = (uint32_t)(i / CDR_SLICE_WIDTH);
-  cdr_wf_result& r = O.result[w];
+  // Everything that depends only on (w, s) is loaded before the first branch on any of
+  // it, so the chain of dependent global loads is lane_wf -> {records, slice row} -> slab
+  // (-> arena) instead of one link per record.
+  const uint64_t row0 = B.ev.slice_row0[s];
+  const bool wave = (B.ev.slice_flags[s] & CDR_SLICE_WAVE) != 0;
+  const cdr_wf_result r = O.result[w];
+  const cdr_wf_caps cp = B.caps[w];
+  const cdr_wf_desc d = B.wfs[w];
+  const cdr_exec_info x = O.exec[w];
+  const Events E{B.ev.slab, row0, (uint32_t)(i % CDR_SLICE_WIDTH), wave, d.ev_len};
+  const bool any = d.ev_len > 0;
+  const int64_t id0 = any ? E.i64(0, CDR_COL_EVENT_ID) : 0;
+  const uint32_t ty0 = any ? E.type(0) : (uint32_t)CDR_EV_PAD;
+  const int64_t ver0 = any ? E.i64(0, CDR_COL_VERSION) : 0;
+  const int64_t aux0 = any ? E.i64(0, CDR_COL_AUX) : 0;
+  // the last event: the NDC current version's usual source (a closed history ends with
+  // its closing event)
+  const uint32_t tyL = any ? E.type(d.ev_len - 1) : (uint32_t)CDR_EV_PAD;
+  const int64_t verL = any ? E.i64(d.ev_len - 1, CDR_COL_VERSION) : 0;
   if (r.code != CDR_OK) return;
-  const cdr_wf_caps& cp = B.caps[w];
-  const cdr_wf_desc& d = B.wfs[w];
-  const cdr_exec_info& x = O.exec[w];
-  Events E{B.ev.slab, B.ev.slice_row0[s], (uint32_t)(i % CDR_SLICE_WIDTH),
-           (B.ev.slice_flags[s] & CDR_SLICE_WAVE) != 0, d.ev_len};
 
   uint32_t nx = 0, nt = 0;
   const uint32_t xcap = cp.xfer_cap, tcap = cp.ttask_cap;
@@ -131,20 +144,30 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
       curVer = O.repl[w].current_version;
     } else if (d.builder == CDR_BUILDER_NDC && E.n > 0) {
       // the prelude's last version while running: the (only) closing event's, or the last
-      uint64_t k = E.n - 1;
-      if (x.close_status != CDR_CLOSE_NONE)
+      curVer = verL;
+      if (x.close_status != CDR_CLOSE_NONE && !is_close_type(tyL)) {
+        uint64_t k = E.n - 1;
         while (k > 0 && !is_close_type(E.type(k))) k--;
-      curVer = E.i64(k, CDR_COL_VERSION);
+        curVer = E.i64(k, CDR_COL_VERSION);
+      }
     }
     // ---- ForWorkflowStart (:162-191): the start event is event 1
-    const int64_t ks = E.n > 0 && E.i64(0, CDR_COL_EVENT_ID) == CDR_FIRST_EVENT_ID ? 0 : E.find(CDR_FIRST_EVENT_ID);
-    if (ks < 0 || E.type(ks) != CDR_EV_WF_STARTED) {
-      code = CDR_E_REFRESH_EVENT_NOT_FOUND;
+    int64_t startVer = ver0, saux = aux0;
+    if (id0 != CDR_FIRST_EVENT_ID || ty0 != CDR_EV_WF_STARTED) {  // not the entry's first event
+      const int64_t ks = E.find(CDR_FIRST_EVENT_ID);
+      if (ks < 0 || E.type(ks) != CDR_EV_WF_STARTED) {
+        code = CDR_E_REFRESH_EVENT_NOT_FOUND;
+        break;
+      }
+      startVer = E.i64(ks, CDR_COL_VERSION);
+      saux = E.i64(ks, CDR_COL_AUX);
+    }
+    constexpr uint64_t kStartWords = (sizeof(cdr_attr_wf_started) + 7) / 8;
+    if ((uint64_t)saux + kStartWords > B.ev.arena_words) {  // malformed input: no attribute record
+      code = CDR_E_BAD_INPUT;
       break;
     }
-    const int64_t startVer = E.i64(ks, CDR_COL_VERSION);
-    const cdr_attr_wf_started* sa =
-        (const cdr_attr_wf_started*)(B.ev.arena + (uint64_t)E.i64(ks, CDR_COL_AUX));
+    const cdr_attr_wf_started* sa = (const cdr_attr_wf_started*)(B.ev.arena + (uint64_t)saux);
     const int32_t backoff_s = sa->first_decision_backoff_s;
     const uint32_t sflags = sa->flags;
     const int64_t backoff = (int64_t)backoff_s * kSec;
@@ -244,10 +267,16 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
     if (head >= 0) T(CDR_TT_USER_TIMER, 0, hs, he, 0, 0);
     // ---- ForChildWorkflow (:344-385), ForRequestCancelExternalWorkflow (:387-423),
     // ForSignalExternalWorkflow (:425-461); target domain per getTargetDomainID (:531-545)
-    auto ext = [&](int64_t id) -> const cdr_attr_external* {
+    // the initiated event's attributes; an event of another type has none (Go's nil
+    // attribute struct reads as zero values: empty domain, workflow, run)
+    const cdr_attr_external zero_ext{};
+    constexpr uint64_t kExtWords = (sizeof(cdr_attr_external) + 7) / 8;
+    auto ext = [&](int64_t id, uint32_t type) -> const cdr_attr_external* {
       const int64_t k = E.find(id);
       if (k < 0) return nullptr;
-      return (const cdr_attr_external*)(B.ev.arena + ((uint64_t)E.i64(k, CDR_COL_KEY) >> 32));
+      const uint64_t off = (uint64_t)E.i64(k, CDR_COL_KEY) >> 32;
+      if (E.type(k) != type || off + kExtWords > B.ev.arena_words) return &zero_ext;
+      return (const cdr_attr_external*)(B.ev.arena + off);
     };
     auto target = [&](const cdr_attr_external* a, uint32_t* dom) -> int32_t {
       if (a->domain == 0) {
@@ -261,7 +290,7 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
     const cdr_child_info* ch = O.child + cp.child_off;
     for (uint32_t j = 0; j < r.n_child && code == CDR_OK; j++) {
       if (ch[j].started_id != CDR_EMPTY_EVENT_ID) continue;
-      const cdr_attr_external* a = ext(ch[j].initiated_id);
+      const cdr_attr_external* a = ext(ch[j].initiated_id, CDR_EV_CHILD_INITIATED);
       uint32_t dom = 0;
       code = a ? target(a, &dom) : CDR_E_REFRESH_EVENT_NOT_FOUND;
       if (code == CDR_OK)
@@ -269,7 +298,7 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
     }
     const cdr_cancel_info* rc = O.cancel + cp.cancel_off;
     for (uint32_t j = 0; j < r.n_cancel && code == CDR_OK; j++) {
-      const cdr_attr_external* a = ext(rc[j].initiated_id);
+      const cdr_attr_external* a = ext(rc[j].initiated_id, CDR_EV_RCE_INITIATED);
       uint32_t dom = 0;
       code = a ? target(a, &dom) : CDR_E_REFRESH_EVENT_NOT_FOUND;
       if (code == CDR_OK)
@@ -278,7 +307,7 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
     }
     const cdr_signal_info* sg = O.signal + cp.signal_off;
     for (uint32_t j = 0; j < r.n_signal && code == CDR_OK; j++) {
-      const cdr_attr_external* a = ext(sg[j].initiated_id);
+      const cdr_attr_external* a = ext(sg[j].initiated_id, CDR_EV_SE_INITIATED);
       uint32_t dom = 0;
       code = a ? target(a, &dom) : CDR_E_REFRESH_EVENT_NOT_FOUND;
       if (code == CDR_OK)
@@ -292,9 +321,10 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
   } while (false);
 
   if (code != CDR_OK) {
-    r.code = code;
-    r.fail_event_id = 0;
-    r.fail_index = 0;
+    cdr_wf_result& R = O.result[w];
+    R.code = code;
+    R.fail_event_id = 0;
+    R.fail_index = 0;
     O.n_tasks[2 * (uint64_t)w] = 0;
     O.n_tasks[2 * (uint64_t)w + 1] = 0;
     return;

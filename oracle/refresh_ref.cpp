@@ -210,21 +210,24 @@ struct Refresh {
         head = (int)j;
     if (head >= 0) T(CDR_TT_USER_TIMER, 0, tim[head].started_id, tim[head].expiry_time, 0, 0);
     // target domain (getTargetDomainID :531-545)
-    auto target = [&](const cdr_event* e, uint32_t* dom) -> int32_t {
-      if (e->a.ext.domain == 0) {  // "" -> the execution's domain
+    auto target = [&](const cdr_attr_external* e, uint32_t* dom) -> int32_t {
+      if (e->domain == 0) {  // "" -> the execution's domain
         *dom = x.domain_id;
         return CDR_OK;
       }
-      if (e->a.ext.flags & CDR_XF_DOMAIN_MISSING) return CDR_E_DOMAIN_NOT_FOUND;
-      *dom = e->a.ext.target_domain_id;
+      if (e->flags & CDR_XF_DOMAIN_MISSING) return CDR_E_DOMAIN_NOT_FOUND;
+      *dom = e->target_domain_id;
       return CDR_OK;
     };
     // ---- ForChildWorkflow (:344-385) -> generateChildWorkflowTasks (:356-387)
     const cdr_child_info* ch = out->child + cp.child_off;
     for (uint32_t j = 0; j < r.n_child; j++) {
       if (ch[j].started_id != CDR_EMPTY_EVENT_ID) continue;
-      const cdr_event* e = find(w, ch[j].initiated_id);
-      if (!e) return CDR_E_REFRESH_EVENT_NOT_FOUND;
+      const cdr_event* ev = find(w, ch[j].initiated_id);
+      if (!ev) return CDR_E_REFRESH_EVENT_NOT_FOUND;
+      const cdr_attr_external* e = &ev->a.ext;
+      const cdr_attr_external zero{};
+      if (ev->type != CDR_EV_CHILD_INITIATED) e = &zero;  // nil attributes read as zero values
       uint32_t dom;
       if (int32_t c = target(e, &dom)) return c;
       cdr_task& t = X(CDR_TT_START_CHILD, ch[j].initiated_id, ch[j].version);
@@ -232,24 +235,29 @@ struct Refresh {
       t.target_workflow_id = ch[j].started_workflow_id;
     }
     // ---- ForRequestCancelExternalWorkflow (:387-423) / ForSignalExternalWorkflow (:425-461)
-    auto external = [&](uint32_t type, int64_t initiated, int64_t ver) -> int32_t {
-      const cdr_event* e = find(w, initiated);
-      if (!e) return CDR_E_REFRESH_EVENT_NOT_FOUND;
+    const cdr_attr_external zero_ext{};  // a nil attribute struct reads as zero values
+    auto attrs = [&](const cdr_event* e, uint32_t type) -> const cdr_attr_external* {
+      return e->type == type ? &e->a.ext : &zero_ext;
+    };
+    auto external = [&](uint32_t type, uint32_t evtype, int64_t initiated, int64_t ver) -> int32_t {
+      const cdr_event* ev = find(w, initiated);
+      if (!ev) return CDR_E_REFRESH_EVENT_NOT_FOUND;
+      const cdr_attr_external* e = attrs(ev, evtype);
       uint32_t dom;
       if (int32_t c = target(e, &dom)) return c;
       cdr_task& t = X(type, initiated, ver);
       t.domain_id = dom;
-      t.target_workflow_id = e->a.ext.workflow_id;
-      t.target_run_id = e->a.ext.run_id;
-      t.flags = (e->a.ext.flags & CDR_XF_CHILD_ONLY) ? CDR_TF_CHILD_ONLY : 0u;
+      t.target_workflow_id = e->workflow_id;
+      t.target_run_id = e->run_id;
+      t.flags = (e->flags & CDR_XF_CHILD_ONLY) ? CDR_TF_CHILD_ONLY : 0u;
       return CDR_OK;
     };
     const cdr_cancel_info* rc = out->cancel + cp.cancel_off;
     for (uint32_t j = 0; j < r.n_cancel; j++)
-      if (int32_t c = external(CDR_TT_CANCEL_EXECUTION, rc[j].initiated_id, rc[j].version)) return c;
+      if (int32_t c = external(CDR_TT_CANCEL_EXECUTION, CDR_EV_RCE_INITIATED, rc[j].initiated_id, rc[j].version)) return c;
     const cdr_signal_info* sg = out->signal + cp.signal_off;
     for (uint32_t j = 0; j < r.n_signal; j++)
-      if (int32_t c = external(CDR_TT_SIGNAL_EXECUTION, sg[j].initiated_id, sg[j].version)) return c;
+      if (int32_t c = external(CDR_TT_SIGNAL_EXECUTION, CDR_EV_SE_INITIATED, sg[j].initiated_id, sg[j].version)) return c;
     // ---- ForWorkflowSearchAttr (:463-472), when advanced visibility is on (:148-156)
     if (flags & 1u) X(CDR_TT_UPSERT_SA, 0, curVer);
 
