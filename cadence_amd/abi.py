@@ -280,6 +280,8 @@ EXPORTS = {
                                       C.c_void_p]),
     "cdr_rebuild_batch": (i32, [C.c_void_p, C.POINTER(CdrBatch), C.POINTER(CdrWfCaps), C.POINTER(CdrTotals),
                                 C.POINTER(CdrOut), u32]),
+    "cdr_encode_rows_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
+                                    C.c_void_p]),
     "cdr_compact_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
                                 C.c_void_p, C.c_void_p]),
     "cdr_checksum_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p, C.c_void_p]),

@@ -275,6 +275,22 @@ class Outputs:
         return [self.tables[table][off + j] for j in range(n)]
 
 
+_hip_lib = None
+
+
+def _hip():
+    """The HIP runtime (device buffers for small host-driven calls; no torch)."""
+    global _hip_lib
+    if _hip_lib is None:
+        L = C.CDLL("libamdhip64.so")
+        L.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        L.hipFree.argtypes = [C.c_void_p]
+        L.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        L.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+        _hip_lib = L
+    return _hip_lib
+
+
 class Engine:
     """One device context (the analogue of one stateBuilder provider)."""
 
@@ -322,6 +338,50 @@ class Engine:
         if rc:
             raise RuntimeError(f"cdr_replay_batch rc={rc}")
         return out
+
+    def encode_rows(self, batch: Batch, out: Outputs, table: str) -> bytes:
+        """sqlblobs row blobs of one pending table ("timer" or "cancel") of replayed
+        outputs through cdr_encode_rows_async (the records go to HBM, the blobs come
+        back): blob of row r at r * CDR_BLOB_*_BYTES.  Device memory through the HIP
+        runtime directly (the context this engine already initialised)."""
+        tid, size = {"timer": (1, 45), "cancel": (3, 66)}[table]
+        hip = _hip()
+        pl = out.plan
+        ptrs = []
+
+        def dalloc(nbytes):
+            p = C.c_void_p()
+            if hip.hipMalloc(C.byref(p), C.c_size_t(max(8, nbytes))) != 0:
+                raise RuntimeError("hipMalloc failed")
+            ptrs.append(p)
+            return p
+
+        def up(x):
+            nb = C.sizeof(x)
+            p = dalloc(nb)
+            if hip.hipMemcpy(p, C.addressof(x), C.c_size_t(nb), 1) != 0:  # hipMemcpyHostToDevice
+                raise RuntimeError("hipMemcpy H2D failed")
+            return p
+        try:
+            n_rows = max(1, getattr(pl.totals, table))
+            db = abi.CdrDevBatch()
+            db.n_wfs = batch.n_wfs
+            db.caps = up(pl.caps)
+            o = abi.CdrOut()
+            o.result = up(out.result)
+            setattr(o, table, up(out.tables[table]))
+            blobs = dalloc(n_rows * size)
+            hip.hipMemset(blobs, 0, C.c_size_t(n_rows * size))
+            rc = abi.lib().cdr_encode_rows_async(self.ctx, tid, C.byref(db), C.byref(o), blobs, None)
+            if rc:
+                raise RuntimeError(f"cdr_encode_rows_async rc={rc}")
+            host = (C.c_uint8 * (n_rows * size))()
+            if hip.hipMemcpy(host, blobs, C.c_size_t(n_rows * size), 2) != 0:  # DeviceToHost (synchronises)
+                raise RuntimeError("hipMemcpy D2H failed")
+            return bytes(host)
+        finally:
+            for p in ptrs:
+                hip.hipFree(p)
 
     def rebuild(self, batch: Batch, pl: Plan | None = None, advanced_visibility: bool = True, snapshot: bool = False) -> Outputs:
         """nDCStateRebuilder.rebuild's device half through cdr_rebuild_batch: replay

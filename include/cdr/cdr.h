@@ -17,6 +17,9 @@
  *                                       service/history/mutableStateTaskRefresher.go:66-160
  *                                       service/history/nDCStateRebuilder.go:154-157
  *     -> cdr_refresh_tasks_async (device-resident) / cdr_rebuild_batch (host buffers)
+ *   sql row blobs (timerInfoToBlob, requestCancelInfoToBlob)
+ *                                       common/persistence/sql/workflowStateMaps.go:239-260,504-521
+ *     -> cdr_encode_rows_async
  *   common.WorkflowIDToHistoryShard     common/util.go:249-252
  *     -> cdr_workflow_id_to_shard (farmhash Fingerprint32 % numShards)
  *
@@ -312,6 +315,23 @@ int cdr_refresh_tasks_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out
  * timer_tasks and n_tasks are required (sized by `totals`).  Synchronous. */
 int cdr_rebuild_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* totals,
                       cdr_out* out, uint32_t flags);
+
+/* Persisted-format row encoders: the SQL persistence's per-row blobs,
+ * thriftrw binary protocol (common/persistence/sql/blob.go:61-73, protocol.Binary) of
+ * the sqlblobs structs the row writers build (common/persistence/sql/workflowStateMaps.go):
+ *   table 1  TimerInfo{Version, StartedID, ExpiryTimeNanos, TaskID}
+ *            (sqlblobs.thrift:201-206, workflowStateMaps.go:242-247): CDR_BLOB_TIMER_BYTES
+ *   table 3  RequestCancelInfo{Version, InitiatedEventBatchID, CancelRequestID}
+ *            (sqlblobs.thrift:195-199, workflowStateMaps.go:507-511): CDR_BLOB_CANCEL_BYTES;
+ *            CancelRequestID is the row's UUID in RFC 4122 text form (hi then lo, 8-4-4-4-12
+ *            lowercase hex)
+ * Every field is set (the row writers pass pointers), so each blob has a fixed size and
+ * row r of the table (caps.*_off + j) is written at blobs + r * size, for the rows
+ * j < result.n_* of every CDR_OK entry (other rows untouched).  Asynchronous. */
+#define CDR_BLOB_TIMER_BYTES 45u
+#define CDR_BLOB_CANCEL_BYTES 66u
+int cdr_encode_rows_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out, uint8_t* blobs,
+                          void* stream);
 
 /* Stream compaction of the per-workflow pending tables into dense tables
  * (device pointers): for each table, rows [caps.off, caps.off + result.n) of every
