@@ -274,6 +274,44 @@ def refresh_measure(torch, L, ctx, db, stream, steps):
             "achieved_gbs": alg / (ms / 1e3) / 1e9, "frac": alg / (ms / 1e3) / 1e9 / PEAK_HBM_GBS}
 
 
+def encode_measure(torch, L, ctx, db, stream, steps):
+    """SQL row blobs (encode.hip, cdr_encode_rows_async) of the pending TimerInfo and
+    RequestCancelInfo rows of the replayed states: K launches per table timed with HIP
+    events on the launch stream, outside the headline's timed region.  Algorithmic
+    bytes per row: the record read (40 B) + the blob slot written (48 / 80 B)."""
+    res = np.frombuffer(db.results(), dtype=np.dtype([("code", "<i4"), ("flags", "<u4"), ("fid", "<i8"),
+                                                      ("fix", "<i8"), ("n_activity", "<u4"), ("n_timer", "<u4"),
+                                                      ("n_child", "<u4"), ("n_cancel", "<u4"), ("n_signal", "<u4"),
+                                                      ("n_vh", "<u4"), ("n_rp", "<u4"), ("n_sa", "<u4")]))
+    ok = res["code"] == 0
+    out = {}
+    for name, tid, size, stride, cnt, tot in (("timer", 1, 45, 48, "n_timer", db.info.totals.timer),
+                                              ("cancel", 3, 66, 80, "n_cancel", db.info.totals.cancel)):
+        rows = int(res[cnt][ok].sum())
+        blobs = torch.empty(max(16, tot * stride), dtype=torch.uint8, device="cuda")
+
+        def launch():
+            rc = L.cdr_encode_rows_async(ctx, tid, C.byref(db.db), C.byref(db.out),
+                                         C.c_void_p(blobs.data_ptr()), C.c_void_p(stream))
+            if rc:
+                raise RuntimeError(f"cdr_encode_rows_async rc={rc}")
+        launch()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            launch()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / steps
+        alg = rows * (40 + stride)
+        out[name] = {"kernel": "k_encode_rows", "kernel_ms": ms, "rows": rows, "rows_per_s": rows / (ms / 1e3),
+                     "algorithmic_bytes_per_launch": alg, "achieved_gbs": alg / (ms / 1e3) / 1e9,
+                     "frac": alg / (ms / 1e3) / 1e9 / PEAK_HBM_GBS}
+        del blobs
+    return out
+
+
 def stream_peak_gbs(torch, nbytes=4 << 30, reps=5):
     a = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
     b = torch.empty_like(a)
@@ -338,7 +376,7 @@ def main():
     ap.add_argument("--no-fast-path", action="store_true", help="replay every slice with the general kernel")
     ap.add_argument("--no-wave", action="store_true", help="no wave slices: divergent histories in lane slices")
     ap.add_argument("--wave-all", action="store_true", help="every divergent history on a wave slice")
-    ap.add_argument("--no-refresh", action="store_true", help="skip the refreshTasks side measurement")
+    ap.add_argument("--no-refresh", action="store_true", help="skip the refreshTasks / row-encoder side measurements")
     args = ap.parse_args()
 
     import torch
@@ -407,6 +445,7 @@ def main():
     if tot_ok != tot_wfs:
         log(f"WARNING: {tot_wfs - tot_ok} workflows did not replay OK")
 
+    encode = None if args.no_refresh else encode_measure(torch, L, ctx, db, stream, max(1, args.steps))
     refresh = None if args.no_refresh else refresh_measure(torch, L, ctx, db, stream, max(1, args.steps))
     if rank != 0:
         if dist:
@@ -442,6 +481,7 @@ def main():
                      "stream_copy_peak_gbs": peak_meas},
         "cpu_baseline": cpu,
         "refresh": refresh,
+        "encode": encode,
         "host": {"soa_pack_s": db.pack_s, "h2d_s": db.h2d_s,
                  "h2d_gbs": db.in_bytes / max(db.h2d_s, 1e-9) / 1e9},
         "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_workflows": tot_ok,

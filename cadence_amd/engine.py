@@ -342,9 +342,10 @@ class Engine:
     def encode_rows(self, batch: Batch, out: Outputs, table: str) -> bytes:
         """sqlblobs row blobs of one pending table ("timer" or "cancel") of replayed
         outputs through cdr_encode_rows_async (the records go to HBM, the blobs come
-        back): blob of row r at r * CDR_BLOB_*_BYTES.  Device memory through the HIP
+        back): blob of row r in the slot at r * CDR_BLOB_*_STRIDE, returned as
+        {row: blob bytes} for the rows of OK entries.  Device memory through the HIP
         runtime directly (the context this engine already initialised)."""
-        tid, size = {"timer": (1, 45), "cancel": (3, 66)}[table]
+        tid, size, stride = {"timer": (1, 45, 48), "cancel": (3, 66, 80)}[table]
         hip = _hip()
         pl = out.plan
         ptrs = []
@@ -370,15 +371,26 @@ class Engine:
             o = abi.CdrOut()
             o.result = up(out.result)
             setattr(o, table, up(out.tables[table]))
-            blobs = dalloc(n_rows * size)
-            hip.hipMemset(blobs, 0, C.c_size_t(n_rows * size))
+            blobs = dalloc(n_rows * stride)
+            hip.hipMemset(blobs, 0, C.c_size_t(n_rows * stride))
             rc = abi.lib().cdr_encode_rows_async(self.ctx, tid, C.byref(db), C.byref(o), blobs, None)
             if rc:
                 raise RuntimeError(f"cdr_encode_rows_async rc={rc}")
-            host = (C.c_uint8 * (n_rows * size))()
-            if hip.hipMemcpy(host, blobs, C.c_size_t(n_rows * size), 2) != 0:  # DeviceToHost (synchronises)
+            host = (C.c_uint8 * (n_rows * stride))()
+            if hip.hipMemcpy(host, blobs, C.c_size_t(n_rows * stride), 2) != 0:  # DeviceToHost (synchronises)
                 raise RuntimeError("hipMemcpy D2H failed")
-            return bytes(host)
+            raw = bytes(host)
+            off = {"timer": "timer_off", "cancel": "cancel_off"}[table]
+            cnt = {"timer": "n_timer", "cancel": "n_cancel"}[table]
+            blobs_out = {}
+            for w in range(batch.n_wfs):
+                if out.result[w].code == abi.OK:
+                    base = getattr(pl.caps[w], off)
+                    for j in range(getattr(out.result[w], cnt)):
+                        r = base + j
+                        blobs_out[r] = raw[r * stride:r * stride + size]
+                        assert raw[r * stride + size:(r + 1) * stride] == bytes(stride - size), "slot padding"
+            return blobs_out
         finally:
             for p in ptrs:
                 hip.hipFree(p)

@@ -325,11 +325,15 @@ int cdr_rebuild_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps,
  *            (sqlblobs.thrift:195-199, workflowStateMaps.go:507-511): CDR_BLOB_CANCEL_BYTES;
  *            CancelRequestID is the row's UUID in RFC 4122 text form (hi then lo, 8-4-4-4-12
  *            lowercase hex)
- * Every field is set (the row writers pass pointers), so each blob has a fixed size and
- * row r of the table (caps.*_off + j) is written at blobs + r * size, for the rows
- * j < result.n_* of every CDR_OK entry (other rows untouched).  Asynchronous. */
+ * Every field is set (the row writers pass pointers), so each blob has a fixed size
+ * (CDR_BLOB_*_BYTES); row r of the table (caps.*_off + j) is written to the 16-B aligned
+ * slot blobs + r * CDR_BLOB_*_STRIDE (its first *_BYTES bytes are the blob, the rest
+ * zero), for the rows j < result.n_* of every CDR_OK entry (other slots untouched);
+ * `blobs` must be 16-B aligned.  Asynchronous. */
 #define CDR_BLOB_TIMER_BYTES 45u
+#define CDR_BLOB_TIMER_STRIDE 48u
 #define CDR_BLOB_CANCEL_BYTES 66u
+#define CDR_BLOB_CANCEL_STRIDE 80u
 int cdr_encode_rows_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out, uint8_t* blobs,
                           void* stream);
 
