@@ -345,7 +345,19 @@ def cpu_baseline(config, n_wfs, seed, min_seconds=10.0):
             if el >= (min_seconds if th == threads else min_seconds / 4) or reps >= 200:
                 break
         res[th] = n_ev * reps / el
+    # refreshTasks on the same sample (oracle/refresh_ref.cpp, one thread), beside k_refresh
+    out = oracle.replay(b, pl, threads=threads)
+    out.alloc_tasks(pl)
+    bs, cs = b.cstruct(), out.cstruct()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle.lib().cdro_refresh_tasks(C.byref(bs), pl.caps, C.byref(cs), bs.now_ns, 1)
+        reps += 1
+        if time.perf_counter() - t0 >= min_seconds / 4 or reps >= 1000:
+            break
+    refresh_eps = b.n_wfs * reps / (time.perf_counter() - t0)
     return {"value": res[threads], "unit": "events/s", "cores": threads, "kind": "port",
+            "refresh_entries_per_s_1thread": refresh_eps,
             "sample": f"config {config}: {n_wfs} workflows x {n_ev // max(1, n_wfs)} events, replayed "
                       f"{'repeatedly'} for >= {min_seconds:.0f} s; single-thread {res[1]:.4g} events/s; "
                       f"the Go stateBuilder cannot run here (no Go toolchain)",
