@@ -76,20 +76,24 @@ __device__ __forceinline__ void put_blob(const Row& row, uint8_t* dst, ByteFn by
   }
 }
 
-__global__ __launch_bounds__(64) void k_encode_rows(int table, cdr_dev_batch B, cdr_out O, uint8_t* blobs) {
-  const uint32_t w = blockIdx.x, lane = threadIdx.x;
+// one thread per entry: the entry records are read coalesced across a wavefront and an
+// entry's rows (a handful) are written by its own lane, blob after blob
+__global__ __launch_bounds__(256) void k_encode_rows(int table, cdr_dev_batch B, cdr_out O, uint8_t* blobs) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= B.n_wfs) return;
   const cdr_wf_result& r = O.result[w];
   if (r.code != CDR_OK) return;
   const cdr_wf_caps& c = B.caps[w];
   if (table == 1) {
-    for (uint32_t j = lane; j < r.n_timer; j += 64) {
+    const uint32_t n = r.n_timer;
+    for (uint32_t j = 0; j < n; j++) {
       const uint64_t row = c.timer_off + j;
       put_blob<CDR_BLOB_TIMER_BYTES, CDR_BLOB_TIMER_STRIDE>(O.timer[row], blobs + row * CDR_BLOB_TIMER_STRIDE,
                                                             timer_byte);
     }
   } else {
-    for (uint32_t j = lane; j < r.n_cancel; j += 64) {
+    const uint32_t n = r.n_cancel;
+    for (uint32_t j = 0; j < n; j++) {
       const uint64_t row = c.cancel_off + j;
       put_blob<CDR_BLOB_CANCEL_BYTES, CDR_BLOB_CANCEL_STRIDE>(O.cancel[row], blobs + row * CDR_BLOB_CANCEL_STRIDE,
                                                               cancel_byte);
@@ -104,7 +108,8 @@ extern "C" int cdr_encode_rows_async(cdr_ctx* ctx, int table, const cdr_dev_batc
   if (!ctx || !in || !out || !blobs || (table != 1 && table != 3) || !out->result) return CDR_API_EINVAL;
   if ((table == 1 && !out->timer) || (table == 3 && !out->cancel)) return CDR_API_EINVAL;
   if (in->n_wfs == 0) return CDR_API_OK;
-  hipLaunchKernelGGL(k_encode_rows, dim3(in->n_wfs), dim3(64), 0, (hipStream_t)stream, table, *in, *out, blobs);
+  hipLaunchKernelGGL(k_encode_rows, dim3((in->n_wfs + 255) / 256), dim3(256), 0, (hipStream_t)stream, table, *in,
+                     *out, blobs);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     fprintf(stderr, "cdr: k_encode_rows launch failed: %s\n", hipGetErrorString(e));
