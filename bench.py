@@ -34,15 +34,7 @@ from cadence_amd import abi  # noqa: E402
 NUM_SHARDS = 16384
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
-# SURVEY §8(d) canonical algorithmic bytes
-A_TYPE = np.zeros(256, np.int64)
-for _name, _b in (("WorkflowExecutionStarted", 96), ("ActivityTaskScheduled", 48), ("DecisionTaskScheduled", 12),
-                  ("DecisionTaskCompleted", 12), ("TimerStarted", 8), ("StartChildWorkflowExecutionInitiated", 16),
-                  ("SignalExternalWorkflowExecutionInitiated", 12), ("DecisionTaskStarted", 4),
-                  ("ActivityTaskStarted", 4), ("DecisionTaskTimedOut", 4), ("ChildWorkflowExecutionStarted", 4),
-                  ("WorkflowExecutionContinuedAsNew", 4), ("UpsertWorkflowSearchAttributes", 8)):
-    A_TYPE[abi.EV[_name]] = _b
-ROW_BYTES = {"n_activity": 128, "n_timer": 32, "n_child": 48, "n_cancel": 24, "n_signal": 40}
+from cadence_amd.synth import DeviceBatch, RESULT_DTYPE, ROW_BYTES  # noqa: E402
 
 
 def log(*a):
@@ -56,154 +48,40 @@ def dist_env():
     return ws, rank, local
 
 
+def workflow_weights(config: int, total_wfs: int, seed: int) -> np.ndarray:
+    """Planned event count of every workflow of the population (synth.cpp plan_one),
+    drawn without generating the histories: the shard->GPU assignment's weights."""
+    L = abi.lib()
+    p = abi.CdrSynthParams(config=config, n_wfs=0, seed=seed)
+    w = np.zeros(total_wfs, np.uint32)
+    rc = L.cdr_synth_weights(C.byref(p), total_wfs, w.ctypes.data)
+    if rc:
+        raise RuntimeError(f"cdr_synth_weights rc={rc}")
+    return w
+
+
+BIG_HISTORY = 100_000  # SURVEY §8(e): shards holding a >=100k-event history are spread first
+
+
 def assign_shards(total_wfs: int, world: int, rank: int, lengths=None):
-    """workflow ids "wf-<i>" -> historyShardID -> GPU (greedy largest-first on events)."""
+    """workflow ids "wf-<i>" -> historyShardID (Fingerprint32 % 16384, common/util.go:249-252)
+    -> GPU: greedy largest-first (LPT) on the shards' event counts, shards that hold a
+    >=100k-event history dealt first.  Returns (my workflow indices,
+    per-GPU event load)."""
     L = abi.lib()
     shard = np.empty(total_wfs, np.int32)
     L.cdr_synth_shards(total_wfs, NUM_SHARDS, shard.ctypes.data)
-    w = np.bincount(shard, weights=lengths, minlength=NUM_SHARDS) if lengths is not None else \
-        np.bincount(shard, minlength=NUM_SHARDS).astype(np.float64)
+    lengths = np.ones(total_wfs) if lengths is None else np.asarray(lengths, np.float64)
+    w = np.bincount(shard, weights=lengths, minlength=NUM_SHARDS)
+    big = np.bincount(shard, weights=(lengths >= BIG_HISTORY).astype(np.float64), minlength=NUM_SHARDS) > 0
     owner = np.zeros(NUM_SHARDS, np.int32)
     load = np.zeros(world)
-    for s in np.argsort(-w, kind="stable"):
+    for s in np.lexsort((-w, ~big)):  # big-history shards first, then by events, descending
         g = int(np.argmin(load))
         owner[s] = g
         load[g] += w[s]
     mine = np.nonzero(owner[shard] == rank)[0].astype(np.uint32)
     return mine, load
-
-
-class DeviceBatch:
-    """Synthetic batch generated straight into the sliced layout, uploaded to HBM."""
-
-    def __init__(self, torch, config, index_map, seed, target_len=0, plan_mode=abi.PLAN_WAVE):
-        L = abi.lib()
-        self.torch = torch
-        self.index_map = index_map
-        p = abi.CdrSynthParams(config=config, n_wfs=len(index_map), seed=seed, target_len=target_len, max_len=0,
-                               error_rate=0.0, builder=-1, rebuild=0, index_map=index_map.ctypes.data,
-                               plan_mode=plan_mode)
-        self.params = p
-        t0 = time.perf_counter()
-        info = abi.CdrSynthPlanInfo()
-        assert L.cdr_synth_sliced_plan(C.byref(p), C.byref(info)) == 0
-        self.info = info
-        self.h_slab = np.empty(info.n_rows * 64 * abi.EL_BYTES, np.uint8)
-        self.h_lane = np.empty(info.n_slices * 64, np.int32)
-        self.h_slen = np.empty(info.n_slices, np.uint32)
-        self.h_row0 = np.empty(info.n_slices, np.uint64)
-        self.h_sc_off = np.zeros(info.n_slices, np.uint64)
-        self.h_sc_act = np.zeros(info.n_slices, np.uint32)
-        self.h_sc_tim = np.zeros(info.n_slices, np.uint32)
-        self.h_sflags = np.zeros(info.n_slices, np.uint32)
-        self.h_arena = np.empty(max(1, info.arena_words), np.uint64)
-        self.h_wfs = (abi.CdrWfDesc * info.n_entries)()
-        self.h_caps = (abi.CdrWfCaps * info.n_entries)()
-        self.h_kvs = np.zeros(max(1, info.n_kvs) * 2, np.uint32)
-        self.h_rps = (abi.CdrResetPoint * max(1, info.n_rps))()
-        s = abi.CdrSlices(n_slices=info.n_slices, n_rows=info.n_rows, arena_words=info.arena_words)
-        s.slice_row0, s.slice_len, s.lane_wf = self.h_row0.ctypes.data, self.h_slen.ctypes.data, \
-            self.h_lane.ctypes.data
-        s.slab = self.h_slab.ctypes.data
-        s.arena = self.h_arena.ctypes.data
-        s.slice_scratch_off, s.slice_act_slots, s.slice_tim_slots = (
-            self.h_sc_off.ctypes.data, self.h_sc_act.ctypes.data, self.h_sc_tim.ctypes.data)
-        s.slice_flags = self.h_sflags.ctypes.data
-        meta = abi.CdrBatch()
-        threads = min(32, os.cpu_count() or 8)
-        rc = L.cdr_synth_sliced_fill(C.byref(p), C.byref(s), self.h_wfs, self.h_caps, self.h_kvs.ctypes.data,
-                                     self.h_rps, C.byref(meta), threads)
-        assert rc == 0, rc
-        self.meta = meta
-        self.pack_s = time.perf_counter() - t0
-        # ---- upload (H2D timed separately)
-        dev = torch.device("cuda", torch.cuda.current_device())
-        t0 = time.perf_counter()
-        self.keep = []
-
-        def up(a):
-            t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to(dev)
-            self.keep.append(t)
-            return t.data_ptr()
-
-        def up_ct(a):
-            return up(np.frombuffer(a, np.uint8))
-
-        db = abi.CdrDevBatch()
-        db.ev.n_slices, db.ev.n_rows, db.ev.arena_words = info.n_slices, info.n_rows, info.arena_words
-        db.ev.slice_row0, db.ev.slice_len, db.ev.lane_wf = up(self.h_row0), up(self.h_slen), up(self.h_lane)
-        db.ev.slab = up(self.h_slab)
-        db.ev.arena = up(self.h_arena)
-        db.ev.slice_scratch_off = up(self.h_sc_off)
-        db.ev.slice_act_slots = up(self.h_sc_act)
-        db.ev.slice_tim_slots = up(self.h_sc_tim)
-        db.ev.slice_flags = up(self.h_sflags)
-        L.cdr_plan_scratch(self.h_caps, self.h_lane.ctypes.data, info.n_slices, None, None, None, None,
-                           C.byref(sc_words := C.c_uint64()), None)
-        self.scratch_t = torch.zeros(max(8, sc_words.value * 8), dtype=torch.uint8, device=dev)
-        db.scratch = self.scratch_t.data_ptr()
-        db.wfs, db.caps = up_ct(self.h_wfs), up_ct(self.h_caps)
-        db.kvs, db.rps = up(self.h_kvs), up_ct(self.h_rps)
-        db.n_wfs = info.n_entries
-        db.max_act_slots = int(self.h_sc_act.max()) if len(self.h_sc_act) else 0
-        db.max_tim_slots = int(self.h_sc_tim.max()) if len(self.h_sc_tim) else 0
-        self.n_fast = int(((self.h_sflags & abi.SLICE_FAST) != 0).sum())
-        self.n_wave = int(((self.h_sflags & abi.SLICE_WAVE) != 0).sum())
-        db.n_fast_slices = self.n_fast
-        db.n_wave_slices = self.n_wave
-        db.empty_uuid = meta.empty_uuid
-        db.cluster = meta.cluster
-        db.now_ns = meta.now_ns
-        db.uuid_seed = meta.uuid_seed
-        self.db = db
-        tot = info.totals
-        out = abi.CdrOut()
-        sizes = {"result": info.n_entries * C.sizeof(abi.CdrWfResult),
-                 "exec": info.n_entries * C.sizeof(abi.CdrExecInfo),
-                 "repl": info.n_entries * C.sizeof(abi.CdrReplState),
-                 "vh": tot.vh * C.sizeof(abi.CdrVHItem), "act": tot.act * C.sizeof(abi.CdrActivityInfo),
-                 "timer": tot.timer * C.sizeof(abi.CdrTimerInfo), "child": tot.child * C.sizeof(abi.CdrChildInfo),
-                 "cancel": tot.cancel * C.sizeof(abi.CdrCancelInfo),
-                 "signal": tot.signal * C.sizeof(abi.CdrSignalInfo),
-                 "rp": tot.rp * C.sizeof(abi.CdrResetPoint), "sa": tot.sa * C.sizeof(abi.CdrKV)}
-        self.out_bytes = sum(sizes.values())
-        self.out_t = {}
-        for k, nb in sizes.items():
-            t = torch.zeros(max(8, nb), dtype=torch.uint8, device=dev)
-            self.out_t[k] = t
-            setattr(out, k, t.data_ptr())
-        self.out = out
-        torch.cuda.synchronize()
-        self.h2d_s = time.perf_counter() - t0
-        self.in_bytes = self.h_slab.nbytes + self.h_arena.nbytes
-        types = abi.slab_columns(self.h_slab, self.h_row0, self.h_slen, ("type_flags",))["type_flags"] & 0xFF
-        self.type_counts = np.bincount(types, minlength=256)
-        self.n_events = int(self.type_counts[:abi.EV["UpsertWorkflowSearchAttributes"] + 1].sum())
-
-    def results(self):
-        n = self.info.n_entries
-        raw = self.out_t["result"][: n * C.sizeof(abi.CdrWfResult)].cpu().numpy().copy()
-        return (abi.CdrWfResult * n).from_buffer(raw)
-
-    def algorithmic_bytes(self, res):
-        ev_bytes = int((self.type_counts[:42] * (48 + A_TYPE[:42])).sum())
-        n_ok, vh, rows, repl = 0, 0, 0, 0
-        arr = np.frombuffer(res, dtype=np.dtype([("code", "<i4"), ("flags", "<u4"), ("fid", "<i8"), ("fix", "<i8"),
-                                                   ("n_activity", "<u4"), ("n_timer", "<u4"), ("n_child", "<u4"),
-                                                   ("n_cancel", "<u4"), ("n_signal", "<u4"), ("n_vh", "<u4"),
-                                                   ("n_rp", "<u4"), ("n_sa", "<u4")]))
-        builders = np.frombuffer(self.h_wfs, dtype=np.uint8).reshape(len(self.h_wfs), -1)
-        ok = arr["code"] == 0
-        n_ok = int(ok.sum())
-        vh = int(arr["n_vh"][ok].sum())
-        for f, b in ROW_BYTES.items():
-            rows += int(arr[f][ok].sum()) * b
-        # builder field offset in cdr_wf_desc
-        boff = abi.CdrWfDesc.builder.offset
-        bld = builders[:, boff:boff + 4].copy().view(np.uint32)[:, 0]
-        repl = int(((bld == abi.BUILDER_2DC) & ok).sum()) * 32
-        wf_bytes = len(arr) * (256 + 8) + 16 * vh + repl
-        return ev_bytes + wf_bytes + rows, n_ok, ev_bytes, wf_bytes, rows
 
 
 def _np_dtype(ty, names):
@@ -257,10 +135,7 @@ def refresh_measure(torch, L, ctx, db, stream, steps):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     counts = nt.view(-1, 2).sum(dim=0).tolist()
-    res = np.frombuffer(db.results(), dtype=np.dtype([("code", "<i4"), ("flags", "<u4"), ("fid", "<i8"),
-                                                      ("fix", "<i8"), ("n_activity", "<u4"), ("n_timer", "<u4"),
-                                                      ("n_child", "<u4"), ("n_cancel", "<u4"), ("n_signal", "<u4"),
-                                                      ("n_vh", "<u4"), ("n_rp", "<u4"), ("n_sa", "<u4")]))
+    res = np.frombuffer(db.results(), dtype=RESULT_DTYPE)
     ok = res["code"] == 0
     rows = sum(int(res[f][ok].sum()) * b for f, b in ROW_BYTES.items() if f in (
         "n_activity", "n_timer", "n_child", "n_cancel", "n_signal"))
@@ -279,10 +154,7 @@ def encode_measure(torch, L, ctx, db, stream, steps):
     RequestCancelInfo rows of the replayed states: K launches per table timed with HIP
     events on the launch stream, outside the headline's timed region.  Algorithmic
     bytes per row: the record read (40 B) + the blob slot written (48 / 80 B)."""
-    res = np.frombuffer(db.results(), dtype=np.dtype([("code", "<i4"), ("flags", "<u4"), ("fid", "<i8"),
-                                                      ("fix", "<i8"), ("n_activity", "<u4"), ("n_timer", "<u4"),
-                                                      ("n_child", "<u4"), ("n_cancel", "<u4"), ("n_signal", "<u4"),
-                                                      ("n_vh", "<u4"), ("n_rp", "<u4"), ("n_sa", "<u4")]))
+    res = np.frombuffer(db.results(), dtype=RESULT_DTYPE)
     ok = res["code"] == 0
     out = {}
     for name, tid, size, stride, cnt, tot in (("timer", 1, 45, 48, "n_timer", db.info.totals.timer),
@@ -364,15 +236,42 @@ def cpu_baseline(config, n_wfs, seed, min_seconds=10.0):
             "single_thread_events_per_s": res[1], "workflows_per_s": res[threads] / (n_ev / max(1, n_wfs))}
 
 
+def lib_sha1() -> str:
+    import hashlib
+    return hashlib.sha1(open(abi.LIB_PATH, "rb").read()).hexdigest()
+
+
 def load_traffic(workload):
+    """PMC HBM bytes per launch (tools/pmc.sh + tools/traffic.py) for this workload, used
+    only when they were collected on this very build of libcdr.so (same SHA-1); else
+    (None, reason)."""
     p = os.path.join(HERE, "profiles", "traffic_latest.json")
     try:
         d = json.load(open(p))
-        if d.get("workload") == workload:
-            return d
     except Exception:
-        pass
-    return None
+        return None, "no PMC summary"
+    if d.get("workload") != workload:
+        return None, f"PMC summary is for {d.get('workload')}"
+    if d.get("lib_sha1") != lib_sha1():
+        return None, "stale: PMC summary from another build of libcdr.so"
+    return d, None
+
+
+def parity_check(db, ctx, stream, config, mine, seed):
+    """Full-size parity: every entry's output digest on the GPU (k_digest) against the
+    CPU restatement's (oracle/, restated hash in digest_ref.cpp) over the same
+    population, entry by entry.  Runs after the timed region."""
+    import oracle
+    t0 = time.perf_counter()
+    got, got_sum = db.digests(ctx, stream)
+    threads = max(1, min(os.cpu_count() or 1, int(os.environ.get("CDR_CPU_THREADS", "16"))))
+    want, want_sum, hist = oracle.synth_digests(config, mine, seed, threads=threads)
+    bad = np.nonzero(got != want)[0] if len(got) == len(want) else np.arange(max(len(got), len(want)))
+    return {"checked": True, "entries": int(len(want)), "mismatched_entries": int(len(bad)),
+            "first_mismatches": bad[:8].tolist(), "gpu_checksum": got_sum, "oracle_checksum": want_sum,
+            "oracle_status": hist, "cpu_threads": threads, "seconds": time.perf_counter() - t0,
+            "method": "per-entry digest of the persisted projection (cdr_entry_digests_async vs "
+                      "oracle/digest_ref.cpp), CopyToPersistence mutableStateBuilder.go:257-270"}
 
 
 def main():
@@ -389,6 +288,7 @@ def main():
     ap.add_argument("--no-wave", action="store_true", help="no wave slices: divergent histories in lane slices")
     ap.add_argument("--wave-all", action="store_true", help="every divergent history on a wave slice")
     ap.add_argument("--no-refresh", action="store_true", help="skip the refreshTasks / row-encoder side measurements")
+    ap.add_argument("--no-parity", action="store_true", help="skip the full-size GPU == oracle digest check")
     args = ap.parse_args()
 
     import torch
@@ -408,7 +308,7 @@ def main():
         L.cdr_set_fast_path(ctx, 0)
 
     total = args.wfs * world
-    mine, _ = assign_shards(total, world, rank)
+    mine, load = assign_shards(total, world, rank, workflow_weights(args.config, total, args.seed))
     log(f"[rank {rank}] {len(mine)} of {total} workflows (shard->GPU greedy over {NUM_SHARDS} shards)")
     db = DeviceBatch(torch, args.config, mine, args.seed, plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0))
     log(f"[rank {rank}] {db.n_fast} of {db.info.n_slices} slices on the fast-path kernel, {db.n_wave} wave slices")
@@ -457,6 +357,14 @@ def main():
     if tot_ok != tot_wfs:
         log(f"WARNING: {tot_wfs - tot_ok} workflows did not replay OK")
 
+    parity = None if args.no_parity else parity_check(db, ctx, stream, args.config, mine, args.seed)
+    if parity:
+        log(f"[rank {rank}] parity: {parity['mismatched_entries']} of {parity['entries']} entries differ from the "
+            f"oracle ({parity['seconds']:.1f}s)")
+        flag = torch.tensor([parity["mismatched_entries"], parity["entries"]], dtype=torch.int64, device="cuda")
+        if dist:
+            dist.all_reduce(flag)
+        parity["mismatched_entries_all_ranks"], parity["entries_all_ranks"] = [int(x) for x in flag.tolist()]
     encode = None if args.no_refresh else encode_measure(torch, L, ctx, db, stream, max(1, args.steps))
     refresh = None if args.no_refresh else refresh_measure(torch, L, ctx, db, stream, max(1, args.steps))
     if rank != 0:
@@ -469,7 +377,10 @@ def main():
     wf_per_s = tot_wfs * args.steps / elapsed
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
     workload = f"C{args.config}-{args.wfs}wf-sliced"
-    traffic = load_traffic(workload)
+    traffic, traffic_note = load_traffic(workload)
+    bld = db.builders()
+    names = {abi.BUILDER_LOCAL: "local", abi.BUILDER_2DC: "2DC", abi.BUILDER_NDC: "NDC"}
+    builders = {names[int(k)]: int(c) for k, c in zip(*np.unique(bld, return_counts=True))}
     peak_meas = None if args.no_stream_peak else stream_peak_gbs(torch)
     cpu = None if (args.no_cpu_baseline or args.gpus > 1) else cpu_baseline(args.config, 20000, args.seed)
     line = {
@@ -478,13 +389,15 @@ def main():
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "int64", "data": "synthetic (deterministic generator, SURVEY §8(d) shapes)",
         "config": {"workload": workload, "workflows_per_gpu": args.wfs, "events_per_gpu": db.n_events,
-                   "events_per_workflow": round(db.n_events / max(1, len(mine)), 2), "builder": "NDC",
+                   "events_per_workflow": round(db.n_events / max(1, len(mine)), 2),
+                   "builder": next(iter(builders)) if len(builders) == 1 else "mixed", "builders": builders,
                    "sharding": f"Fingerprint32(workflowID) % {NUM_SHARDS} -> greedy shard->GPU",
                    "parallelism": f"shard{world}"},
         "workflows_per_s": wf_per_s,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS,
                      "traffic": traffic["bytes_per_launch"] if traffic else None,
+                     "traffic_note": traffic_note or traffic.get("source"),
                      # HBM bytes actually moved per launch (PMC) / the live kernel time
                      "traffic_gbs": traffic["bytes_per_launch"] / (kern_ms / 1e3) / 1e9 if traffic else None,
                      "kernel": "k_replay_fast" if args.config in (1, 2) and not args.no_fast_path else "k_replay*",
@@ -497,6 +410,9 @@ def main():
         "host": {"soa_pack_s": db.pack_s, "h2d_s": db.h2d_s,
                  "h2d_gbs": db.in_bytes / max(db.h2d_s, 1e-9) / 1e9},
         "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_workflows": tot_ok,
+        "parity_checked": bool(parity) and parity["mismatched_entries_all_ranks"] == 0,
+        "parity": parity,
+        "shard_load_events": load.tolist(),
     }
     print(json.dumps(line), flush=True)
     if dist:

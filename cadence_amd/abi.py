@@ -285,6 +285,8 @@ EXPORTS = {
     "cdr_compact_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
                                 C.c_void_p, C.c_void_p]),
     "cdr_checksum_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p, C.c_void_p]),
+    "cdr_entry_digests_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
+                                      C.c_void_p, C.c_void_p]),
     "cdr_fingerprint32": (u32, [C.c_char_p, C.c_size_t]),
     "cdr_workflow_id_to_shard": (i32, [C.c_char_p, C.c_size_t, i32]),
     "cdr_last_kernel_ms": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
@@ -292,6 +294,7 @@ EXPORTS = {
     "cdr_timing_begin": (i32, [C.c_void_p, u32]),
     "cdr_timing_read": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(u32)]),
     "cdr_synth_shards": (i32, [u64, i32, C.c_void_p]),
+    "cdr_synth_weights": (i32, [C.POINTER(CdrSynthParams), u64, C.c_void_p]),
     "cdr_struct_size": (u64, [C.c_char_p]),
     "cdr_synth_size": (i32, [C.POINTER(CdrSynthParams), C.POINTER(CdrSynthSizes)]),
     "cdr_synth_fill": (i32, [C.POINTER(CdrSynthParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -89,8 +89,9 @@ __device__ uint64_t hash_bytes(uint64_t h, const void* p, uint32_t bytes) {
   return h;
 }
 
-// per-workflow hash of the whole output record set, summed (order-independent)
-__global__ void k_checksum(cdr_dev_batch B, cdr_out O, unsigned long long* sum) {
+// per-workflow hash of the whole output record set (restated by oracle/digest_ref.cpp),
+// summed (order-independent); per_entry (nullable) receives each entry's hash
+__global__ void k_digest(cdr_dev_batch B, cdr_out O, uint64_t* per_entry, unsigned long long* sum) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t h = 0;
   if (w < B.n_wfs) {
@@ -110,6 +111,7 @@ __global__ void k_checksum(cdr_dev_batch B, cdr_out O, unsigned long long* sum) 
       h = hash_bytes(h, O.rp + c.rp_off, r.n_reset_points * sizeof(cdr_reset_point));
       h = hash_bytes(h, O.sa + c.sa_off, r.n_search_attr * sizeof(cdr_kv));
     }
+    if (per_entry) per_entry[w] = h;
   }
   // wave reduction then one atomic per wave
   for (int o = 32; o > 0; o >>= 1) h += __shfl_down(h, o, 64);
@@ -165,15 +167,20 @@ int cdr_compact_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cd
   return CDR_API_OK;
 }
 
-int cdr_checksum_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, uint64_t* dev_sum, void* stream) {
+int cdr_entry_digests_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, uint64_t* per_entry,
+                            uint64_t* dev_sum, void* stream) {
   if (!ctx || !in || !out || !dev_sum) return CDR_API_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipMemsetAsync(dev_sum, 0, sizeof(uint64_t), st));
   const uint32_t blocks = (in->n_wfs + 255) / 256;
   if (blocks)
-    hipLaunchKernelGGL(k_checksum, dim3(blocks), dim3(256), 0, st, *in, *out, (unsigned long long*)dev_sum);
+    hipLaunchKernelGGL(k_digest, dim3(blocks), dim3(256), 0, st, *in, *out, per_entry, (unsigned long long*)dev_sum);
   HIPCHK(hipGetLastError());
   return CDR_API_OK;
+}
+
+int cdr_checksum_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, uint64_t* dev_sum, void* stream) {
+  return cdr_entry_digests_async(ctx, in, out, nullptr, dev_sum, stream);
 }
 
 int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot, cdr_out* out) {

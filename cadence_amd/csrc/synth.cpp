@@ -536,16 +536,52 @@ inline uint32_t global_index(const cdr_synth_params& P, uint32_t local) {
   return P.index_map ? P.index_map[local] : local;
 }
 
+// the per-workflow draws that precede generation (builder, version origin, target
+// length), from the workflow's second stream; shared by gen_one and cdr_synth_weights
+struct WfPlan {
+  int builder;
+  int64_t version;
+  uint32_t target;  // target event count of the walk (0: fixed-shape configs)
+};
+WfPlan plan_one(const cdr_synth_params& P, uint32_t w, Rng& r2) {
+  WfPlan q{};
+  q.builder = P.builder >= 0 ? P.builder : default_builder(P.config, r2);
+  const uint32_t cap = P.max_len ? P.max_len : 204800u;
+  q.version = 1;
+  if (q.builder == CDR_BUILDER_LOCAL) q.version = CDR_EMPTY_VERSION;
+  else if (q.builder == CDR_BUILDER_2DC) q.version = 1 + r2.below(3);
+  switch (P.config) {
+    case 1:
+      q.target = 11;
+      break;
+    case 2:
+      q.target = P.target_len ? 5 + 6 * ((P.target_len - 5) / 6) : 203;
+      break;
+    case 3:
+      q.target = P.target_len ? P.target_len : 200;
+      break;
+    case 4:
+      q.target = lognormal_len(r2, P.target_len ? P.target_len : 200, cap);
+      break;
+    case 5:
+      q.target = lognormal_len(r2, P.target_len ? P.target_len : 120, cap);
+      break;
+    default:
+      q.target = lognormal_len(r2, P.target_len ? P.target_len : 60, cap);
+      break;
+  }
+  return q;
+}
+
 // generate workflow `w` (pure function of params and w)
 void gen_one(const cdr_synth_params& P, uint32_t local, WfOut& o) {
   const uint32_t w = global_index(P, local);  // global workflow index
   Gen g(P, w, o);
   Rng r2(P.seed ^ cdr_mix64(0xB17D + (uint64_t)w));
-  const int builder = P.builder >= 0 ? P.builder : default_builder(P.config, r2);
+  const WfPlan q = plan_one(P, w, r2);
+  const int builder = q.builder;
   Gen* gp = &g;
-  uint32_t cap = P.max_len ? P.max_len : 204800u;
-  if (builder == CDR_BUILDER_LOCAL) g.version = CDR_EMPTY_VERSION;
-  else if (builder == CDR_BUILDER_2DC) g.version = 1 + r2.below(3);
+  g.version = q.version;
   switch (P.config) {
     case 1:
       gp->echo();
@@ -554,16 +590,16 @@ void gen_one(const cdr_synth_params& P, uint32_t local, WfOut& o) {
       gp->activity_heavy(P.target_len ? (P.target_len - 5) / 6 : 33);
       break;
     case 3:
-      gp->random_walk(P.target_len ? P.target_len : 200, false, 0.5, 1.5, 0.7);
+      gp->random_walk(q.target, false, 0.5, 1.5, 0.7);
       break;
     case 4:
-      gp->random_walk(lognormal_len(r2, P.target_len ? P.target_len : 200, cap), true, 0.6, 0.6, 1.2);
+      gp->random_walk(q.target, true, 0.6, 0.6, 1.2);
       break;
     case 5:
-      gp->random_walk(lognormal_len(r2, P.target_len ? P.target_len : 120, cap), false, 1.0, 0.8, 0.5);
+      gp->random_walk(q.target, false, 1.0, 0.8, 0.5);
       break;
     default:
-      gp->random_walk(lognormal_len(r2, P.target_len ? P.target_len : 60, cap), r2.p(0.2), 1.0, 1.0, 1.0);
+      gp->random_walk(q.target, r2.p(0.2), 1.0, 1.0, 1.0);
       break;
   }
   if (builder == CDR_BUILDER_LOCAL) {
@@ -940,6 +976,18 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
   cluster_meta(&meta->cluster);
   meta->now_ns = 1700000000000000000ll;
   meta->uuid_seed = p->seed * 0x9E3779B97F4A7C15ull + 1;
+  return CDR_API_OK;
+}
+
+// Planned event count of every workflow of the population (index_map ignored: global
+// indices 0..n-1), without generating it: the walk's target length (the generated
+// history ends within a few events of it) — the weights of the shard->GPU assignment.
+int cdr_synth_weights(const cdr_synth_params* p, uint64_t n, uint32_t* out) {
+  if (!p || !out) return CDR_API_EINVAL;
+  par((uint32_t)n, 0, [&](uint32_t w) {
+    Rng r2(p->seed ^ cdr_mix64(0xB17D + (uint64_t)w));
+    out[w] = plan_one(*p, w, r2).target;
+  });
   return CDR_API_OK;
 }
 

@@ -150,13 +150,31 @@ def default_cluster() -> abi.CdrClusterMeta:
     return c
 
 
+class SynthBuffers:
+    """Host buffers reused across synth_batch calls (chunked full-size generation):
+    grown on demand, never zero-filled (cdr_synth_fill writes every byte it hands out)."""
+
+    def __init__(self):
+        self._b = {}
+
+    def get(self, name: str, ty, n: int):
+        need = max(1, n) * C.sizeof(ty)
+        buf = self._b.get(name)
+        if buf is None or buf.nbytes < need:
+            buf = np.empty(int(need * 1.25) if name in self._b else need, np.uint8)
+            self._b[name] = buf
+        return (ty * max(1, n)).from_buffer(buf)
+
+
 def synth_batch(config: int, n_wfs: int, seed: int, target_len: int = 0, max_len: int = 0,
                 error_rate: float = 0.0, builder: int = -1, rebuild: bool = False, fault_kinds: int = 0,
-                index_map=None) -> Batch:
+                index_map=None, buffers: "SynthBuffers | None" = None) -> Batch:
     """Deterministic synthetic batch (cadence_amd/csrc/synth.cpp) in natural order.
     `index_map` (uint32 array of n_wfs global workflow indices) generates a shard's
     share of a larger population: workflow i of the batch is global workflow
-    index_map[i], identical to what the whole-population batch holds at that index."""
+    index_map[i], identical to what the whole-population batch holds at that index.
+    `buffers`: reuse these host buffers (the batch is valid until the next call with
+    the same buffers)."""
     L = abi.lib()
     p = abi.CdrSynthParams(config=config, n_wfs=n_wfs, seed=seed, target_len=target_len, max_len=max_len,
                            error_rate=error_rate, builder=builder, rebuild=1 if rebuild else 0,
@@ -169,15 +187,22 @@ def synth_batch(config: int, n_wfs: int, seed: int, target_len: int = 0, max_len
     rc = L.cdr_synth_size(C.byref(p), C.byref(sz))
     if rc:
         raise RuntimeError(f"cdr_synth_size rc={rc}")
-    ev = (abi.CdrEvent * max(1, sz.n_events))()
-    wfs = (abi.CdrWfDesc * sz.n_entries)()
-    kvs = (abi.CdrKV * max(1, sz.n_kvs))()
-    rps = (abi.CdrResetPoint * max(1, sz.n_rps))()
+    if buffers is not None:
+        ev = buffers.get("ev", abi.CdrEvent, sz.n_events)
+        wfs = buffers.get("wfs", abi.CdrWfDesc, sz.n_entries)
+        kvs = buffers.get("kvs", abi.CdrKV, sz.n_kvs)
+        rps = buffers.get("rps", abi.CdrResetPoint, sz.n_rps)
+    else:
+        ev = (abi.CdrEvent * max(1, sz.n_events))()
+        wfs = (abi.CdrWfDesc * sz.n_entries)()
+        kvs = (abi.CdrKV * max(1, sz.n_kvs))()
+        rps = (abi.CdrResetPoint * max(1, sz.n_rps))()
     cb = abi.CdrBatch()
     rc = L.cdr_synth_fill(C.byref(p), ev, wfs, kvs, rps, C.byref(cb))
     if rc:
         raise RuntimeError(f"cdr_synth_fill rc={rc}")
     ev = (abi.CdrEvent * sz.n_events).from_buffer(ev) if sz.n_events else (abi.CdrEvent * 0)()
+    wfs = (abi.CdrWfDesc * sz.n_entries).from_buffer(wfs)
     kvs = (abi.CdrKV * sz.n_kvs).from_buffer(kvs) if sz.n_kvs else (abi.CdrKV * 0)()
     rps = (abi.CdrResetPoint * sz.n_rps).from_buffer(rps) if sz.n_rps else (abi.CdrResetPoint * 0)()
     return Batch(events=ev, wfs=wfs, kvs=kvs, rps=rps, cluster=cb.cluster, now_ns=cb.now_ns,

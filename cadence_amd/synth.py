@@ -1,0 +1,178 @@
+"""Synthetic device-resident batches (benchmark and full-size parity plumbing).
+
+``DeviceBatch`` generates a deterministic synthetic population (csrc/synth.cpp, the
+SURVEY §8(d) config shapes) straight into the sliced SELL-64 layout on the host,
+uploads it to HBM with torch (device memory only: torch is plumbing here) and keeps
+device output buffers sized by the host planner.  Entry order is the natural order of
+``engine.synth_batch`` over the same ``index_map`` (each workflow followed by its
+continue-as-new run), so per-entry digests line up with the CPU restatement's.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import time
+
+import numpy as np
+
+from . import abi
+
+# SURVEY §8(d) canonical algorithmic bytes: 48 B core per event + A[type]
+A_TYPE = np.zeros(256, np.int64)
+for _name, _b in (("WorkflowExecutionStarted", 96), ("ActivityTaskScheduled", 48), ("DecisionTaskScheduled", 12),
+                  ("DecisionTaskCompleted", 12), ("TimerStarted", 8), ("StartChildWorkflowExecutionInitiated", 16),
+                  ("SignalExternalWorkflowExecutionInitiated", 12), ("DecisionTaskStarted", 4),
+                  ("ActivityTaskStarted", 4), ("DecisionTaskTimedOut", 4), ("ChildWorkflowExecutionStarted", 4),
+                  ("WorkflowExecutionContinuedAsNew", 4), ("UpsertWorkflowSearchAttributes", 8)):
+    A_TYPE[abi.EV[_name]] = _b
+ROW_BYTES = {"n_activity": 128, "n_timer": 32, "n_child": 48, "n_cancel": 24, "n_signal": 40}
+RESULT_DTYPE = np.dtype([("code", "<i4"), ("flags", "<u4"), ("fid", "<i8"), ("fix", "<i8"),
+                         ("n_activity", "<u4"), ("n_timer", "<u4"), ("n_child", "<u4"), ("n_cancel", "<u4"),
+                         ("n_signal", "<u4"), ("n_vh", "<u4"), ("n_rp", "<u4"), ("n_sa", "<u4")])
+
+
+class DeviceBatch:
+    """Synthetic batch generated straight into the sliced layout, uploaded to HBM."""
+
+    def __init__(self, torch, config, index_map, seed, target_len=0, plan_mode=abi.PLAN_WAVE):
+        L = abi.lib()
+        self.torch = torch
+        self.index_map = index_map
+        p = abi.CdrSynthParams(config=config, n_wfs=len(index_map), seed=seed, target_len=target_len, max_len=0,
+                               error_rate=0.0, builder=-1, rebuild=0, index_map=index_map.ctypes.data,
+                               plan_mode=plan_mode)
+        self.params = p
+        t0 = time.perf_counter()
+        info = abi.CdrSynthPlanInfo()
+        assert L.cdr_synth_sliced_plan(C.byref(p), C.byref(info)) == 0
+        self.info = info
+        self.h_slab = np.empty(info.n_rows * 64 * abi.EL_BYTES, np.uint8)
+        self.h_lane = np.empty(info.n_slices * 64, np.int32)
+        self.h_slen = np.empty(info.n_slices, np.uint32)
+        self.h_row0 = np.empty(info.n_slices, np.uint64)
+        self.h_sc_off = np.zeros(info.n_slices, np.uint64)
+        self.h_sc_act = np.zeros(info.n_slices, np.uint32)
+        self.h_sc_tim = np.zeros(info.n_slices, np.uint32)
+        self.h_sflags = np.zeros(info.n_slices, np.uint32)
+        self.h_arena = np.empty(max(1, info.arena_words), np.uint64)
+        self.h_wfs = (abi.CdrWfDesc * info.n_entries)()
+        self.h_caps = (abi.CdrWfCaps * info.n_entries)()
+        self.h_kvs = np.zeros(max(1, info.n_kvs) * 2, np.uint32)
+        self.h_rps = (abi.CdrResetPoint * max(1, info.n_rps))()
+        s = abi.CdrSlices(n_slices=info.n_slices, n_rows=info.n_rows, arena_words=info.arena_words)
+        s.slice_row0, s.slice_len, s.lane_wf = self.h_row0.ctypes.data, self.h_slen.ctypes.data, \
+            self.h_lane.ctypes.data
+        s.slab = self.h_slab.ctypes.data
+        s.arena = self.h_arena.ctypes.data
+        s.slice_scratch_off, s.slice_act_slots, s.slice_tim_slots = (
+            self.h_sc_off.ctypes.data, self.h_sc_act.ctypes.data, self.h_sc_tim.ctypes.data)
+        s.slice_flags = self.h_sflags.ctypes.data
+        meta = abi.CdrBatch()
+        threads = min(32, os.cpu_count() or 8)
+        rc = L.cdr_synth_sliced_fill(C.byref(p), C.byref(s), self.h_wfs, self.h_caps, self.h_kvs.ctypes.data,
+                                     self.h_rps, C.byref(meta), threads)
+        assert rc == 0, rc
+        self.meta = meta
+        self.pack_s = time.perf_counter() - t0
+        # ---- upload (H2D timed separately)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        t0 = time.perf_counter()
+        self.keep = []
+
+        def up(a):
+            t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to(dev)
+            self.keep.append(t)
+            return t.data_ptr()
+
+        def up_ct(a):
+            return up(np.frombuffer(a, np.uint8))
+
+        db = abi.CdrDevBatch()
+        db.ev.n_slices, db.ev.n_rows, db.ev.arena_words = info.n_slices, info.n_rows, info.arena_words
+        db.ev.slice_row0, db.ev.slice_len, db.ev.lane_wf = up(self.h_row0), up(self.h_slen), up(self.h_lane)
+        db.ev.slab = up(self.h_slab)
+        db.ev.arena = up(self.h_arena)
+        db.ev.slice_scratch_off = up(self.h_sc_off)
+        db.ev.slice_act_slots = up(self.h_sc_act)
+        db.ev.slice_tim_slots = up(self.h_sc_tim)
+        db.ev.slice_flags = up(self.h_sflags)
+        L.cdr_plan_scratch(self.h_caps, self.h_lane.ctypes.data, info.n_slices, None, None, None, None,
+                           C.byref(sc_words := C.c_uint64()), None)
+        self.scratch_t = torch.zeros(max(8, sc_words.value * 8), dtype=torch.uint8, device=dev)
+        db.scratch = self.scratch_t.data_ptr()
+        db.wfs, db.caps = up_ct(self.h_wfs), up_ct(self.h_caps)
+        db.kvs, db.rps = up(self.h_kvs), up_ct(self.h_rps)
+        db.n_wfs = info.n_entries
+        db.max_act_slots = int(self.h_sc_act.max()) if len(self.h_sc_act) else 0
+        db.max_tim_slots = int(self.h_sc_tim.max()) if len(self.h_sc_tim) else 0
+        self.n_fast = int(((self.h_sflags & abi.SLICE_FAST) != 0).sum())
+        self.n_wave = int(((self.h_sflags & abi.SLICE_WAVE) != 0).sum())
+        db.n_fast_slices = self.n_fast
+        db.n_wave_slices = self.n_wave
+        db.empty_uuid = meta.empty_uuid
+        db.cluster = meta.cluster
+        db.now_ns = meta.now_ns
+        db.uuid_seed = meta.uuid_seed
+        self.db = db
+        tot = info.totals
+        out = abi.CdrOut()
+        sizes = {"result": info.n_entries * C.sizeof(abi.CdrWfResult),
+                 "exec": info.n_entries * C.sizeof(abi.CdrExecInfo),
+                 "repl": info.n_entries * C.sizeof(abi.CdrReplState),
+                 "vh": tot.vh * C.sizeof(abi.CdrVHItem), "act": tot.act * C.sizeof(abi.CdrActivityInfo),
+                 "timer": tot.timer * C.sizeof(abi.CdrTimerInfo), "child": tot.child * C.sizeof(abi.CdrChildInfo),
+                 "cancel": tot.cancel * C.sizeof(abi.CdrCancelInfo),
+                 "signal": tot.signal * C.sizeof(abi.CdrSignalInfo),
+                 "rp": tot.rp * C.sizeof(abi.CdrResetPoint), "sa": tot.sa * C.sizeof(abi.CdrKV)}
+        self.out_bytes = sum(sizes.values())
+        self.out_t = {}
+        for k, nb in sizes.items():
+            t = torch.zeros(max(8, nb), dtype=torch.uint8, device=dev)
+            self.out_t[k] = t
+            setattr(out, k, t.data_ptr())
+        self.out = out
+        torch.cuda.synchronize()
+        self.h2d_s = time.perf_counter() - t0
+        self.in_bytes = self.h_slab.nbytes + self.h_arena.nbytes
+        types = abi.slab_columns(self.h_slab, self.h_row0, self.h_slen, ("type_flags",))["type_flags"] & 0xFF
+        self.type_counts = np.bincount(types, minlength=256)
+        self.n_events = int(self.type_counts[:abi.EV["UpsertWorkflowSearchAttributes"] + 1].sum())
+
+    def builders(self) -> np.ndarray:
+        """cdr_wf_desc.builder of every entry."""
+        raw = np.frombuffer(self.h_wfs, dtype=np.uint8).reshape(len(self.h_wfs), -1)
+        boff = abi.CdrWfDesc.builder.offset
+        return raw[:, boff:boff + 4].copy().view(np.uint32)[:, 0]
+
+    def digests(self, ctx, stream) -> tuple:
+        """(per-entry output digests as uint64[n_entries], their wrapping sum) of the
+        last replay, through cdr_entry_digests_async (k_digest) on `stream`."""
+        torch = self.torch
+        n = self.info.n_entries
+        per = torch.zeros(max(1, n), dtype=torch.int64, device="cuda")
+        tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+        rc = abi.lib().cdr_entry_digests_async(ctx, C.byref(self.db), C.byref(self.out), C.c_void_p(per.data_ptr()),
+                                               C.c_void_p(tot.data_ptr()), C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"cdr_entry_digests_async rc={rc}")
+        torch.cuda.synchronize()
+        return per[:n].cpu().numpy().view(np.uint64).copy(), int(tot.item()) & 0xFFFFFFFFFFFFFFFF
+
+    def results(self):
+        n = self.info.n_entries
+        raw = self.out_t["result"][: n * C.sizeof(abi.CdrWfResult)].cpu().numpy().copy()
+        return (abi.CdrWfResult * n).from_buffer(raw)
+
+    def algorithmic_bytes(self, res):
+        ev_bytes = int((self.type_counts[:42] * (48 + A_TYPE[:42])).sum())
+        n_ok, vh, rows, repl = 0, 0, 0, 0
+        arr = np.frombuffer(res, dtype=RESULT_DTYPE)
+        ok = arr["code"] == 0
+        n_ok = int(ok.sum())
+        vh = int(arr["n_vh"][ok].sum())
+        for f, b in ROW_BYTES.items():
+            rows += int(arr[f][ok].sum()) * b
+        bld = self.builders()
+        repl = int(((bld == abi.BUILDER_2DC) & ok).sum()) * 32
+        wf_bytes = len(arr) * (256 + 8) + 16 * vh + repl
+        return ev_bytes + wf_bytes + rows, n_ok, ev_bytes, wf_bytes, rows

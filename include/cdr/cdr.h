@@ -350,6 +350,14 @@ int cdr_compact_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cd
  * multi-GPU driver.  Writes one u64 to `*dev_sum` (device memory). */
 int cdr_checksum_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, uint64_t* dev_sum,
                        void* stream);
+/* The same, plus each entry's hash in per_entry[n_wfs] (device memory, nullable): the
+ * full-size parity check compares these entry by entry with the CPU restatement's
+ * (oracle/digest_ref.cpp restates the hash).  Hash of entry w: a fold of cdr_mix64 over
+ * (code | flags << 32), fail_event_id and, when OK, the 8-byte words of its ExecutionInfo,
+ * ReplicationState (2DC builder), version-history items, pending rows, reset points and
+ * search attributes — the CopyToPersistence projection (mutableStateBuilder.go:257-270). */
+int cdr_entry_digests_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, uint64_t* per_entry,
+                            uint64_t* dev_sum, void* stream);
 
 /* ------------------------------------------------------------------ misc */
 

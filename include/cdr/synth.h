@@ -39,6 +39,9 @@ int cdr_synth_fill(const cdr_synth_params* p, cdr_event* ev, cdr_wf_desc* wfs, c
 int cdr_synth_sliced_plan(const cdr_synth_params* p, cdr_synth_plan_info* info);
 int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc* wfs, cdr_wf_caps* caps,
                           cdr_kv* kvs, cdr_reset_point* rps, cdr_batch* meta, int threads);
+/* planned event count of workflows 0..n-1 (the walk's target length, drawn without
+ * generating the histories): weights of the bench's shard->GPU assignment */
+int cdr_synth_weights(const cdr_synth_params* p, uint64_t n, uint32_t* out);
 /* history shard of synthetic workflow ids "wf-<i>", i in [0, n): farmhash
  * Fingerprint32 % num_shards (common/util.go:249-252) */
 int cdr_synth_shards(uint64_t n, int32_t num_shards, int32_t* out);

@@ -36,6 +36,9 @@ def lib():
                                             C.c_int64, C.c_int64]
         L.cdro_state_transition.restype = C.c_int
         L.cdro_state_transition.argtypes = [C.c_int] * 4
+        L.cdro_entry_digests.restype = C.c_int
+        L.cdro_entry_digests.argtypes = [C.POINTER(abi.CdrBatch), C.POINTER(abi.CdrWfCaps), C.POINTER(abi.CdrOut),
+                                         C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
         _lib = L
     return _lib
 
@@ -66,3 +69,43 @@ def rebuild(batch, pl=None, advanced_visibility: bool = True, snapshot: bool = F
     if rc:
         raise RuntimeError(f"cdro_refresh_tasks rc={rc}")
     return out
+
+
+def entry_digests(batch, pl, out, threads: int = 1):
+    """(per-entry digests uint64[n_wfs], wrapping sum) of oracle outputs — the restated
+    k_digest hash (digest_ref.cpp)."""
+    import numpy as np
+    per = np.zeros(max(1, batch.n_wfs), np.uint64)
+    tot = C.c_uint64()
+    rc = lib().cdro_entry_digests(C.byref(batch.cstruct()), pl.caps, C.byref(out.cstruct()), per.ctypes.data,
+                                  C.byref(tot), threads)
+    if rc:
+        raise RuntimeError(f"cdro_entry_digests rc={rc}")
+    return per[:batch.n_wfs], tot.value
+
+
+def synth_digests(config: int, index_map, seed: int, threads: int = 16, chunk: int = 65536, **kw):
+    """Oracle digests of a synthetic population at full size: the workflows of
+    `index_map` (global indices, in order) generated in natural order chunk by chunk,
+    replayed by the restatement on `threads` host threads and hashed entry by entry.
+    Returns (per-entry digests in cadence_amd.synth.DeviceBatch's entry order, sum,
+    {status name: count})."""
+    import numpy as np
+    from cadence_amd import abi, engine
+    index_map = np.ascontiguousarray(index_map, dtype=np.uint32)
+    parts, total, hist = [], 0, {}
+    bufs = engine.SynthBuffers()
+    for i in range(0, len(index_map), chunk):
+        im = index_map[i:i + chunk]
+        b = engine.synth_batch(config, len(im), seed, index_map=im, buffers=bufs, **kw)
+        pl = engine.plan(b)
+        out = replay(b, pl, threads=threads)
+        per, s = entry_digests(b, pl, out, threads)
+        parts.append(per)
+        total = (total + s) & 0xFFFFFFFFFFFFFFFF
+        codes = np.frombuffer(out.result, dtype=np.int32).reshape(-1, C.sizeof(abi.CdrWfResult) // 4)[:b.n_wfs, 0]
+        for v, c in zip(*np.unique(codes, return_counts=True)):
+            k = abi.STATUS.get(int(v), str(int(v)))
+            hist[k] = hist.get(k, 0) + int(c)
+        del b, pl, out
+    return (np.concatenate(parts) if parts else np.zeros(0, np.uint64)), total, hist

@@ -10,6 +10,7 @@ shift; [ $# -gt 0 ] && shift
 extra="$*"
 out=gpurun_out/${tag}_pmc
 mkdir -p "$out"
+sha1sum "$lib" | cut -d' ' -f1 > "$out/lib_sha1"  # bench.py uses the summary only for this build
 export TMPDIR=/tmp
 run() {  # name counters...
   local name=$1; shift

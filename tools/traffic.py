@@ -33,6 +33,9 @@ def main():
     waves = avg.get("SQ_WAVES", 0)
     out = {"workload": workload, "kernel": kern, "source": f"rocprofv3 --pmc passes, tools/pmc.sh ({tag})",
            "counters": avg}
+    sha = os.path.join(ROOT, "gpurun_out", f"{tag}_pmc", "lib_sha1")
+    if os.path.exists(sha):
+        out["lib_sha1"] = open(sha).read().strip()
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         rd = avg["FETCH_SIZE"] * 1024 * 2
         wr = avg["WRITE_SIZE"] * 1024
