@@ -51,7 +51,9 @@ STATUS = {
     7: "E_DECISION_NOT_FOUND", 8: "E_ACTIVITY_NOT_FOUND", 9: "E_ACTIVITY_ID_NOT_FOUND",
     10: "E_MISSING_ACTIVITY_INFO", 11: "E_DOMAIN_NOT_FOUND", 12: "E_REBUILD_NEXT_EVENT_ID",
     13: "E_BAD_INPUT", 14: "E_REFRESH_EVENT_NOT_FOUND", 15: "E_REFRESH_BACKOFF_INITIATOR",
-    16: "E_REFRESH_CAPACITY", 32: "P_ACTIVITY_STARTED_NIL", 33: "P_CHILD_STARTED_NIL",
+    16: "E_REFRESH_CAPACITY", 17: "E_VH_NO_LCA", 18: "E_VH_LCA_NOT_CONTAINED", 19: "E_VH_FIRST_ITEM_MISMATCH",
+    20: "E_NDC_RETRY_TASK", 21: "E_NDC_BRANCH_CHANGED", 22: "E_NDC_SAME_VERSION", 23: "E_REBUILD_VH_MISMATCH",
+    24: "E_VHS_CAPACITY", 25: "E_VH_EMPTY", 32: "P_ACTIVITY_STARTED_NIL", 33: "P_CHILD_STARTED_NIL",
     34: "P_VH_ITEM_INVALID", 35: "P_UNKNOWN_CLUSTER", 64: "NOT_APPLIED",
 }
 OK = 0

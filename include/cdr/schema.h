@@ -162,6 +162,16 @@ enum cdr_status {
   CDR_E_REFRESH_BACKOFF_INITIATOR = 15, /* generateDelayedDecisionTasks InternalServiceError
                                            mutableStateTaskGenerator.go:197-205 */
   CDR_E_REFRESH_CAPACITY = 16,      /* task slice of the entry too small (caller sized it) */
+  /* NDC branch management / conflict-resolution rebuild (cdr_ndc_branch_async, ndc.hip) */
+  CDR_E_VH_NO_LCA = 17,             /* FindLCAItem "No joint point found" versionHistory.go:285-288 */
+  CDR_E_VH_LCA_NOT_CONTAINED = 18,  /* DuplicateUntilLCAItem versionHistory.go:158-186 */
+  CDR_E_VH_FIRST_ITEM_MISMATCH = 19, /* AddVersionHistory versionHistory.go:463-465 */
+  CDR_E_NDC_RETRY_TASK = 20,        /* verifyEventsOrder gap nDCBranchMgr.go:188-190 */
+  CDR_E_NDC_BRANCH_CHANGED = 21,    /* createNewBranch nDCBranchMgr.go:242-246 */
+  CDR_E_NDC_SAME_VERSION = 22,      /* prepareMutableState nDCConflictResolver.go:100-105 */
+  CDR_E_REBUILD_VH_MISMATCH = 23,   /* rebuilt VH != branch VH nDCConflictResolver.go:154-165 */
+  CDR_E_VHS_CAPACITY = 24,          /* branch / item slots exhausted (caller-planned) */
+  CDR_E_VH_EMPTY = 25,              /* GetFirstItem / GetLastItem on an empty history :399-420 */
   CDR_P_ACTIVITY_STARTED_NIL = 32,  /* nil deref mutableStateBuilder.go:2089-2091 */
   CDR_P_CHILD_STARTED_NIL = 33,     /* nil deref mutableStateBuilder.go:3319-3320 */
   CDR_P_VH_ITEM_INVALID = 34,       /* NewVersionHistoryItem panic versionHistory.go:36-42 */
@@ -604,6 +614,62 @@ typedef struct cdr_carry {
   cdr_totals totals;       /* rows in each table of `state` */
   cdr_out state;           /* read only */
 } cdr_carry;
+
+/* ==================================================== NDC VERSION HISTORIES ===
+ * The persisted VersionHistories of an NDC workflow (common/persistence/versionHistory.go:
+ * VersionHistories{currentVersionHistoryIndex, histories []*VersionHistory}), one branch
+ * per fork of the history tree.  A branch token is the history tree's branch token
+ * (TreeID = run handle, BranchID = 128-bit UUID; dataInterfaces.go:2428-2440), compared
+ * by value.  The items of branch b of a workflow live at
+ * items[vhs.items_off + b * vhs.items_cap ...] (caller-planned capacity). */
+#define CDR_VHS_MAX_BRANCHES 8
+typedef struct cdr_vh_token {
+  uint32_t tree, _pad;
+  uint64_t branch_lo, branch_hi;
+} cdr_vh_token;
+typedef struct cdr_vh_branch { /* one VersionHistory */
+  cdr_vh_token token;
+  uint32_t n_items, _pad;
+} cdr_vh_branch;
+typedef struct cdr_vhs { /* VersionHistories */
+  uint32_t current, n_branches;
+  uint32_t items_cap, _pad;
+  uint64_t items_off;
+  cdr_vh_branch branch[CDR_VHS_MAX_BRANCHES];
+} cdr_vhs;
+
+/* One NDC replication task as nDCBranchMgr.prepareVersionHistory and
+ * nDCConflictResolver.prepareMutableState see it (nDCBranchMgr.go:80-125,
+ * nDCConflictResolver.go:73-114): the incoming VersionHistory (task.getVersionHistory(),
+ * its items in the task item pool), the first / last event and the task's version, and
+ * the token ForkHistoryBranch would return if a branch has to be created
+ * (nDCBranchMgr.go:205-240, host-supplied). */
+typedef struct cdr_ndc_task {
+  uint64_t items_off;
+  uint32_t n_items, _pad;
+  int64_t first_event_id;
+  int64_t last_event_id, last_version;
+  int64_t version;
+  cdr_vh_token new_token;
+} cdr_ndc_task;
+
+/* What the replicator does with the task (nDCHistoryReplicator.go:295-470) */
+enum cdr_ndc_action {
+  CDR_NDC_SKIP = 0,          /* duplicate task: verifyEventsOrder returned doContinue = false */
+  CDR_NDC_APPLY_CURRENT = 1, /* branch is the current one: applyEvents onto the mutable state */
+  CDR_NDC_REBUILD = 2,       /* rebuild the branch (nDCStateRebuilder, events 1 .. rebuild_next-1),
+                                then applyEvents onto the rebuilt state */
+  CDR_NDC_BACKFILL = 3       /* non-current branch, lower version: branch VH AddOrUpdateItem(last
+                                event) only, mutable state unchanged */
+};
+typedef struct cdr_ndc_decision {
+  int32_t code;   /* cdr_status (CDR_OK or the Go error site) */
+  int32_t action; /* cdr_ndc_action */
+  uint32_t branch_index, created; /* target branch; 1 if createNewBranch ran */
+  int64_t rebuild_next_event_id;  /* REBUILD: baseNextEventID = branch lastItem.EventID + 1 */
+  cdr_vh_item lca;                /* FindLCAVersionHistoryIndexAndItem's item */
+  cdr_vh_token rebuild_token;     /* REBUILD: the branch's token (SetCurrentBranchToken target) */
+} cdr_ndc_decision;
 
 #ifdef __cplusplus
 }
