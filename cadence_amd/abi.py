@@ -57,6 +57,7 @@ STATUS = {
     34: "P_VH_ITEM_INVALID", 35: "P_UNKNOWN_CLUSTER", 64: "NOT_APPLIED",
 }
 OK = 0
+E_HISTORY_EMPTY = 1
 RF_IN_NEWRUN, RF_IS_NEWRUN, RF_NEWRUN_APPLIED = 1, 2, 4
 
 SF_HAS_PARENT_DOMAIN, SF_PARENT_DOMAIN_MISSING, SF_HAS_PARENT_EXEC = 0x1, 0x2, 0x4
@@ -187,6 +188,19 @@ CdrTotals = _S("cdr_totals", [(n, u64) for n in ("act", "timer", "child", "cance
 CdrOut = _S("cdr_out", [(n, C.c_void_p) for n in (
     "result", "exec", "repl", "vh", "act", "timer", "child", "cancel", "signal", "rp", "sa", "transfer",
     "timer_tasks", "n_tasks")])
+CdrVHToken = _S("cdr_vh_token", [("tree", u32), ("_pad", u32), ("branch_lo", u64), ("branch_hi", u64)])
+CdrVHBranch = _S("cdr_vh_branch", [("token", CdrVHToken), ("n_items", u32), ("_pad", u32)])
+VHS_MAX_BRANCHES = 8
+CdrVHS = _S("cdr_vhs", [("current", u32), ("n_branches", u32), ("items_cap", u32), ("_pad", u32),
+                        ("items_off", u64), ("branch", CdrVHBranch * VHS_MAX_BRANCHES)])
+CdrNdcTask = _S("cdr_ndc_task", [("items_off", u64), ("n_items", u32), ("_pad", u32), ("first_event_id", i64),
+                                 ("last_event_id", i64), ("last_version", i64), ("version", i64),
+                                 ("new_token", CdrVHToken)])
+CdrNdcDecision = _S("cdr_ndc_decision", [("code", i32), ("action", i32), ("branch_index", u32), ("created", u32),
+                                         ("rebuild_next_event_id", i64), ("lca", CdrVHItem),
+                                         ("rebuild_token", CdrVHToken)])
+NDC_SKIP, NDC_APPLY_CURRENT, NDC_REBUILD, NDC_BACKFILL = range(4)
+NDC_ACTIONS = {0: "SKIP", 1: "APPLY_CURRENT", 2: "REBUILD", 3: "BACKFILL"}
 CdrTask = _S("cdr_task", [("type", u32), ("timeout_type", i32), ("event_id", i64), ("visibility_ts", i64),
                           ("attempt", i64), ("domain_id", u32), ("task_list", u32), ("target_workflow_id", u32),
                           ("target_run_id", u32), ("flags", u32), ("_pad", u32),
@@ -240,7 +254,9 @@ CdrDevBatch = _S("cdr_dev_batch", [
 # ------------------------------------------------------------------ synth
 CdrSynthParams = _S("cdr_synth_params", [
     ("config", i32), ("n_wfs", u32), ("seed", u64), ("target_len", u32), ("max_len", u32), ("error_rate", f64),
-    ("builder", i32), ("rebuild", i32), ("fault_kinds", u32), ("plan_mode", u32), ("index_map", C.c_void_p)])
+    ("builder", i32), ("rebuild", i32), ("fault_kinds", u32), ("plan_mode", u32), ("index_map", C.c_void_p),
+    ("ndc_part", u32), ("_pad2", u32)])
+SYNTH_PART_BASE, SYNTH_PART_REBUILD, SYNTH_PART_FORK_A, SYNTH_PART_FORK_B = range(4)
 # synth fault kinds that keep a sequential-activity history on the fast path (synth.cpp inject_fault)
 FAULTS_FAST = (1 << 1) | (1 << 2) | (1 << 3) | (1 << 5) | (1 << 6)
 CdrSynthSizes = _S("cdr_synth_sizes", [("n_events", u64), ("n_entries", u32), ("_pad", u32), ("n_kvs", u64),
@@ -257,7 +273,8 @@ MIRRORS = {
     "cdr_child_info": CdrChildInfo, "cdr_cancel_info": CdrCancelInfo, "cdr_signal_info": CdrSignalInfo,
     "cdr_wf_result": CdrWfResult, "cdr_wf_caps": CdrWfCaps, "cdr_totals": CdrTotals, "cdr_out": CdrOut,
     "cdr_slices": CdrSlices, "cdr_dev_batch": CdrDevBatch, "cdr_carry": CdrCarry,
-    "cdr_task": CdrTask,
+    "cdr_task": CdrTask, "cdr_vh_token": CdrVHToken, "cdr_vh_branch": CdrVHBranch, "cdr_vhs": CdrVHS,
+    "cdr_ndc_task": CdrNdcTask, "cdr_ndc_decision": CdrNdcDecision,
 }
 
 # C ABI entry points declared in include/cdr/cdr.h and include/cdr/synth.h
@@ -289,6 +306,12 @@ EXPORTS = {
     "cdr_checksum_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p, C.c_void_p]),
     "cdr_entry_digests_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
                                       C.c_void_p, C.c_void_p]),
+    "cdr_ndc_branch_async": (i32, [C.c_void_p, C.c_void_p, C.c_void_p, u32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_void_p]),
+    "cdr_ndc_rebuild_verify_async": (i32, [C.c_void_p, u32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.POINTER(CdrOut), C.c_void_p]),
+    "cdr_vhs_sync_async": (i32, [C.c_void_p, u32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(CdrOut),
+                                 C.c_void_p]),
     "cdr_fingerprint32": (u32, [C.c_char_p, C.c_size_t]),
     "cdr_workflow_id_to_shard": (i32, [C.c_char_p, C.c_size_t, i32]),
     "cdr_last_kernel_ms": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
@@ -297,6 +320,7 @@ EXPORTS = {
     "cdr_timing_read": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(u32)]),
     "cdr_synth_shards": (i32, [u64, i32, C.c_void_p]),
     "cdr_synth_weights": (i32, [C.POINTER(CdrSynthParams), u64, C.c_void_p]),
+    "cdr_synth_ndc_tasks": (i32, [C.POINTER(CdrSynthParams), i32, C.c_void_p, C.c_void_p, u32]),
     "cdr_struct_size": (u64, [C.c_char_p]),
     "cdr_synth_size": (i32, [C.POINTER(CdrSynthParams), C.POINTER(CdrSynthSizes)]),
     "cdr_synth_fill": (i32, [C.POINTER(CdrSynthParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -787,6 +787,11 @@ uint64_t cdr_struct_size(const char* name) {
       {"cdr_dev_batch", sizeof(cdr_dev_batch)},
       {"cdr_carry", sizeof(cdr_carry)},
       {"cdr_task", sizeof(cdr_task)},
+      {"cdr_vh_token", sizeof(cdr_vh_token)},
+      {"cdr_vh_branch", sizeof(cdr_vh_branch)},
+      {"cdr_vhs", sizeof(cdr_vhs)},
+      {"cdr_ndc_task", sizeof(cdr_ndc_task)},
+      {"cdr_ndc_decision", sizeof(cdr_ndc_decision)},
   };
   for (const E& e : table)
     if (std::strcmp(e.n, name) == 0) return e.s;

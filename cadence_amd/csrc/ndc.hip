@@ -1,0 +1,309 @@
+// ndc.hip — NDC branch management and conflict-resolution rebuild bookkeeping.
+//
+// When a replication task forks a workflow's history, the history
+// service decides per task, before any replay (paths relative to /root/reference):
+//   nDCBranchMgr.prepareVersionHistory       service/history/nDCBranchMgr.go:80-249
+//     FindLCAVersionHistoryIndexAndItem / IsLCAAppendable / DuplicateUntilLCAItem /
+//     AddVersionHistory                      common/persistence/versionHistory.go:152-520
+//   nDCConflictResolver.prepareMutableState   service/history/nDCConflictResolver.go:73-114
+// and, after the stateRebuilder replay of a branch (cdr_replay_* with
+// expected_next_event_id = the branch's last item + 1), verifies the rebuilt version
+// history against the branch's (nDCConflictResolver.go:154-165) and switches the current
+// branch (:172-174).  These kernels do that bookkeeping for a whole batch of workflows,
+// one thread per workflow: the work is a few dozen version-history items per workflow
+// (no events), so it is latency-, not bandwidth-bound; what matters is that it runs on
+// the device next to the replays it routes, with no host round trip per workflow.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "cdr/cdr.h"
+
+#define HIPCHK(x)                                                                                     \
+  do {                                                                                                \
+    hipError_t _e = (x);                                                                              \
+    if (_e != hipSuccess) {                                                                           \
+      fprintf(stderr, "cdr: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(_e), __FILE__, __LINE__); \
+      return CDR_API_EDEVICE;                                                                         \
+    }                                                                                                 \
+  } while (0)
+
+extern "C" int cdr_ctx_device(const cdr_ctx* ctx);  // replay.hip
+
+namespace {
+
+struct It {
+  int64_t e, v;
+};
+__device__ __forceinline__ It ld(const cdr_vh_item* p) {
+  const cdr_vh_item x = *p;
+  return It{x.event_id, x.version};
+}
+__device__ __forceinline__ bool tok_eq(const cdr_vh_token& a, const cdr_vh_token& b) {
+  return a.tree == b.tree && a.branch_lo == b.branch_lo && a.branch_hi == b.branch_hi;
+}
+
+// FindLCAItem (versionHistory.go:262-290): walk both histories back from their last items
+__device__ int32_t find_lca(const cdr_vh_item* a, uint32_t na, const cdr_vh_item* b, uint32_t nb, It* out) {
+  int li = (int)na - 1, ri = (int)nb - 1;
+  while (li >= 0 && ri >= 0) {
+    const It l = ld(a + li), r = ld(b + ri);
+    if (l.v == r.v) {
+      *out = l.e > r.e ? r : l;
+      return CDR_OK;
+    }
+    if (l.v > r.v) li--;
+    else ri--;
+  }
+  return CDR_E_VH_NO_LCA;
+}
+
+// AddOrUpdateItem (versionHistory.go:203-236) onto a history whose items live at dst
+// (count n, last item in `last`); items past `cap` are tracked but not stored
+__device__ int32_t add_or_update(cdr_vh_item* dst, uint32_t cap, uint32_t* n, It* last, It it, bool* over) {
+  if (*n == 0) {
+    if (cap > 0) dst[0] = cdr_vh_item{it.e, it.v};
+    else *over = true;
+    *n = 1;
+    *last = it;
+    return CDR_OK;
+  }
+  if (it.v < last->v) return CDR_E_VH_LOWER_VERSION;
+  if (it.e <= last->e) return CDR_E_VH_LOWER_EVENT_ID;
+  if (it.v > last->v) {
+    if (*n < cap) dst[*n] = cdr_vh_item{it.e, it.v};
+    else *over = true;
+    (*n)++;
+  } else if (*n <= cap) {
+    dst[*n - 1].event_id = it.e;
+  }
+  *last = it;
+  return CDR_OK;
+}
+
+__device__ int32_t branch_one(const cdr_ndc_task& t, const cdr_vh_item* ti, cdr_vhs& s, cdr_vh_item* pool,
+                              cdr_ndc_decision& d) {
+  const cdr_vh_item* inc = ti + t.items_off;
+  const uint32_t ni = t.n_items;
+  cdr_vh_item* base = pool + s.items_off;
+  const uint32_t cap = s.items_cap;
+  // FindLCAVersionHistoryIndexAndItem (versionHistory.go:489-520)
+  uint32_t idx = 0, len = 0;
+  It lca{0, 0};
+  bool set = false;
+  for (uint32_t b = 0; b < s.n_branches; b++) {
+    It it;
+    const int32_t rc = find_lca(base + (uint64_t)b * cap, s.branch[b].n_items, inc, ni, &it);
+    if (rc) return rc;
+    if (!set || it.e > lca.e || (it.e == lca.e && s.branch[b].n_items < len)) {
+      set = true;
+      idx = b;
+      len = s.branch[b].n_items;
+      lca = it;
+    }
+  }
+  if (!set) return CDR_E_VH_NO_LCA;  // no branch at all: NewVersionHistories never ran
+  d.lca = cdr_vh_item{lca.e, lca.v};
+  const cdr_vh_item* src = base + (uint64_t)idx * cap;
+  const uint32_t ns = s.branch[idx].n_items;
+  uint32_t branch = idx, n_br = s.n_branches, cur = s.current;
+  bool over = false;
+  uint32_t tgt_n = ns;  // target branch's item count after the task
+  It tgt_last = ns ? ld(src + ns - 1) : It{0, 0};
+  cdr_vh_item* tgt = base + (uint64_t)idx * cap;
+  bool created = false;
+  if (ns > 0 && tgt_last.e == lca.e && tgt_last.v == lca.v) {  // IsLCAAppendable
+    const int64_t next = tgt_last.e + 1;                        // verifyEventsOrder :171-193
+    if (t.first_event_id < next) {
+      d.action = CDR_NDC_SKIP;
+      d.branch_index = idx;
+      return CDR_OK;
+    }
+    if (t.first_event_id > next) return CDR_E_NDC_RETRY_TASK;
+  } else {
+    // DuplicateUntilLCAItem (versionHistory.go:152-186) into the next branch slot
+    const uint32_t nb = s.n_branches;
+    const bool slot = nb < CDR_VHS_MAX_BRANCHES;
+    cdr_vh_item* dst = base + (uint64_t)nb * cap;
+    uint32_t n = 0;
+    It last{0, 0}, first{0, 0};
+    bool found = false;
+    for (uint32_t i = 0; i < ns && !found; i++) {
+      const It it = ld(src + i);
+      if (n == 0) first = it.v < lca.v ? it : lca;
+      int32_t rc;
+      if (it.v < lca.v) {
+        rc = add_or_update(dst, slot ? cap : 0, &n, &last, it, &over);
+      } else if (it.v == lca.v) {
+        if (lca.e > it.e) return CDR_E_VH_LCA_NOT_CONTAINED;
+        rc = add_or_update(dst, slot ? cap : 0, &n, &last, lca, &over);
+        found = true;
+      } else {
+        return CDR_E_VH_LCA_NOT_CONTAINED;
+      }
+      if (rc) return rc;
+    }
+    if (!found) return CDR_E_VH_LCA_NOT_CONTAINED;
+    const int64_t next = last.e + 1;
+    if (t.first_event_id < next) {  // doContinue = false
+      d.action = CDR_NDC_SKIP;
+      d.branch_index = idx;
+      return CDR_OK;
+    }
+    if (t.first_event_id > next) return CDR_E_NDC_RETRY_TASK;
+    // createNewBranch (nDCBranchMgr.go:195-249) -> AddVersionHistory (versionHistory.go:438-487)
+    const cdr_vh_branch& cb = s.branch[cur];
+    const uint32_t cn = cb.n_items;
+    if (cn == 0) return CDR_E_VH_EMPTY;
+    const cdr_vh_item* cur_items = base + (uint64_t)cur * cap;
+    if (first.v != ld(cur_items).v) return CDR_E_VH_FIRST_ITEM_MISMATCH;
+    if (last.v > ld(cur_items + cn - 1).v) return CDR_E_NDC_BRANCH_CHANGED;  // the index switch is an error here
+    if (!slot) over = true;
+    branch = nb;
+    n_br = nb + 1;
+    tgt = dst;
+    tgt_n = n;
+    tgt_last = last;
+    created = true;
+  }
+  // prepareMutableState (nDCConflictResolver.go:73-114)
+  if (branch == cur) {
+    d.action = CDR_NDC_APPLY_CURRENT;
+  } else {
+    const uint32_t cn = s.branch[cur].n_items;
+    if (cn == 0) return CDR_E_VH_EMPTY;
+    const It cur_last = ld(base + (uint64_t)cur * cap + cn - 1);
+    if (t.version < cur_last.v) {
+      // applyNonStartEventsToNoneCurrentBranch: the branch's VH gets the last event
+      const int32_t rc = add_or_update(tgt, branch < CDR_VHS_MAX_BRANCHES ? cap : 0, &tgt_n, &tgt_last,
+                                       It{t.last_event_id, t.last_version}, &over);
+      if (rc) return rc;
+      d.action = CDR_NDC_BACKFILL;
+    } else if (t.version == cur_last.v) {
+      return CDR_E_NDC_SAME_VERSION;
+    } else {
+      if (tgt_n == 0) return CDR_E_VH_EMPTY;
+      d.action = CDR_NDC_REBUILD;
+      d.rebuild_next_event_id = tgt_last.e + 1;
+      d.rebuild_token = created ? t.new_token : s.branch[branch].token;
+    }
+  }
+  if (over) return CDR_E_VHS_CAPACITY;
+  // commit
+  d.branch_index = branch;
+  d.created = created ? 1u : 0u;
+  if (created) {
+    s.branch[branch].token = t.new_token;
+    s.branch[branch]._pad = 0;
+  }
+  s.branch[branch].n_items = tgt_n;
+  s.n_branches = n_br;
+  return CDR_OK;
+}
+
+__global__ __launch_bounds__(256) void k_ndc_branch(const cdr_ndc_task* tasks, const cdr_vh_item* task_items,
+                                                    uint32_t n, cdr_vhs* vhs, cdr_vh_item* pool,
+                                                    cdr_ndc_decision* dec) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n) return;
+  const cdr_ndc_task t = tasks[w];
+  cdr_vhs& s = vhs[w];
+  cdr_ndc_decision d{};
+  const int32_t rc = branch_one(t, task_items, s, pool, d);
+  if (rc) {
+    d = cdr_ndc_decision{};
+    d.code = rc;
+  }
+  dec[w] = d;
+}
+
+__global__ __launch_bounds__(256) void k_ndc_rebuild_verify(uint32_t n, const cdr_ndc_decision* dec, cdr_vhs* vhs,
+                                                            const cdr_vh_item* pool, const cdr_wf_caps* caps,
+                                                            cdr_out O) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n) return;
+  const cdr_ndc_decision d = dec[w];
+  if (d.code != CDR_OK || d.action != CDR_NDC_REBUILD) return;
+  cdr_wf_result& r = O.result[w];
+  if (r.code != CDR_OK) return;
+  cdr_exec_info& x = O.exec[w];  // SetCurrentBranchToken(target) (nDCStateRebuilder.go:144-146)
+  x.branch_tree_id = d.rebuild_token.tree;
+  x.branch_id_lo = d.rebuild_token.branch_lo;
+  x.branch_id_hi = d.rebuild_token.branch_hi;
+  cdr_vhs& s = vhs[w];
+  const cdr_vh_branch& b = s.branch[d.branch_index];
+  const cdr_vh_item* want = pool + s.items_off + (uint64_t)d.branch_index * s.items_cap;
+  const cdr_vh_item* got = O.vh + caps[w].vh_off;
+  bool eq = b.n_items == r.n_vh && tok_eq(b.token, d.rebuild_token);
+  for (uint32_t i = 0; eq && i < r.n_vh; i++) eq = got[i].event_id == want[i].event_id && got[i].version == want[i].version;
+  if (!eq) {  // nDCConflictResolver.go:161-165
+    r.code = CDR_E_REBUILD_VH_MISMATCH;
+    r.fail_event_id = 0;
+    r.fail_index = 0;
+    r.n_activity = r.n_timer = r.n_child = r.n_cancel = r.n_signal = 0;
+    r.n_vh = r.n_reset_points = r.n_search_attr = 0;
+    return;
+  }
+  s.current = d.branch_index;  // SetCurrentVersionHistoryIndex (:172-174)
+}
+
+__global__ __launch_bounds__(256) void k_vhs_sync(uint32_t n, cdr_vhs* vhs, cdr_vh_item* pool,
+                                                  const cdr_wf_caps* caps, cdr_out O) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n) return;
+  const cdr_wf_result& r = O.result[w];
+  if (r.code != CDR_OK) return;
+  cdr_vhs& s = vhs[w];
+  if (r.n_vh > s.items_cap) return;
+  if (s.n_branches == 0) {  // NewVersionHistories (versionHistory.go:350-363)
+    s.n_branches = 1;
+    s.current = 0;
+  }
+  cdr_vh_branch& b = s.branch[s.current];
+  const cdr_exec_info& x = O.exec[w];
+  b.token.tree = x.branch_tree_id;
+  b.token._pad = 0;
+  b.token.branch_lo = x.branch_id_lo;
+  b.token.branch_hi = x.branch_id_hi;
+  b.n_items = r.n_vh;
+  b._pad = 0;
+  cdr_vh_item* dst = pool + s.items_off + (uint64_t)s.current * s.items_cap;
+  const cdr_vh_item* src = O.vh + caps[w].vh_off;
+  for (uint32_t i = 0; i < r.n_vh; i++) dst[i] = src[i];
+}
+
+}  // namespace
+
+extern "C" {
+
+int cdr_ndc_branch_async(cdr_ctx* ctx, const cdr_ndc_task* tasks, const cdr_vh_item* task_items, uint32_t n,
+                         cdr_vhs* vhs, cdr_vh_item* pool, cdr_ndc_decision* dec, void* stream) {
+  if (!ctx || (n && (!tasks || !task_items || !vhs || !pool || !dec))) return CDR_API_EINVAL;
+  HIPCHK(hipSetDevice(cdr_ctx_device(ctx)));
+  if (n) hipLaunchKernelGGL(k_ndc_branch, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, tasks, task_items,
+                            n, vhs, pool, dec);
+  HIPCHK(hipGetLastError());
+  return CDR_API_OK;
+}
+
+int cdr_ndc_rebuild_verify_async(cdr_ctx* ctx, uint32_t n, const cdr_ndc_decision* dec, cdr_vhs* vhs,
+                                 const cdr_vh_item* pool, const cdr_wf_caps* caps, const cdr_out* out, void* stream) {
+  if (!ctx || !out || (n && (!dec || !vhs || !pool || !caps))) return CDR_API_EINVAL;
+  HIPCHK(hipSetDevice(cdr_ctx_device(ctx)));
+  if (n) hipLaunchKernelGGL(k_ndc_rebuild_verify, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, dec,
+                            vhs, pool, caps, *out);
+  HIPCHK(hipGetLastError());
+  return CDR_API_OK;
+}
+
+int cdr_vhs_sync_async(cdr_ctx* ctx, uint32_t n, cdr_vhs* vhs, cdr_vh_item* pool, const cdr_wf_caps* caps,
+                       const cdr_out* out, void* stream) {
+  if (!ctx || !out || (n && (!vhs || !pool || !caps))) return CDR_API_EINVAL;
+  HIPCHK(hipSetDevice(cdr_ctx_device(ctx)));
+  if (n) hipLaunchKernelGGL(k_vhs_sync, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, vhs, pool, caps,
+                            *out);
+  HIPCHK(hipGetLastError());
+  return CDR_API_OK;
+}
+
+}  // extern "C"

@@ -1745,6 +1745,7 @@ int cdr_set_plan_mode(cdr_ctx* c, uint32_t mode) {
   return (int)old;
 }
 uint32_t cdr_get_plan_mode(const cdr_ctx* c) { return c ? c->plan_mode : 0u; }
+int cdr_ctx_device(const cdr_ctx* c) { return c ? c->device : 0; }
 
 void cdr_destroy(cdr_ctx* c) {
   if (!c) return;

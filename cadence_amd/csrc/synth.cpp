@@ -78,6 +78,10 @@ struct WfOut {
   bool has_newrun = false;
   uint32_t newrun_call = 0;
   bool newrun_ndc = true;
+  // config-5 forks: events F+1.. of the two continuations, fork point and versions
+  std::vector<cdr_event> fork[2];
+  int64_t fork_F = 0, fork_vF = 0, fork_ver[2] = {0, 0};
+  bool forked = false;
 };
 
 struct Gen {
@@ -94,6 +98,9 @@ struct Gen {
   int64_t ver_inc = 10;
   bool cancel_requested = false;
   int64_t dsched = 0, dstart = 0;
+  bool no_failover = false;  // fork continuations keep one version (a replication task has one)
+  uint32_t fork_at = 0;      // config 5: take the fork snapshot once the history reaches this length
+  std::vector<Gen>* fork_snap = nullptr;
 
   Gen(const cdr_synth_params& p, uint32_t w, WfOut& out)
       : P(p), wf(w), r(p.seed ^ cdr_mix64(0x5EED0000ull + (uint64_t)w)), o(out), cur(&out.ev) {
@@ -372,7 +379,7 @@ struct Gen {
   }
 
   void maybe_failover() {
-    if (P.builder == CDR_BUILDER_LOCAL) return;
+    if (P.builder == CDR_BUILDER_LOCAL || no_failover) return;
     if (r.p(0.08)) {
       // next failover version owned by one of the 3 clusters (initial versions 1, 2, 3)
       int64_t next = (version / ver_inc + 1) * ver_inc + 1 + r.below(3);
@@ -384,7 +391,16 @@ struct Gen {
   void random_walk(uint32_t target, bool end_with_can, double w_act, double w_timer, double w_ext) {
     started(true);
     dt_sched(false);
+    walk_body(target, w_act, w_timer, w_ext);
+    if (fork_snap && fork_snap->empty()) fork_snap->push_back(*this);  // short walks fork here
+    walk_end(end_with_can);
+  }
+  // decision rounds until the history (of the current event vector) reaches `target`; a
+  // round starts with DTStarted and ends with the next DTScheduled, so a round boundary
+  // is a batch boundary (the fork point of config 5)
+  void walk_body(uint32_t target, double w_act, double w_timer, double w_ext) {
     while ((uint32_t)cur->size() + 6 < target) {
+      if (fork_snap && fork_snap->empty() && (uint32_t)cur->size() >= fork_at) fork_snap->push_back(*this);
       dt_started();
       if (r.p(0.06)) {
         // decision timeout / failure: FailDecision + transient decision (stateBuilder.go:221-257)
@@ -412,6 +428,8 @@ struct Gen {
       externals();
       dt_sched(false);
     }
+  }
+  void walk_end(bool end_with_can) {
     dt_started();
     dt_completed(r.p(0.5));
     if (end_with_can) {
@@ -582,6 +600,15 @@ void gen_one(const cdr_synth_params& P, uint32_t local, WfOut& o) {
   const int builder = q.builder;
   Gen* gp = &g;
   g.version = q.version;
+  // config 5 (NDC): the fork snapshot (a DeepCopy of the generator, nDC_integration_test.go:
+  // 224-308) is taken at a round boundary 40-70% into the walk, from its own stream so
+  // that the base history is the same with or without forks
+  std::vector<Gen> snap;
+  Rng rf(P.seed ^ cdr_mix64(0xF0C5 + (uint64_t)w));
+  if (P.config == 5 && q.builder == CDR_BUILDER_NDC) {
+    g.fork_snap = &snap;
+    g.fork_at = (uint32_t)(q.target * (0.4 + 0.3 * rf.uni()));
+  }
   switch (P.config) {
     case 1:
       gp->echo();
@@ -602,11 +629,44 @@ void gen_one(const cdr_synth_params& P, uint32_t local, WfOut& o) {
       gp->random_walk(q.target, r2.p(0.2), 1.0, 1.0, 1.0);
       break;
   }
+  if (!snap.empty()) {
+    // the two continuations from the fork point: fork A above every base version (a
+    // failover to another cluster), fork B above A or between the fork point's version
+    // and A's, half the workflows each; one version per continuation (one replication task)
+    const Gen& at = snap[0];
+    o.forked = true;
+    o.fork_F = at.id - 1;
+    o.fork_vF = at.version;
+    int64_t maxv = 0;
+    for (const cdr_event& e : o.ev) maxv = std::max(maxv, e.version);
+    const int64_t inc = at.ver_inc;
+    o.fork_ver[0] = (maxv / inc + 1) * inc + 1 + rf.below(3);
+    o.fork_ver[1] = rf.p(0.5) ? (o.fork_ver[0] / inc + 1) * inc + 1 + rf.below(3) : at.version + 1;
+    for (int k = 0; k < 2; k++) {
+      Gen f = at;
+      f.fork_snap = nullptr;
+      f.cur = &o.fork[k];
+      f.r = Rng(P.seed ^ cdr_mix64(0xF0C50000ull + 2 * (uint64_t)w + (uint64_t)k));
+      f.version = o.fork_ver[k];
+      f.no_failover = true;
+      f.walk_body(8 + (uint32_t)f.r.below(q.target / 2 + 8), 1.0, 0.8, 0.5);
+      f.walk_end(false);
+    }
+  }
   if (builder == CDR_BUILDER_LOCAL) {
     for (auto& e : o.ev) e.version = CDR_EMPTY_VERSION;
     for (auto& e : o.newrun) e.version = CDR_EMPTY_VERSION;
   }
   if (P.error_rate > 0 && r2.uni() < P.error_rate) g.inject_fault(P.fault_kinds);
+  if (P.ndc_part != CDR_SYNTH_PART_BASE) {  // one part of a config-5 forked history
+    if (!o.forked) {
+      o.ev.clear();
+    } else if (P.ndc_part == CDR_SYNTH_PART_REBUILD) {
+      o.ev.resize((size_t)o.fork_F);  // event ids are 1..n: events 1..F
+    } else {
+      o.ev = o.fork[P.ndc_part == CDR_SYNTH_PART_FORK_A ? 0 : 1];
+    }
+  }
   o.d.wf_key = cdr_mix64(P.seed ^ (0xC0FFEEull + w));
   o.d.domain_id = H_DOMAIN0 + 15;
   o.d.workflow_id = wf_handle(w, 0);
@@ -615,7 +675,9 @@ void gen_one(const cdr_synth_params& P, uint32_t local, WfOut& o) {
   o.d.builder = (uint32_t)builder;
   o.d.retention_days = 1 + (int32_t)r2.below(30);
   o.d.failover_version = builder == CDR_BUILDER_LOCAL ? CDR_EMPTY_VERSION : 1;
-  o.d.expected_next_event_id = P.rebuild ? (int64_t)o.ev.size() + 1 : 0;
+  o.d.expected_next_event_id = P.ndc_part == CDR_SYNTH_PART_REBUILD ? o.fork_F + 1
+                               : (P.rebuild && P.ndc_part == CDR_SYNTH_PART_BASE) ? (int64_t)o.ev.size() + 1
+                                                                                   : 0;
   o.d.parent = -1;
   o.d.newrun = -1;
   o.d.newrun_call = o.newrun_call;
@@ -989,6 +1051,50 @@ int cdr_synth_weights(const cdr_synth_params* p, uint64_t n, uint32_t* out) {
     out[w] = plan_one(*p, w, r2).target;
   });
   return CDR_API_OK;
+}
+
+int cdr_synth_ndc_tasks(const cdr_synth_params* p, int fork, cdr_ndc_task* tasks, cdr_vh_item* items,
+                        uint32_t items_cap) {
+  if (!p || !tasks || !items || (fork != 0 && fork != 1)) return CDR_API_EINVAL;
+  std::atomic<int> bad{0};
+  cdr_synth_params q = *p;
+  q.ndc_part = CDR_SYNTH_PART_BASE;
+  par(p->n_wfs, 0, [&](uint32_t w) {
+    WfOut o;
+    gen_one(q, w, o);
+    cdr_ndc_task t{};
+    t.items_off = (uint64_t)w * items_cap;
+    if (o.forked) {
+      cdr_vh_item* it = items + t.items_off;
+      uint32_t n = 0;
+      bool ok = true;
+      auto add = [&](int64_t id, int64_t v) {  // AddOrUpdateItem on a well-formed history
+        if (n > 0 && it[n - 1].version == v) {
+          it[n - 1].event_id = id;
+        } else if (n < items_cap) {
+          it[n++] = cdr_vh_item{id, v};
+        } else {
+          ok = false;
+        }
+      };
+      for (int64_t k = 0; k < o.fork_F; k++) add(o.ev[k].event_id, o.ev[k].version);
+      const std::vector<cdr_event>& f = o.fork[fork];
+      for (const cdr_event& e : f) add(e.event_id, e.version);
+      if (!ok) bad = 1;
+      t.n_items = n;
+      t.first_event_id = f.empty() ? 0 : f.front().event_id;
+      t.last_event_id = f.empty() ? 0 : f.back().event_id;
+      t.last_version = f.empty() ? 0 : f.back().version;
+      t.version = o.fork_ver[fork];
+      uint64_t lo, hi;
+      cdr_uuid(p->seed, o.d.wf_key, CDR_UUID_FORK, fork, &lo, &hi);
+      t.new_token.tree = o.d.run_id;
+      t.new_token.branch_lo = lo;
+      t.new_token.branch_hi = hi;
+    }
+    tasks[w] = t;
+  });
+  return bad ? CDR_API_EINVAL : CDR_API_OK;
 }
 
 int cdr_synth_shards(uint64_t n, int32_t num_shards, int32_t* out) {

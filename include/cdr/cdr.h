@@ -359,6 +359,37 @@ int cdr_checksum_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out
 int cdr_entry_digests_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, uint64_t* per_entry,
                             uint64_t* dev_sum, void* stream);
 
+/* ------------------------------------------------ NDC branches (ndc.hip) */
+/* Conflict resolution around the replay when replication tasks fork a history
+ * (SURVEY §8(d) C5).  Per workflow w (all pointers device memory):
+ *
+ *   cdr_ndc_branch_async: task[w] against the workflow's persisted VersionHistories
+ *     vhs[w] (items in `pool`): nDCBranchMgr.prepareVersionHistory
+ *     (service/history/nDCBranchMgr.go:80-249: FindLCAVersionHistoryIndexAndItem,
+ *     IsLCAAppendable, verifyEventsOrder, DuplicateUntilLCAItem + createNewBranch's
+ *     AddVersionHistory) then nDCConflictResolver.prepareMutableState
+ *     (nDCConflictResolver.go:73-114), and for a lower-version task on a non-current
+ *     branch the backfill's AddOrUpdateItem (nDCHistoryReplicator.go:437-447).  vhs[w]
+ *     is updated only when dec[w].code is CDR_OK; dec[w].action says what the caller
+ *     replays next (CDR_NDC_*).
+ *   cdr_ndc_rebuild_verify_async: after the rebuild replay of every CDR_NDC_REBUILD
+ *     workflow (entry w of `out`, NDC builder, expected_next_event_id =
+ *     dec[w].rebuild_next_event_id — nDCStateRebuilder.rebuild, nDCStateRebuilder.go:92-160):
+ *     SetCurrentBranchToken(dec[w].rebuild_token), the rebuilt VersionHistory must equal
+ *     the branch's (else result.code = CDR_E_REBUILD_VH_MISMATCH, nDCConflictResolver.go:
+ *     154-165), then vhs[w].current = the branch (SetCurrentVersionHistoryIndex, :172-174).
+ *   cdr_vhs_sync_async: after a replay applied to the current branch, its VersionHistory
+ *     (the replay output's items and token) becomes branch vhs[w].current (a workflow
+ *     with no branch gets its first, NewVersionHistories).  Needs items_cap >= the
+ *     entry's caps.vh_cap.
+ * Asynchronous on `stream`. */
+int cdr_ndc_branch_async(cdr_ctx* ctx, const cdr_ndc_task* tasks, const cdr_vh_item* task_items, uint32_t n,
+                         cdr_vhs* vhs, cdr_vh_item* pool, cdr_ndc_decision* dec, void* stream);
+int cdr_ndc_rebuild_verify_async(cdr_ctx* ctx, uint32_t n, const cdr_ndc_decision* dec, cdr_vhs* vhs,
+                                 const cdr_vh_item* pool, const cdr_wf_caps* caps, const cdr_out* out, void* stream);
+int cdr_vhs_sync_async(cdr_ctx* ctx, uint32_t n, cdr_vhs* vhs, cdr_vh_item* pool, const cdr_wf_caps* caps,
+                       const cdr_out* out, void* stream);
+
 /* ------------------------------------------------------------------ misc */
 
 /* farmhash Fingerprint32(workflowID) % numShards (common/util.go:249-252) */

@@ -192,7 +192,8 @@ enum cdr_uuid_site {
   CDR_UUID_CANCEL_REQ = 3, /* stateBuilder.go:410 cancelRequestID */
   CDR_UUID_SIGNAL_REQ = 4, /* stateBuilder.go:441 signalRequestID */
   CDR_UUID_NEWRUN_REQ = 5, /* stateBuilder.go:566 requestID of the new run */
-  CDR_UUID_NEWRUN_KEY = 6  /* derives the new run's workflow key from its parent's */
+  CDR_UUID_NEWRUN_KEY = 6, /* derives the new run's workflow key from its parent's */
+  CDR_UUID_FORK = 7        /* ForkHistoryBranch NewBranchToken's BranchID (nDCBranchMgr.go:205-211) */
 };
 
 CDR_HD uint64_t cdr_mix64(uint64_t x) {

@@ -21,7 +21,17 @@ typedef struct cdr_synth_params {
   uint32_t fault_kinds; /* bit i allows injected fault kind i (synth.cpp inject_fault); 0 = all */
   uint32_t plan_mode;   /* CDR_PLAN_* of the sliced layout (cdr_plan_slices_ex) */
   const uint32_t* index_map; /* optional [n_wfs]: global index of each generated workflow */
+  /* config 5 forks: every workflow's history forks at a batch boundary
+   * F (a DeepCopy of the generator with a version bump, nDC_integration_test.go:224-308)
+   * into two continuations.  Which part a batch holds: */
+  uint32_t ndc_part;  /* CDR_SYNTH_PART_* */
+  uint32_t _pad2;
 } cdr_synth_params;
+#define CDR_SYNTH_PART_BASE 0    /* the base branch, whole (default) */
+#define CDR_SYNTH_PART_REBUILD 1 /* the base branch's events 1..F (the rebuild path; expected next = F+1) */
+#define CDR_SYNTH_PART_FORK_A 2  /* fork A's events F+1.. (version above every base version) */
+#define CDR_SYNTH_PART_FORK_B 3  /* fork B's events F+1.. (above fork A's version, or between the
+                                    base's version at F and fork A's: half the workflows each) */
 typedef struct cdr_synth_sizes {
   uint64_t n_events;
   uint32_t n_entries, _pad;
@@ -42,6 +52,13 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
 /* planned event count of workflows 0..n-1 (the walk's target length, drawn without
  * generating the histories): weights of the bench's shard->GPU assignment */
 int cdr_synth_weights(const cdr_synth_params* p, uint64_t n, uint32_t* out);
+/* The replication tasks that deliver fork A (fork = 0) or B (fork = 1) of every
+ * config-5 workflow of `p`: task w's incoming VersionHistory (the base's items up to F
+ * then the fork's) at items[w * items_cap ...], first / last event, version and the
+ * ForkHistoryBranch token of the branch it would create.  -EINVAL if an item list
+ * exceeds items_cap. */
+int cdr_synth_ndc_tasks(const cdr_synth_params* p, int fork, cdr_ndc_task* tasks, cdr_vh_item* items,
+                        uint32_t items_cap);
 /* history shard of synthetic workflow ids "wf-<i>", i in [0, n): farmhash
  * Fingerprint32 % num_shards (common/util.go:249-252) */
 int cdr_synth_shards(uint64_t n, int32_t num_shards, int32_t* out);

@@ -36,6 +36,26 @@ def lib():
                                             C.c_int64, C.c_int64]
         L.cdro_state_transition.restype = C.c_int
         L.cdro_state_transition.argtypes = [C.c_int] * 4
+        P = C.POINTER
+        VH = abi.CdrVHItem
+        for name, args in (
+                ("cdro_vh_duplicate_until_lca", [P(VH), C.c_uint32, VH, P(VH), P(C.c_uint32)]),
+                ("cdro_vh_contains", [P(VH), C.c_uint32, VH]),
+                ("cdro_vh_is_lca_appendable", [P(VH), C.c_uint32, VH]),
+                ("cdro_vh_find_lca", [P(VH), C.c_uint32, P(VH), C.c_uint32, P(VH)]),
+                ("cdro_vhs_add", [P(abi.CdrVHS), P(VH), P(abi.CdrVHToken), P(VH), C.c_uint32, P(C.c_int),
+                                  P(C.c_uint32)]),
+                ("cdro_vhs_find_lca_index", [P(abi.CdrVHS), P(VH), P(VH), C.c_uint32, P(C.c_uint32), P(VH)]),
+                ("cdro_vhs_find_first_index_by_item", [P(abi.CdrVHS), P(VH), VH, P(C.c_uint32)]),
+                ("cdro_vhs_is_rebuilt", [P(abi.CdrVHS), P(VH)]),
+                ("cdro_ndc_branch", [P(abi.CdrNdcTask), P(VH), C.c_uint32, P(abi.CdrVHS), P(VH),
+                                     P(abi.CdrNdcDecision)]),
+                ("cdro_ndc_rebuild_verify", [C.c_uint32, P(abi.CdrNdcDecision), P(abi.CdrVHS), P(VH),
+                                             P(abi.CdrWfCaps), P(abi.CdrOut)]),
+                ("cdro_vhs_sync", [C.c_uint32, P(abi.CdrVHS), P(VH), P(abi.CdrWfCaps), P(abi.CdrOut)])):
+            fn = getattr(L, name)
+            fn.restype = C.c_int
+            fn.argtypes = args
         L.cdro_entry_digests.restype = C.c_int
         L.cdro_entry_digests.argtypes = [C.POINTER(abi.CdrBatch), C.POINTER(abi.CdrWfCaps), C.POINTER(abi.CdrOut),
                                          C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
@@ -109,3 +129,23 @@ def synth_digests(config: int, index_map, seed: int, threads: int = 16, chunk: i
             hist[k] = hist.get(k, 0) + int(c)
         del b, pl, out
     return (np.concatenate(parts) if parts else np.zeros(0, np.uint64)), total, hist
+
+
+class NdcBackend:
+    """The CPU restatement behind cadence_amd.ndc.replicate's compute steps: replays by
+    replay_ref.cpp, branch bookkeeping by ndc_ref.cpp."""
+
+    def replay(self, batch):
+        return replay(batch)
+
+    def branch(self, tasks, items, vhs, pool, n):
+        from cadence_amd import abi
+        dec = (abi.CdrNdcDecision * max(1, n))()
+        lib().cdro_ndc_branch(tasks, items, n, vhs, pool, dec)
+        return dec
+
+    def rebuild_verify(self, dec, vhs, pool, out, n):
+        lib().cdro_ndc_rebuild_verify(n, dec, vhs, pool, out.plan.caps, C.byref(out.cstruct()))
+
+    def vhs_sync(self, vhs, pool, out, n):
+        lib().cdro_vhs_sync(n, vhs, pool, out.plan.caps, C.byref(out.cstruct()))

@@ -125,6 +125,7 @@ struct VersionHistories {
   int32_t FindLCAVersionHistoryIndexAndItem(const VersionHistory& incoming, uint32_t* idx, Item* item) const {
     bool set = false;
     size_t len = 0;
+    if (h.empty()) return CDR_E_VH_NO_LCA;  // no history at all (NewVersionHistories never ran)
     for (size_t i = 0; i < h.size(); i++) {
       Item it;
       int32_t rc = h[i].FindLCAItem(incoming, &it);

@@ -1,0 +1,145 @@
+"""GPU parity of the NDC conflict-resolution path (cadence_amd/csrc/ndc.hip + the replay
+kernels) against the CPU restatement (oracle/ndc_ref.cpp, replay_ref.cpp): the branch
+kernel on randomised version histories and tasks (every decision and error site), the
+forked synthetic config 5 end to end, and the reference's hand-crafted 3-branch history."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from cadence_amd import abi, engine, ndc
+
+from . import ndc_fixture
+
+pytestmark = pytest.mark.gpu
+
+
+def _vhs_state(vhs, pool, n):
+    """The logical VersionHistories of every workflow (slots past a branch's items and
+    branches past n_branches are scratch)."""
+    out = []
+    for w in range(n):
+        s = vhs[w]
+        out.append((s.current, s.n_branches, tuple(
+            (bytes(s.branch[b].token), tuple(ndc.branch_items(vhs, pool, w, b))) for b in range(s.n_branches))))
+    return out
+
+
+def _copy(a):
+    b = type(a)()
+    C.memmove(b, a, C.sizeof(a))
+    return b
+
+
+def _random_cases(n, seed):
+    """Branching version histories built the way replication builds them (a base, forks
+    duplicated up to an LCA and extended with higher versions), then tasks derived from
+    a random branch: truncated / extended, first event on, before or after the next ID,
+    versions below, equal to or above the current branch's last write; 5% of the items
+    corrupted (malformed histories)."""
+    rng = np.random.default_rng(seed)
+    cap = 16
+    vhs, pool = ndc.new_vhs(n, cap)
+    tasks = (abi.CdrNdcTask * n)()
+    items = (abi.CdrVHItem * (n * cap))()
+    for w in range(n):
+        base, e, v = [], 0, int(rng.integers(1, 4))
+        for _ in range(int(rng.integers(1, 5))):
+            e += int(rng.integers(1, 20))
+            base.append((e, v))
+            v += int(rng.integers(1, 15))
+        branches = [base]
+        for _ in range(int(rng.integers(0, 4 if rng.random() < 0.9 else 9))):
+            src = branches[int(rng.integers(len(branches)))]
+            k = int(rng.integers(len(src)))
+            cut = src[:k + 1]
+            if rng.random() < 0.5 and k > 0:
+                cut[-1] = (int(rng.integers(cut[-2][0] + 1, cut[-1][0] + 1)), cut[-1][1])
+            b = list(cut)
+            ee, vv = b[-1]
+            for _ in range(int(rng.integers(1, 3))):
+                ee += int(rng.integers(1, 10))
+                vv += int(rng.integers(1, 30))
+                b.append((ee, vv))
+            branches.append(b)
+        branches = branches[:abi.VHS_MAX_BRANCHES]
+        s = vhs[w]
+        s.n_branches = len(branches)
+        s.current = int(np.argmax([b[-1][1] for b in branches])) if rng.random() < 0.8 else \
+            int(rng.integers(len(branches)))
+        for bi, b in enumerate(branches):
+            s.branch[bi].token.tree = w
+            s.branch[bi].token.branch_lo, s.branch[bi].token.branch_hi = bi, 7
+            s.branch[bi].n_items = len(b)
+            for i, (ee, vv) in enumerate(b):
+                pool[s.items_off + bi * cap + i].event_id = ee
+                pool[s.items_off + bi * cap + i].version = vv
+        # the task: a branch's prefix, extended
+        src = branches[int(rng.integers(len(branches)))]
+        k = int(rng.integers(len(src)))
+        inc = list(src[:k + 1])
+        if rng.random() < 0.4 and inc[-1][0] > 1:
+            inc[-1] = (int(rng.integers(max(1, inc[-2][0] + 1 if len(inc) > 1 else 1), inc[-1][0] + 1)), inc[-1][1])
+        lca_e = inc[-1][0]
+        ee, vv = inc[-1]
+        cur_last = branches[s.current][-1][1]
+        r = rng.random()
+        newv = cur_last + int(rng.integers(1, 9)) if r < 0.45 else (cur_last if r < 0.55 else
+                                                                   vv + int(rng.integers(0, 3)))
+        ee += int(rng.integers(1, 6))
+        inc.append((ee, max(newv, vv)))
+        if rng.random() < 0.05:
+            j = int(rng.integers(len(inc)))
+            inc[j] = (inc[j][0], int(rng.integers(0, 100)))
+        t = tasks[w]
+        t.items_off, t.n_items = w * cap, len(inc)
+        for i, (a, b) in enumerate(inc):
+            items[w * cap + i].event_id, items[w * cap + i].version = a, b
+        t.first_event_id = lca_e + 1 + int(rng.choice([-1, 0, 0, 0, 0, 1]))
+        t.last_event_id, t.last_version = inc[-1]
+        t.version = inc[-1][1]
+        t.new_token.tree, t.new_token.branch_lo, t.new_token.branch_hi = w, 99, 9
+    return tasks, items, vhs, pool
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_ndc_branch_kernel_matches_oracle(engine_gpu, seed):
+    import oracle
+    n = 3000
+    tasks, items, vhs, pool = _random_cases(n, seed)
+    g_vhs, g_pool = _copy(vhs), _copy(pool)
+    dec_gpu = ndc.GpuBackend(engine_gpu).branch(tasks, items, g_vhs, g_pool, n)
+    dec_ref = oracle.NdcBackend().branch(tasks, items, vhs, pool, n)
+    bad = [w for w in range(n) if bytes(dec_gpu[w]) != bytes(dec_ref[w])]
+    assert not bad, [(w, abi.STATUS[dec_gpu[w].code], abi.STATUS[dec_ref[w].code]) for w in bad[:5]]
+    assert _vhs_state(g_vhs, g_pool, n) == _vhs_state(vhs, pool, n)
+    seen = {abi.STATUS[dec_ref[w].code] for w in range(n)} | {abi.NDC_ACTIONS[dec_ref[w].action] for w in range(n)}
+    for want in ("OK", "SKIP", "APPLY_CURRENT", "REBUILD", "BACKFILL", "E_NDC_RETRY_TASK", "E_NDC_SAME_VERSION"):
+        assert want in seen, (want, seen)
+
+
+def _replicate_both(eng, base, rebuild, forks):
+    import oracle
+    got = ndc.replicate(ndc.GpuBackend(eng), base, rebuild, forks)
+    ref = ndc.replicate(oracle.NdcBackend(), base, rebuild, forks)
+    n = base.n_wfs
+    bad = engine.compare(base, got[0], ref[0])
+    assert not bad, "\n".join(bad[:10])
+    assert _vhs_state(got[1], got[2], n) == _vhs_state(ref[1], ref[2], n)
+    for dg, dr in zip(got[3], ref[3]):
+        assert [bytes(dg[w]) for w in range(n)] == [bytes(dr[w]) for w in range(n)]
+    return got
+
+
+def test_handcrafted_three_branches_gpu(engine_gpu):
+    base, rebuild, forks, doc = ndc_fixture.handcrafted()
+    final, vhs, pool, decs, _ = _replicate_both(engine_gpu, base, rebuild, forks)
+    ndc_fixture.check_reference_outcome(final, vhs, pool, decs, doc)
+
+
+@pytest.mark.parametrize("seed", [0x5EED0C05, 7])
+def test_forked_config5_gpu(engine_gpu, seed):
+    base, rebuild, forks = ndc.synth_forked(5, 400, seed)
+    final, vhs, pool, decs, info = _replicate_both(engine_gpu, base, rebuild, forks)
+    assert engine.status_histogram(final) == {"OK": 400}
+    assert {abi.NDC_ACTIONS[decs[1][w].action] for w in range(400)} == {"REBUILD", "BACKFILL"}
