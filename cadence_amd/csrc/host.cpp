@@ -78,7 +78,8 @@ namespace cdr_internal {
 
 uint32_t arena_words_for(uint32_t type) { return ::arena_words_for(type); }
 
-void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* out) {
+void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* out, const cdr_kv* kvs,
+              const cdr_reset_point* rps) {
   cdr_wf_caps c{};
   bool fast = builder != CDR_BUILDER_2DC && n > 0 && ev[0].type == CDR_EV_WF_STARTED;
   bool have_ver = false;
@@ -89,6 +90,12 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   // reused first-free, so a table's high-water mark is its peak live count)
   std::vector<int64_t> lv[4];  // user timers (timer id), children, request-cancels, signals (initiated id)
   size_t lv_max[4] = {0, 0, 0, 0};
+  // k_replay_reg envelope (CDR_CAP_REG): ids, call lengths, reset-point rows (Started's
+  // plus new distinct checksums), distinct search-attribute keys
+  bool reg = n > 0 && n < (1u << 20);
+  int64_t last_id = 0;
+  uint64_t call_start = 0;
+  std::vector<uint32_t> rp_cks, sa_keys;
   auto lv_add = [&](int t, int64_t key, bool unique) {
     if (unique && std::find(lv[t].begin(), lv[t].end(), key) != lv[t].end()) return;
     lv[t].push_back(key);
@@ -100,6 +107,30 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   };
   for (uint64_t k = 0; k < n; k++) {
     const cdr_event& e = ev[k];
+    if (k == 0 || (e.flags & CDR_EVF_BATCH_FIRST)) call_start = k;
+    reg = reg && e.event_id > last_id && e.event_id < (1ll << 31) && k - call_start < 4096;
+    last_id = e.event_id;
+    if (e.type == CDR_EV_WF_STARTED) {  // rows from the start attributes (a second Started resets them)
+      const cdr_attr_wf_started& a = e.a.started;
+      rp_cks.clear();
+      sa_keys.clear();
+      if (a.flags & CDR_SF_HAS_RESET_POINTS)
+        for (uint32_t q = 0; q < a.reset_points_len; q++) {  // a row each; unknown checksums match nothing
+          const cdr_reset_point* p = rps ? rps + a.reset_points_off + q : nullptr;
+          rp_cks.push_back(p && (p->flags & CDR_RP_HAS_CHECKSUM) ? p->binary_checksum : 0u);
+        }
+      if (a.flags & CDR_SF_HAS_SEARCH_ATTR)
+        for (uint32_t q = 0; q < a.search_attr_len; q++)
+          sa_keys.push_back(kvs ? kvs[a.search_attr_off + q].key : 0xFFFFFFF0u - q);
+    } else if (e.type == CDR_EV_DT_COMPLETED && e.a.dt.binary_checksum) {
+      if (std::find(rp_cks.begin(), rp_cks.end(), e.a.dt.binary_checksum) == rp_cks.end())
+        rp_cks.push_back(e.a.dt.binary_checksum);
+    } else if (e.type == CDR_EV_UPSERT_SA) {
+      for (uint32_t q = 0; q < e.a.upsert.search_attr_len && sa_keys.size() <= CDR_REG_NSA; q++) {
+        const uint32_t key = kvs ? kvs[e.a.upsert.search_attr_off + q].key : 0xFFFFFF00u - (uint32_t)sa_keys.size();
+        if (std::find(sa_keys.begin(), sa_keys.end(), key) == sa_keys.end()) sa_keys.push_back(key);
+      }
+    }
     // live-activity bound: a close of a missing activity stops the replay, so before
     // the first error every close removed one live activity
     if (e.type == CDR_EV_AT_SCHEDULED) live_max = std::max(live_max, ++live);
@@ -180,6 +211,10 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
         lv_max[1] + lv_max[2] + lv_max[3] <= lim[2] && n <= lim[3])
       c.flags |= CDR_CAP_LANE;
   }
+  reg = reg && !(c.flags & CDR_CAP_FAST) && live_max <= (int64_t)CDR_REG_NA && lv_max[0] <= CDR_REG_NT &&
+        lv_max[1] <= CDR_REG_NX && lv_max[2] <= CDR_REG_NX && lv_max[3] <= CDR_REG_NX &&
+        rp_cks.size() <= CDR_REG_NRP && sa_keys.size() <= CDR_REG_NSA;
+  if (reg) c.flags |= CDR_CAP_REG;
   *out = c;
 }
 
@@ -431,7 +466,7 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
       }
     }
     cdr_wf_caps c{};
-    cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c);
+    cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c, b->kvs, b->rps);
     if (b->carry && b->carry->src && b->carry->src[w] >= 0) {
       // a loaded state (cdr_carry): its rows are live from the start; only the
       // general kernel replays onto a loaded state
@@ -450,7 +485,7 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
       c.sa_cap += r.n_search_attr;
       c.act_live += r.n_activity;
       c.timer_live += r.n_timer;
-      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE);
+      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_REG);
     }
     cdr_internal::task_caps(b->events + d.ev_off, d.ev_len, &c.xfer_cap, &c.ttask_cap);
     c.xfer_off = t.xfer;
@@ -488,7 +523,7 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   lanes.reserve(n_wfs);
   for (uint32_t w = 0; w < n_wfs; w++)
     ((mode & CDR_PLAN_WAVE) && (caps[w].flags & CDR_CAP_WAVE) &&
-             ((mode & CDR_PLAN_WAVE_ALL) || !(caps[w].flags & CDR_CAP_LANE))
+             ((mode & CDR_PLAN_WAVE_ALL) || !(caps[w].flags & (CDR_CAP_LANE | CDR_CAP_REG)))
          ? waves
          : lanes)
         .push_back(w);
@@ -501,7 +536,14 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   // to its lanes' own and more slices fit the LDS tier of the general kernel
   auto lclass = [&](uint32_t a) { return (uint32_t)(std::log2((double)wfs[a].ev_len + 1.0) * 16.0); };
   auto slots = [&](uint32_t a) { return caps ? caps[a].act_live * CDR_ACT_PLANES + caps[a].timer_live * CDR_TIM_PLANES : 0u; };
+  // kernel groups first (fast-path, register-table, general), so that slices are
+  // homogeneous and go to the specialised kernels whole
+  auto group = [&](uint32_t a) {
+    return !caps ? 0u : (caps[a].flags & CDR_CAP_FAST) ? 0u : (caps[a].flags & CDR_CAP_REG) ? 1u : 2u;
+  };
   auto lane_order = [&](uint32_t a, uint32_t c) {
+    const uint32_t ga = group(a), gc = group(c);
+    if (ga != gc) return ga < gc;
     const uint32_t ka = lclass(a), kc = lclass(c);
     if (ka != kc) return ka > kc;
     const uint32_t sa = slots(a), sc = slots(c);
@@ -565,21 +607,23 @@ int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n
       continue;
     }
     uint32_t a = 0, t = 0, lanes = 0;
-    bool fast = true;
+    bool fast = true, reg = true;
     for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
       const int32_t w = lane_wf[(size_t)s * CDR_SLICE_WIDTH + l];
       if (w < 0) continue;
       a = std::max(a, caps[w].act_live);
       t = std::max(t, caps[w].timer_live);
       fast = fast && (caps[w].flags & CDR_CAP_FAST);
+      reg = reg && (caps[w].flags & CDR_CAP_REG);
       lanes++;
     }
     fast = fast && lanes > 0;
+    reg = reg && lanes > 0 && !fast;
     nf += fast ? 1u : 0u;
     if (scratch_off) scratch_off[s] = off;
     if (act_slots) act_slots[s] = a;
     if (tim_slots) tim_slots[s] = t;
-    if (slice_flags) slice_flags[s] = fast ? CDR_SLICE_FAST : 0u;
+    if (slice_flags) slice_flags[s] = fast ? CDR_SLICE_FAST : reg ? CDR_SLICE_REG : 0u;
     off += ((uint64_t)a * CDR_ACT_PLANES + (uint64_t)t * CDR_TIM_PLANES) * CDR_SLICE_WIDTH;
   }
   *total_words = off;

@@ -11,7 +11,8 @@ uint32_t arena_words_for(uint32_t type);
 
 // Output capacities of one history (cdr_plan_caps restricted to one workflow);
 // offsets are left zero.
-void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* c);
+void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* c, const cdr_kv* kvs = nullptr,
+              const cdr_reset_point* rps = nullptr);
 
 // Pack one workflow's events into lane `lane` of a slice whose first row is row0 and
 // whose length is len (rows beyond n are padding).  `apos` is the workflow's arena

@@ -462,7 +462,7 @@ struct cdr_launch {
   cdr_out O;
   uint32_t la, lt;  // activity / user-timer working slots per lane held in LDS
   uint32_t fast;    // CDR_SLICE_FAST slices go to k_replay_fast (else every slice here)
-  uint32_t _pad;
+  uint32_t reg;     // CDR_SLICE_REG slices go to k_replay_reg (else here)
 };
 #define AS4 __attribute__((address_space(4)))
 __device__ __forceinline__ const AS4 cdr_launch* KA() {
@@ -503,6 +503,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     const uint32_t sf = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_flags[s]);
     if (sf & CDR_SLICE_WAVE) return;  // k_replay_wave
     if (KA()->fast && (sf & CDR_SLICE_FAST)) return;
+    if (KA()->reg && (sf & CDR_SLICE_REG)) return;  // k_replay_reg
   }
   const uint64_t row0_ = KA()->B.ev.slice_row0[s];
   const uint64_t row0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(row0_ >> 32)) << 32) |
@@ -1627,6 +1628,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
 
 #include "replay_fast.inc"
 #include "replay_wave.inc"
+#include "replay_reg.inc"
 
 // Per-workflow table epilogue: move live rows to the front in key order (the
 // canonical order of the Go maps' keys), sort the SearchAttributes map by key, and
@@ -1687,6 +1689,7 @@ __global__ void k_finalize(cdr_dev_batch B, cdr_out O) {
 struct cdr_ctx {
   int device;
   int fast = 1;  // cdr_set_fast_path
+  int reg = 1;   // cdr_set_reg_path
   uint32_t plan_mode = CDR_PLAN_WAVE;  // cdr_set_plan_mode
   hipEvent_t ev[4];
   bool timed;
@@ -1738,6 +1741,13 @@ int cdr_set_fast_path(cdr_ctx* c, int enable) {
   return old;
 }
 
+int cdr_set_reg_path(cdr_ctx* c, int enable) {
+  if (!c) return CDR_API_EINVAL;
+  const int old = c->reg;
+  c->reg = enable ? 1 : 0;
+  return old;
+}
+
 int cdr_set_plan_mode(cdr_ctx* c, uint32_t mode) {
   if (!c || (mode & ~CDR_PLAN_WAVE)) return CDR_API_EINVAL;
   const uint32_t old = c->plan_mode;
@@ -1773,13 +1783,18 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const bool tasks = out->transfer != nullptr;
   if (tasks && (in->n_wave_slices > 0 || !out->timer_tasks || !out->n_tasks)) return CDR_API_EINVAL;
   const bool fast = c->fast && in->n_fast_slices > 0 && !tasks;
+  // register-table kernel: LastReplicationInfo kept for clusters < CDR_REG_NCL only
+  const bool reg = c->fast && c->reg && in->n_reg_slices > 0 && !tasks && in->cluster.n_clusters <= (int)CDR_REG_NCL;
   const bool wave = in->n_wave_slices > 0;
-  const bool general = (fast ? in->n_fast_slices : 0u) + in->n_wave_slices < in->ev.n_slices;
+  const bool general =
+      (fast ? in->n_fast_slices : 0u) + (reg ? in->n_reg_slices : 0u) + in->n_wave_slices < in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
-  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, 0u};
+  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u};
   if (blocks && fast)
     hipLaunchKernelGGL(k_replay_fast, dim3(blocks), dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, st, L);
+  HIPCHK(hipGetLastError());
+  if (blocks && reg) hipLaunchKernelGGL(k_replay_reg, dim3(blocks), dim3(CDR_SLICE_WIDTH), REG_LDS_BYTES, st, L);
   HIPCHK(hipGetLastError());
   // the wave kernel on the side stream when lane slices also run: both kernels' waves
   // share the CUs (wave slices: scalar unit; lane slices: VALU)

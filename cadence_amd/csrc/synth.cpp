@@ -748,9 +748,10 @@ void size_pass(const cdr_synth_params& P, Sizes& S, int threads, bool want_caps 
     S.n_kv[w] = (uint32_t)o.kvs.size();
     S.n_rp[w] = (uint32_t)o.rps.size();
     if (want_caps) {
-      cdr_internal::caps_one(o.ev.data(), o.ev.size(), o.d.builder, &S.cap_ev[w]);
+      cdr_internal::caps_one(o.ev.data(), o.ev.size(), o.d.builder, &S.cap_ev[w], o.kvs.data(), o.rps.data());
       cdr_internal::caps_one(o.newrun.data(), o.newrun.size(),
-                             o.newrun_ndc ? (uint32_t)CDR_BUILDER_NDC : (uint32_t)CDR_BUILDER_2DC, &S.cap_nr[w]);
+                             o.newrun_ndc ? (uint32_t)CDR_BUILDER_NDC : (uint32_t)CDR_BUILDER_2DC, &S.cap_nr[w],
+                             o.kvs.data(), o.rps.data());
       S.aw_ev[w] = arena_of(o.ev);
       S.aw_nr[w] = arena_of(o.newrun);
     }

@@ -107,8 +107,10 @@ class DeviceBatch:
         db.max_tim_slots = int(self.h_sc_tim.max()) if len(self.h_sc_tim) else 0
         self.n_fast = int(((self.h_sflags & abi.SLICE_FAST) != 0).sum())
         self.n_wave = int(((self.h_sflags & abi.SLICE_WAVE) != 0).sum())
+        self.n_reg = int(((self.h_sflags & abi.SLICE_REG) != 0).sum())
         db.n_fast_slices = self.n_fast
         db.n_wave_slices = self.n_wave
+        db.n_reg_slices = self.n_reg
         db.empty_uuid = meta.empty_uuid
         db.cluster = meta.cluster
         db.now_ns = meta.now_ns

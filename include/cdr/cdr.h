@@ -125,6 +125,10 @@ typedef struct cdr_slices {
  * wavefront (replay_wave.inc); its slice_len rows hold the workflow's events 64 at a
  * time, event k in row k/64, lane k%64 (cdr_plan_slices_ex with CDR_PLAN_WAVE) */
 #define CDR_SLICE_WAVE 0x2u
+/* every lane's history has CDR_CAP_REG: the slice replays in k_replay_reg
+ * (replay_reg.inc: entity tables in registers, no global memory traffic in the step
+ * loop beyond the event stream) */
+#define CDR_SLICE_REG 0x4u
 /* event types the fast-path kernel replays (bit = cdr_event_type) */
 #define CDR_FAST_TYPES                                                                                       \
   (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_WF_COMPLETED) | CDR_TB(CDR_EV_WF_FAILED) |                      \
@@ -209,6 +213,8 @@ typedef struct cdr_dev_batch {
   uint32_t max_act_slots, max_tim_slots;
   uint32_t n_fast_slices; /* slices with CDR_SLICE_FAST (cdr_plan_scratch) */
   uint32_t n_wave_slices; /* slices with CDR_SLICE_WAVE (cdr_plan_slices_ex) */
+  uint32_t n_reg_slices;  /* slices with CDR_SLICE_REG (cdr_plan_scratch) */
+  uint32_t _pad_reg;
   cdr_cluster_meta cluster;
   int64_t now_ns;
   uint64_t uuid_seed;
@@ -266,9 +272,13 @@ typedef struct cdr_ctx cdr_ctx;
 cdr_ctx* cdr_create(int device);
 void cdr_destroy(cdr_ctx* ctx);
 
-/* Route CDR_SLICE_FAST slices to the fast-path kernel (default 1) or replay every
- * slice with the general kernel (0; parity tests run both).  Returns the old value. */
+/* Route CDR_SLICE_FAST slices to the fast-path kernel and CDR_SLICE_REG slices to the
+ * register-table kernel (default 1) or replay every lane slice with the general kernel
+ * (0; parity tests run both).  Returns the old value. */
 int cdr_set_fast_path(cdr_ctx* ctx, int enable);
+/* Route CDR_SLICE_REG slices to k_replay_reg (default 1) or to the general kernel (0);
+ * returns the old value. */
+int cdr_set_reg_path(cdr_ctx* ctx, int enable);
 
 /* Slicing mode of cdr_replay_batch's planning (CDR_PLAN_*; default CDR_PLAN_WAVE).
  * Returns the previous mode. */

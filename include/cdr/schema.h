@@ -566,6 +566,18 @@ typedef struct cdr_wf_caps {
  * (cdr_plan_slices_ex keeps it in the lane slices): peak live activities, user timers,
  * children + request-cancels + signals and the event count within these bounds */
 #define CDR_CAP_LANE 0x4u
+/* the history fits the register-table lane kernel (replay_reg.inc): not CDR_CAP_FAST; at
+ * most CDR_REG_NA live activities, CDR_REG_NT live user timers, CDR_REG_NX live children,
+ * request-cancels and signals each, CDR_REG_NRP reset points, CDR_REG_NSA search-attribute
+ * keys; event ids strictly increasing in [1, 2^31); fewer than 2^20 events and calls
+ * shorter than 4096 events (event indices are packed in 20 + 12 bits) */
+#define CDR_CAP_REG 0x8u
+#define CDR_REG_NA 6u
+#define CDR_REG_NT 10u
+#define CDR_REG_NX 4u
+#define CDR_REG_NRP 8u
+#define CDR_REG_NSA 8u
+#define CDR_REG_NCL 4u /* 2DC: LastReplicationInfo kept for clusters < 4 (batch with more: general kernel) */
 #define CDR_LANE_MAX_ACT 6u
 #define CDR_LANE_MAX_TIMERS 10u
 #define CDR_LANE_MAX_EXT 8u

@@ -25,16 +25,20 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-wave", action="store_true", help="plan divergent histories into lane slices")
     ap.add_argument("--wave-all", action="store_true", help="every divergent history on a wave slice")
+    ap.add_argument("--no-reg", action="store_true", help="register-table slices on the general kernel")
     args = ap.parse_args()
     import torch
-    import bench
+    from cadence_amd.synth import DeviceBatch
     torch.cuda.set_device(0)
     idx = np.arange(args.wfs, dtype=np.uint32)
-    db = bench.DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config,
+    db = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config,
                            plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0))
     stream = torch.cuda.current_stream().cuda_stream
     libs = [(p, abi.load(p)) for p in args.libs]
     ctxs = [L.cdr_create(0) for _, L in libs]
+    if args.no_reg:
+        for (_, L), c in zip(libs, ctxs):
+            L.cdr_set_reg_path(c, 0)
     times = {p: [] for p, _ in libs}
     sums = {}
     for rnd in range(args.rounds):
