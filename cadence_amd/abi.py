@@ -218,12 +218,14 @@ CdrSlices = _S("cdr_slices", [
 SLICE_FAST = 0x1
 SLICE_WAVE = 0x2
 SLICE_REG = 0x4
+SLICE_REG2 = 0x8
 CAP_FAST = 0x1
 CAP_WAVE = 0x2
 PLAN_WAVE = 0x1
 PLAN_WAVE_ALL = 0x2  # with PLAN_WAVE: lane-friendly (CAP_LANE) entries on the wave kernel too
 CAP_LANE = 0x4
 CAP_REG = 0x8
+CAP_REG2 = 0x10
 
 # slice-major slab of event columns (cdr.h enum cdr_col): name, dtype, in order
 SLAB_COLS = (("event_id", np.int64), ("version", np.int64), ("timestamp", np.int64), ("task_id", np.int64),
@@ -250,7 +252,7 @@ def slab_columns(slab, row0=None, slen=None, cols=None):
 CdrDevBatch = _S("cdr_dev_batch", [
     ("ev", CdrSlices), ("scratch", C.c_void_p), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
     ("n_wfs", u32), ("empty_uuid", u32), ("max_act_slots", u32), ("max_tim_slots", u32),
-    ("n_fast_slices", u32), ("n_wave_slices", u32), ("n_reg_slices", u32), ("_pad_reg", u32),
+    ("n_fast_slices", u32), ("n_wave_slices", u32), ("n_reg_slices", u32), ("n_reg2_slices", u32),
     ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64), ("carry", C.c_void_p)])
 
 # ------------------------------------------------------------------ synth

@@ -269,7 +269,10 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   db.ev.slice_flags = (const uint32_t*)up(sflags.data(), ns * 4ull);
   db.n_fast_slices = n_fast;
   db.n_wave_slices = n_wave;
-  for (uint32_t i = 0; i < ns; i++) db.n_reg_slices += (sflags[i] & CDR_SLICE_REG) ? 1u : 0u;
+  for (uint32_t i = 0; i < ns; i++) {
+    db.n_reg_slices += (sflags[i] & CDR_SLICE_REG) ? 1u : 0u;
+    db.n_reg2_slices += (sflags[i] & CDR_SLICE_REG2) ? 1u : 0u;
+  }
   db.ev.slice_scratch_off = (const uint64_t*)up(sc_off.data(), ns * 8ull);
   db.ev.slice_act_slots = (const uint32_t*)up(sc_act.data(), ns * 4ull);
   db.ev.slice_tim_slots = (const uint32_t*)up(sc_tim.data(), ns * 4ull);

@@ -211,10 +211,11 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
         lv_max[1] + lv_max[2] + lv_max[3] <= lim[2] && n <= lim[3])
       c.flags |= CDR_CAP_LANE;
   }
-  reg = reg && !(c.flags & CDR_CAP_FAST) && live_max <= (int64_t)CDR_REG_NA && lv_max[0] <= CDR_REG_NT &&
-        lv_max[1] <= CDR_REG_NX && lv_max[2] <= CDR_REG_NX && lv_max[3] <= CDR_REG_NX &&
-        rp_cks.size() <= CDR_REG_NRP && sa_keys.size() <= CDR_REG_NSA;
-  if (reg) c.flags |= CDR_CAP_REG;
+  reg = reg && !(c.flags & CDR_CAP_FAST) && lv_max[0] <= CDR_REG_NT && lv_max[1] <= CDR_REG_NX &&
+        lv_max[2] <= CDR_REG_NX && lv_max[3] <= CDR_REG_NX && rp_cks.size() <= CDR_REG_NRP &&
+        sa_keys.size() <= CDR_REG_NSA;
+  if (reg && live_max <= (int64_t)CDR_REG_NA) c.flags |= CDR_CAP_REG;
+  else if (reg && live_max <= (int64_t)CDR_REG2_NA) c.flags |= CDR_CAP_REG2;
   *out = c;
 }
 
@@ -485,7 +486,7 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
       c.sa_cap += r.n_search_attr;
       c.act_live += r.n_activity;
       c.timer_live += r.n_timer;
-      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_REG);
+      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_REG | CDR_CAP_REG2);
     }
     cdr_internal::task_caps(b->events + d.ev_off, d.ev_len, &c.xfer_cap, &c.ttask_cap);
     c.xfer_off = t.xfer;
@@ -523,7 +524,7 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   lanes.reserve(n_wfs);
   for (uint32_t w = 0; w < n_wfs; w++)
     ((mode & CDR_PLAN_WAVE) && (caps[w].flags & CDR_CAP_WAVE) &&
-             ((mode & CDR_PLAN_WAVE_ALL) || !(caps[w].flags & (CDR_CAP_LANE | CDR_CAP_REG)))
+             ((mode & CDR_PLAN_WAVE_ALL) || !(caps[w].flags & (CDR_CAP_LANE | CDR_CAP_REG | CDR_CAP_REG2)))
          ? waves
          : lanes)
         .push_back(w);
@@ -539,7 +540,11 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   // kernel groups first (fast-path, register-table, general), so that slices are
   // homogeneous and go to the specialised kernels whole
   auto group = [&](uint32_t a) {
-    return !caps ? 0u : (caps[a].flags & CDR_CAP_FAST) ? 0u : (caps[a].flags & CDR_CAP_REG) ? 1u : 2u;
+    return !caps                               ? 0u
+           : (caps[a].flags & CDR_CAP_FAST)  ? 0u
+           : (caps[a].flags & CDR_CAP_REG)   ? 1u
+           : (caps[a].flags & CDR_CAP_REG2)  ? 2u
+                                             : 3u;
   };
   auto lane_order = [&](uint32_t a, uint32_t c) {
     const uint32_t ga = group(a), gc = group(c);
@@ -552,13 +557,27 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   };
   std::stable_sort(lanes.begin(), lanes.end(), lane_order);
   std::stable_sort(waves.begin(), waves.end(), longer);
+  // each kernel group starts a slice of its own (a mixed slice would replay on the
+  // general kernel at the length of the next group's longest histories)
+  {
+    std::vector<uint32_t> padded;
+    padded.reserve(lanes.size() + 3 * CDR_SLICE_WIDTH);
+    for (size_t i = 0; i < lanes.size(); i++) {
+      if (i > 0 && group(lanes[i]) != group(lanes[i - 1]))
+        while (padded.size() % CDR_SLICE_WIDTH) padded.push_back(UINT32_MAX);
+      padded.push_back(lanes[i]);
+    }
+    lanes.swap(padded);
+  }
   const uint32_t nl = (uint32_t)((lanes.size() + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
   const uint32_t nw = (uint32_t)waves.size();
   uint64_t rows = 0;
   for (uint32_t s = 0; s < nl; s++) {
     uint32_t len = 0;  // the slice's longest lane
-    for (uint32_t l = 0; l < CDR_SLICE_WIDTH && (size_t)s * CDR_SLICE_WIDTH + l < lanes.size(); l++)
-      len = std::max(len, (uint32_t)wfs[lanes[(size_t)s * CDR_SLICE_WIDTH + l]].ev_len);
+    for (uint32_t l = 0; l < CDR_SLICE_WIDTH && (size_t)s * CDR_SLICE_WIDTH + l < lanes.size(); l++) {
+      const uint32_t w = lanes[(size_t)s * CDR_SLICE_WIDTH + l];
+      if (w != UINT32_MAX) len = std::max(len, (uint32_t)wfs[w].ev_len);
+    }
     if (slice_len) slice_len[s] = len;
     if (slice_row0) slice_row0[s] = rows;
     if (slice_flags) slice_flags[s] = 0;
@@ -566,7 +585,7 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     if (lane_wf)
       for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
         const size_t i = (size_t)s * CDR_SLICE_WIDTH + l;
-        lane_wf[i] = i < lanes.size() ? (int32_t)lanes[i] : -1;
+        lane_wf[i] = (i < lanes.size() && lanes[i] != UINT32_MAX) ? (int32_t)lanes[i] : -1;
       }
   }
   for (uint32_t q = 0; q < nw; q++) {
@@ -607,7 +626,7 @@ int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n
       continue;
     }
     uint32_t a = 0, t = 0, lanes = 0;
-    bool fast = true, reg = true;
+    bool fast = true, reg = true, reg2 = true;
     for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
       const int32_t w = lane_wf[(size_t)s * CDR_SLICE_WIDTH + l];
       if (w < 0) continue;
@@ -615,15 +634,17 @@ int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n
       t = std::max(t, caps[w].timer_live);
       fast = fast && (caps[w].flags & CDR_CAP_FAST);
       reg = reg && (caps[w].flags & CDR_CAP_REG);
+      reg2 = reg2 && (caps[w].flags & (CDR_CAP_REG | CDR_CAP_REG2));
       lanes++;
     }
     fast = fast && lanes > 0;
     reg = reg && lanes > 0 && !fast;
+    reg2 = reg2 && lanes > 0 && !fast && !reg;
     nf += fast ? 1u : 0u;
     if (scratch_off) scratch_off[s] = off;
     if (act_slots) act_slots[s] = a;
     if (tim_slots) tim_slots[s] = t;
-    if (slice_flags) slice_flags[s] = fast ? CDR_SLICE_FAST : reg ? CDR_SLICE_REG : 0u;
+    if (slice_flags) slice_flags[s] = fast ? CDR_SLICE_FAST : reg ? CDR_SLICE_REG : reg2 ? CDR_SLICE_REG2 : 0u;
     off += ((uint64_t)a * CDR_ACT_PLANES + (uint64_t)t * CDR_TIM_PLANES) * CDR_SLICE_WIDTH;
   }
   *total_words = off;

@@ -503,7 +503,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     const uint32_t sf = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_flags[s]);
     if (sf & CDR_SLICE_WAVE) return;  // k_replay_wave
     if (KA()->fast && (sf & CDR_SLICE_FAST)) return;
-    if (KA()->reg && (sf & CDR_SLICE_REG)) return;  // k_replay_reg
+    if (KA()->reg && (sf & (CDR_SLICE_REG | CDR_SLICE_REG2))) return;  // k_replay_reg
   }
   const uint64_t row0_ = KA()->B.ev.slice_row0[s];
   const uint64_t row0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(row0_ >> 32)) << 32) |
@@ -1784,17 +1784,29 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   if (tasks && (in->n_wave_slices > 0 || !out->timer_tasks || !out->n_tasks)) return CDR_API_EINVAL;
   const bool fast = c->fast && in->n_fast_slices > 0 && !tasks;
   // register-table kernel: LastReplicationInfo kept for clusters < CDR_REG_NCL only
-  const bool reg = c->fast && c->reg && in->n_reg_slices > 0 && !tasks && in->cluster.n_clusters <= (int)CDR_REG_NCL;
+  const bool reg = c->fast && c->reg && in->n_reg_slices + in->n_reg2_slices > 0 && !tasks &&
+                   in->cluster.n_clusters <= (int)CDR_REG_NCL;
   const bool wave = in->n_wave_slices > 0;
-  const bool general =
-      (fast ? in->n_fast_slices : 0u) + (reg ? in->n_reg_slices : 0u) + in->n_wave_slices < in->ev.n_slices;
+  const bool general = (fast ? in->n_fast_slices : 0u) + (reg ? in->n_reg_slices + in->n_reg2_slices : 0u) +
+                           in->n_wave_slices <
+                       in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
   cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u};
   if (blocks && fast)
     hipLaunchKernelGGL(k_replay_fast, dim3(blocks), dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, st, L);
   HIPCHK(hipGetLastError());
-  if (blocks && reg) hipLaunchKernelGGL(k_replay_reg, dim3(blocks), dim3(CDR_SLICE_WIDTH), REG_LDS_BYTES, st, L);
+  if (blocks && reg && in->n_reg_slices) {
+    typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
+    hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), dim3(blocks),
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, st, L);
+  }
+  HIPCHK(hipGetLastError());
+  if (blocks && reg && in->n_reg2_slices) {
+    typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
+    hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), dim3(blocks),
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, st, L);
+  }
   HIPCHK(hipGetLastError());
   // the wave kernel on the side stream when lane slices also run: both kernels' waves
   // share the CUs (wave slices: scalar unit; lane slices: VALU)

@@ -111,6 +111,8 @@ class DeviceBatch:
         db.n_fast_slices = self.n_fast
         db.n_wave_slices = self.n_wave
         db.n_reg_slices = self.n_reg
+        self.n_reg2 = int(((self.h_sflags & abi.SLICE_REG2) != 0).sum())
+        db.n_reg2_slices = self.n_reg2
         db.empty_uuid = meta.empty_uuid
         db.cluster = meta.cluster
         db.now_ns = meta.now_ns

@@ -129,6 +129,9 @@ typedef struct cdr_slices {
  * (replay_reg.inc: entity tables in registers, no global memory traffic in the step
  * loop beyond the event stream) */
 #define CDR_SLICE_REG 0x4u
+/* every lane's history has CDR_CAP_REG2 or CDR_CAP_REG: the register-table kernel's
+ * variant with CDR_REG2_NA activity slots */
+#define CDR_SLICE_REG2 0x8u
 /* event types the fast-path kernel replays (bit = cdr_event_type) */
 #define CDR_FAST_TYPES                                                                                       \
   (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_WF_COMPLETED) | CDR_TB(CDR_EV_WF_FAILED) |                      \
@@ -214,7 +217,7 @@ typedef struct cdr_dev_batch {
   uint32_t n_fast_slices; /* slices with CDR_SLICE_FAST (cdr_plan_scratch) */
   uint32_t n_wave_slices; /* slices with CDR_SLICE_WAVE (cdr_plan_slices_ex) */
   uint32_t n_reg_slices;  /* slices with CDR_SLICE_REG (cdr_plan_scratch) */
-  uint32_t _pad_reg;
+  uint32_t n_reg2_slices; /* slices with CDR_SLICE_REG2 (cdr_plan_scratch) */
   cdr_cluster_meta cluster;
   int64_t now_ns;
   uint64_t uuid_seed;

@@ -578,6 +578,10 @@ typedef struct cdr_wf_caps {
 #define CDR_REG_NRP 8u
 #define CDR_REG_NSA 8u
 #define CDR_REG_NCL 4u /* 2DC: LastReplicationInfo kept for clusters < 4 (batch with more: general kernel) */
+/* the same envelope with up to CDR_REG2_NA live activities (long activity-heavy
+ * histories, C4/C5 tails): the kernel's second variant, at lower occupancy */
+#define CDR_CAP_REG2 0x10u
+#define CDR_REG2_NA 12u
 #define CDR_LANE_MAX_ACT 6u
 #define CDR_LANE_MAX_TIMERS 10u
 #define CDR_LANE_MAX_EXT 8u

@@ -25,38 +25,49 @@ N_WFS = int(os.environ.get("CDR_FULLSIZE_WFS", "1000000"))
 THREADS = int(os.environ.get("CDR_CPU_THREADS", "16"))
 
 
-def _gpu_digests(ctx, cfg, index_map, seed, plan_mode):
+def _gpu_digests(ctx, cfg, index_map, seed, plan_mode, reg):
     import torch
     from cadence_amd.synth import DeviceBatch
     import ctypes as C
     db = DeviceBatch(torch, cfg, index_map, seed, plan_mode=plan_mode)
     stream = torch.cuda.current_stream().cuda_stream
-    rc = abi.lib().cdr_replay_sliced_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(stream))
+    L = abi.lib()
+    L.cdr_set_reg_path(ctx, int(reg))
+    try:
+        rc = L.cdr_replay_sliced_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(stream))
+    finally:
+        L.cdr_set_reg_path(ctx, 1)
     assert rc == 0, rc
     per, tot = db.digests(ctx, stream)
-    n_wave = db.n_wave
+    kinds = {"wave": db.n_wave, "reg": db.n_reg, "reg2": db.n_reg2}
     del db
     torch.cuda.empty_cache()
-    return per, tot, n_wave
+    return per, tot, kinds
 
 
-@pytest.mark.parametrize("cfg,plan_mode", [
-    (2, abi.PLAN_WAVE),
-    (3, abi.PLAN_WAVE),
-    (3, abi.PLAN_WAVE | abi.PLAN_WAVE_ALL),
-    (4, abi.PLAN_WAVE),
-    (5, abi.PLAN_WAVE),
+@pytest.mark.parametrize("cfg,plan_mode,reg", [
+    (2, abi.PLAN_WAVE, True),
+    (3, abi.PLAN_WAVE, True),
+    (3, abi.PLAN_WAVE | abi.PLAN_WAVE_ALL, True),
+    (4, abi.PLAN_WAVE, True),
+    (5, abi.PLAN_WAVE, True),
+    (5, abi.PLAN_WAVE, False),  # register-table slices on the general kernel
 ])
-def test_fullsize_entry_digests(engine_gpu, cfg, plan_mode):
+def test_fullsize_entry_digests(engine_gpu, cfg, plan_mode, reg):
     import oracle
     seed = 0x5EED0000 + cfg
     index_map = np.arange(N_WFS, dtype=np.uint32)
-    got, got_sum, n_wave = _gpu_digests(engine_gpu.ctx, cfg, index_map, seed, plan_mode)
+    got, got_sum, kinds = _gpu_digests(engine_gpu.ctx, cfg, index_map, seed, plan_mode, reg)
     want, want_sum, hist = oracle.synth_digests(cfg, index_map, seed, threads=THREADS)
     assert len(got) == len(want)
     bad = np.nonzero(got != want)[0]
     assert len(bad) == 0, f"C{cfg}: {len(bad)} of {len(want)} entries differ, first {bad[:10].tolist()}"
     assert got_sum == want_sum
     assert hist.get("OK", 0) == len(want), hist  # clean populations replay OK throughout
-    if cfg in (3, 4, 5):
-        assert n_wave > 0  # the wave kernel took part
+    # the kernels that took part
+    if plan_mode & abi.PLAN_WAVE_ALL:
+        assert kinds["wave"] > 0
+    elif cfg in (3, 4, 5):
+        assert kinds["reg"] > 0, kinds
+    if cfg in (4, 5) and not plan_mode & abi.PLAN_WAVE_ALL:
+        assert kinds["reg2"] > 0, kinds

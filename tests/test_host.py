@@ -225,8 +225,9 @@ def test_wave_slices_plan_and_pack():
 
 
 def test_lane_friendly_entries_stay_in_lane_slices():
-    """CDR_CAP_LANE (small working sets, moderate length) keeps a divergent history in a
-    lane slice under CDR_PLAN_WAVE; PLAN_WAVE_ALL sends it to a wave slice."""
+    """CDR_CAP_LANE (small working sets, moderate length) and the register-table caps keep
+    a divergent history in a lane slice under CDR_PLAN_WAVE; PLAN_WAVE_ALL sends it to a
+    wave slice."""
     b = engine.synth_batch(3, 300, seed=12)
     pl = engine.plan(b)
     lane_ok = [w for w in range(b.n_wfs) if pl.caps[w].flags & abi.CAP_LANE]
@@ -236,4 +237,7 @@ def test_lane_friendly_entries_stay_in_lane_slices():
         assert c.act_live <= 6 and c.timer_live <= 10 and b.wfs[w].ev_len <= 512
     n_all = engine.slice_kinds(b, pl, abi.PLAN_WAVE | abi.PLAN_WAVE_ALL)[1]
     n_def = engine.slice_kinds(b, pl, abi.PLAN_WAVE)[1]
-    assert n_def == n_all - len(lane_ok)
+    # register-table entries (CDR_CAP_REG / REG2) also stay in lane slices
+    keep = [w for w in range(b.n_wfs) if (pl.caps[w].flags & abi.CAP_WAVE) and
+            (pl.caps[w].flags & (abi.CAP_LANE | abi.CAP_REG | abi.CAP_REG2))]
+    assert n_def == n_all - len(keep)
