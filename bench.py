@@ -301,7 +301,7 @@ def main():
         dist = None
         torch.cuda.set_device(0)
     L = abi.lib()
-    ctx = L.cdr_create(torch.cuda.current_device())
+    ctx = L.cdr_create(torch.cuda.current_device(), None)
     if not ctx:
         raise SystemExit("cdr_create failed (no GPU?) — the engine has no CPU fallback")
     if args.no_fast_path:

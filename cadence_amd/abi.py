@@ -187,7 +187,14 @@ CdrTotals = _S("cdr_totals", [(n, u64) for n in ("act", "timer", "child", "cance
                                                  "xfer", "ttask")])
 CdrOut = _S("cdr_out", [(n, C.c_void_p) for n in (
     "result", "exec", "repl", "vh", "act", "timer", "child", "cancel", "signal", "rp", "sa", "transfer",
-    "timer_tasks", "n_tasks")])
+    "timer_tasks", "n_tasks", "last_decision")])
+CdrLastDecision = _S("cdr_last_decision", [
+    ("source", u32), ("request_id", u32), ("event_index", i64), ("version", i64), ("schedule_id", i64),
+    ("started_id", i64), ("attempt", i64), ("scheduled_ts", i64), ("started_ts", i64),
+    ("original_scheduled_ts", i64), ("decision_timeout", i32), ("_pad", i32)])
+LD_NONE, LD_SCHEDULED, LD_STARTED, LD_TRANSIENT = range(4)
+CdrOpts = _S("cdr_opts", [("plan_mode", u32), ("fast_path", i32), ("reg_path", i32), ("concurrent", i32),
+                          ("workspace_bytes", u64)])
 CdrVHToken = _S("cdr_vh_token", [("tree", u32), ("_pad", u32), ("branch_lo", u64), ("branch_hi", u64)])
 CdrVHBranch = _S("cdr_vh_branch", [("token", CdrVHToken), ("n_items", u32), ("_pad", u32)])
 VHS_MAX_BRANCHES = 8
@@ -278,7 +285,8 @@ MIRRORS = {
     "cdr_wf_result": CdrWfResult, "cdr_wf_caps": CdrWfCaps, "cdr_totals": CdrTotals, "cdr_out": CdrOut,
     "cdr_slices": CdrSlices, "cdr_dev_batch": CdrDevBatch, "cdr_carry": CdrCarry,
     "cdr_task": CdrTask, "cdr_vh_token": CdrVHToken, "cdr_vh_branch": CdrVHBranch, "cdr_vhs": CdrVHS,
-    "cdr_ndc_task": CdrNdcTask, "cdr_ndc_decision": CdrNdcDecision,
+    "cdr_ndc_task": CdrNdcTask, "cdr_ndc_decision": CdrNdcDecision, "cdr_last_decision": CdrLastDecision,
+    "cdr_opts": CdrOpts,
 }
 
 # C ABI entry points declared in include/cdr/cdr.h and include/cdr/synth.h
@@ -295,15 +303,18 @@ EXPORTS = {
     "cdr_set_reg_path": (i32, [C.c_void_p, i32]),
     "cdr_set_plan_mode": (i32, [C.c_void_p, u32]),
     "cdr_pack_slices": (i32, [C.POINTER(CdrBatch), C.POINTER(CdrSlices), i32]),
-    "cdr_create": (C.c_void_p, [i32]),
+    "cdr_create": (C.c_void_p, [i32, C.c_void_p]),
+    "cdr_opts_default": (None, [C.c_void_p]),
     "cdr_destroy": (None, [C.c_void_p]),
     "cdr_replay_sliced_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p]),
     "cdr_replay_batch": (i32, [C.c_void_p, C.POINTER(CdrBatch), C.POINTER(CdrWfCaps), C.POINTER(CdrTotals),
-                               C.POINTER(CdrOut)]),
+                               C.POINTER(CdrOut), C.c_void_p]),
+    "cdr_replay_one": (i32, [C.c_void_p, C.POINTER(CdrBatch), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                             C.c_void_p]),
     "cdr_refresh_tasks_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), i64, u32,
                                       C.c_void_p]),
     "cdr_rebuild_batch": (i32, [C.c_void_p, C.POINTER(CdrBatch), C.POINTER(CdrWfCaps), C.POINTER(CdrTotals),
-                                C.POINTER(CdrOut), u32]),
+                                C.POINTER(CdrOut), u32, C.c_void_p]),
     "cdr_encode_rows_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
                                     C.c_void_p]),
     "cdr_compact_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "cdr/cdr.h"
+#include "ctx.h"
 
 extern "C" uint32_t cdr_get_plan_mode(const cdr_ctx* ctx);  // replay.hip
 
@@ -22,7 +23,6 @@ extern "C" uint32_t cdr_get_plan_mode(const cdr_ctx* ctx);  // replay.hip
     }                                                                                                 \
   } while (0)
 
-struct cdr_ctx;  // defined in replay.hip
 
 namespace {
 
@@ -118,18 +118,11 @@ __global__ void k_digest(cdr_dev_batch B, cdr_out O, uint64_t* per_entry, unsign
   if ((threadIdx.x & 63) == 0 && h) atomicAdd(sum, (unsigned long long)h);
 }
 
-template <class T>
-int dmalloc(T** p, uint64_t n) {
-  *p = nullptr;
-  if (n == 0) n = 1;
-  HIPCHK(hipMalloc((void**)p, n * sizeof(T)));
-  return CDR_API_OK;
-}
 
 }  // namespace
 
 static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot,
-                       cdr_out* out, bool refresh, uint32_t rflags);
+                       cdr_out* out, bool refresh, uint32_t rflags, hipStream_t st);
 
 extern "C" {
 
@@ -183,22 +176,58 @@ int cdr_checksum_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out
   return cdr_entry_digests_async(ctx, in, out, nullptr, dev_sum, stream);
 }
 
-int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot, cdr_out* out) {
-  return replay_host(ctx, b, caps, tot, out, false, 0);
+int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot, cdr_out* out,
+                     void* stream) {
+  return replay_host(ctx, b, caps, tot, out, false, 0, (hipStream_t)stream);
 }
 
 int cdr_rebuild_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot, cdr_out* out,
-                      uint32_t flags) {
+                      uint32_t flags, void* stream) {
   if (!out || !out->transfer || !out->timer_tasks || !out->n_tasks) return CDR_API_EINVAL;
-  return replay_host(ctx, b, caps, tot, out, true, flags);
+  return replay_host(ctx, b, caps, tot, out, true, flags, (hipStream_t)stream);
+}
+
+int cdr_replay_one(cdr_ctx* ctx, const cdr_batch* b, const cdr_out** view, const cdr_wf_caps** caps, void* stream) {
+  if (!ctx || !b || !view || !caps || b->n_wfs < 1 || b->n_wfs > 2) return CDR_API_EINVAL;
+  if (b->wfs[0].parent >= 0 || (b->n_wfs == 2 && b->wfs[0].newrun != 1)) return CDR_API_EINVAL;
+  cdr_one_host& H = ctx->one;
+  const uint32_t n = b->n_wfs;
+  H.caps.resize(n);
+  cdr_totals tot{};
+  int rc = cdr_plan_caps(b, H.caps.data(), &tot);
+  if (rc) return rc;
+  // grow-only host buffers: resize keeps the capacity (records are fully written for
+  // OK entries; the replay pipeline downloads every slot)
+  auto fit = [](auto& v, uint64_t k) { v.resize(k ? k : 1); return v.data(); };
+  cdr_out& o = H.view;
+  o = cdr_out{};
+  o.result = fit(H.result, n);
+  o.exec = fit(H.exec, n);
+  o.repl = fit(H.repl, n);
+  o.vh = fit(H.vh, tot.vh);
+  o.act = fit(H.act, tot.act);
+  o.timer = fit(H.timer, tot.timer);
+  o.child = fit(H.child, tot.child);
+  o.cancel = fit(H.cancel, tot.cancel);
+  o.signal = fit(H.signal, tot.signal);
+  o.rp = fit(H.rp, tot.rp);
+  o.sa = fit(H.sa, tot.sa);
+  o.last_decision = fit(H.ld, n);
+  rc = replay_host(ctx, b, H.caps.data(), &tot, &o, false, 0, (hipStream_t)stream);
+  if (rc) return rc;
+  *view = &o;
+  *caps = H.caps.data();
+  return CDR_API_OK;
 }
 
 }  // extern "C"
 
-// plan + pack + H2D + replay (+ refreshTasks) + D2H
+// plan + pack + H2D + replay (+ refreshTasks) + D2H, on `st` with the context's
+// grow-only device workspace
 static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* tot,
-                       cdr_out* out, bool refresh, uint32_t rflags) {
-  if (!ctx || !b || !caps || !tot || !out) return CDR_API_EINVAL;
+                       cdr_out* out, bool refresh, uint32_t rflags, hipStream_t st) {
+  if (!ctx || !b || !caps || !tot || !out || !out->result) return CDR_API_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));  // the context's device, whatever thread calls
   // ---- plan + pack on the host
   uint32_t ns = 0, n_wave = 0;
   uint64_t rows = 0;
@@ -230,35 +259,6 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   hs.arena = arena.data();
   rc = cdr_pack_slices(b, &hs, 0);
   if (rc) return rc;
-
-  // ---- device buffers
-  std::vector<void*> allocs;
-  auto up = [&](const void* src, uint64_t bytes) -> void* {
-    void* p = nullptr;
-    if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess) return nullptr;
-    allocs.push_back(p);
-    if (bytes && hipMemcpy(p, src, bytes, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
-    return p;
-  };
-  auto dz = [&](uint64_t bytes) -> void* {
-    void* p = nullptr;
-    if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess) return nullptr;
-    allocs.push_back(p);
-    (void)hipMemset(p, 0, bytes ? bytes : 8);
-    return p;
-  };
-  auto free_all = [&]() {
-    for (void* p : allocs) (void)hipFree(p);
-  };
-  cdr_dev_batch db{};
-  db.ev.n_slices = ns;
-  db.ev.n_rows = rows;
-  db.ev.arena_words = aw;
-  db.ev.slice_row0 = (const uint64_t*)up(row0.data(), ns * 8ull);
-  db.ev.slice_len = (const uint32_t*)up(slen.data(), ns * 4ull);
-  db.ev.lane_wf = (const int32_t*)up(lane.data(), lane.size() * 4ull);
-  db.ev.slab = (const uint8_t*)up(slab.data(), slab.size());
-  db.ev.arena = (const uint64_t*)up(arena.data(), arena.size() * 8);
   std::vector<uint64_t> sc_off(ns);
   std::vector<uint32_t> sc_act(ns), sc_tim(ns);
   uint64_t sc_words = 0;
@@ -266,44 +266,79 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   rc = cdr_plan_scratch(caps, lane.data(), ns, sc_off.data(), sc_act.data(), sc_tim.data(), sflags.data(), &sc_words,
                         &n_fast);
   if (rc) return rc;
-  db.ev.slice_flags = (const uint32_t*)up(sflags.data(), ns * 4ull);
+
+  // ---- device buffers: workspace slots (no allocation once the context is warm);
+  // any failed allocation or copy is reported before anything is launched
+  bool oom = false, dev_err = false;
+  auto up = [&](int slot, const void* src, uint64_t bytes) -> void* {
+    void* p = cdr_ws_get(ctx, slot, bytes);
+    if (!p) {
+      oom = true;
+      return nullptr;
+    }
+    if (bytes && src && hipMemcpyAsync(p, src, bytes, hipMemcpyHostToDevice, st) != hipSuccess) dev_err = true;
+    return p;
+  };
+  auto dz = [&](int slot, uint64_t bytes) -> void* {
+    void* p = cdr_ws_get(ctx, slot, bytes);
+    if (!p) {
+      oom = true;
+      return nullptr;
+    }
+    if (hipMemsetAsync(p, 0, bytes ? bytes : 8, st) != hipSuccess) dev_err = true;
+    return p;
+  };
+  cdr_dev_batch db{};
+  db.ev.n_slices = ns;
+  db.ev.n_rows = rows;
+  db.ev.arena_words = aw;
+  db.ev.slice_row0 = (const uint64_t*)up(WS_ROW0, row0.data(), ns * 8ull);
+  db.ev.slice_len = (const uint32_t*)up(WS_SLEN, slen.data(), ns * 4ull);
+  db.ev.lane_wf = (const int32_t*)up(WS_LANE, lane.data(), lane.size() * 4ull);
+  db.ev.slab = (const uint8_t*)up(WS_SLAB, slab.data(), slab.size());
+  db.ev.arena = (const uint64_t*)up(WS_ARENA, arena.data(), arena.size() * 8);
+  db.ev.slice_flags = (const uint32_t*)up(WS_SFLAGS, sflags.data(), ns * 4ull);
   db.n_fast_slices = n_fast;
   db.n_wave_slices = n_wave;
   for (uint32_t i = 0; i < ns; i++) {
     db.n_reg_slices += (sflags[i] & CDR_SLICE_REG) ? 1u : 0u;
     db.n_reg2_slices += (sflags[i] & CDR_SLICE_REG2) ? 1u : 0u;
   }
-  db.ev.slice_scratch_off = (const uint64_t*)up(sc_off.data(), ns * 8ull);
-  db.ev.slice_act_slots = (const uint32_t*)up(sc_act.data(), ns * 4ull);
-  db.ev.slice_tim_slots = (const uint32_t*)up(sc_tim.data(), ns * 4ull);
+  db.ev.slice_scratch_off = (const uint64_t*)up(WS_SC_OFF, sc_off.data(), ns * 8ull);
+  db.ev.slice_act_slots = (const uint32_t*)up(WS_SC_ACT, sc_act.data(), ns * 4ull);
+  db.ev.slice_tim_slots = (const uint32_t*)up(WS_SC_TIM, sc_tim.data(), ns * 4ull);
   for (uint32_t i = 0; i < ns; i++) {
     db.max_act_slots = sc_act[i] > db.max_act_slots ? sc_act[i] : db.max_act_slots;
     db.max_tim_slots = sc_tim[i] > db.max_tim_slots ? sc_tim[i] : db.max_tim_slots;
   }
-  db.scratch = (uint64_t*)dz(sc_words * 8);
-  db.wfs = (const cdr_wf_desc*)up(b->wfs, (uint64_t)b->n_wfs * sizeof(cdr_wf_desc));
-  db.caps = (const cdr_wf_caps*)up(caps, (uint64_t)b->n_wfs * sizeof(cdr_wf_caps));
-  db.kvs = (const cdr_kv*)up(b->kvs, b->n_kvs * sizeof(cdr_kv));
-  db.rps = (const cdr_reset_point*)up(b->rps, b->n_rps * sizeof(cdr_reset_point));
+  db.scratch = (uint64_t*)dz(WS_SCRATCH, sc_words * 8);
+  db.wfs = (const cdr_wf_desc*)up(WS_WFS, b->wfs, (uint64_t)b->n_wfs * sizeof(cdr_wf_desc));
+  db.caps = (const cdr_wf_caps*)up(WS_CAPS, caps, (uint64_t)b->n_wfs * sizeof(cdr_wf_caps));
+  db.kvs = (const cdr_kv*)up(WS_KVS, b->kvs, b->n_kvs * sizeof(cdr_kv));
+  db.rps = (const cdr_reset_point*)up(WS_RPS, b->rps, b->n_rps * sizeof(cdr_reset_point));
+  cdr_carry dc{};
   if (b->carry && b->carry->src) {  // the loaded states, copied to the device as they are
     const cdr_carry& hc = *b->carry;
     const cdr_totals& t = hc.totals;
     const uint64_t n = hc.n_src;
-    cdr_carry dc = hc;
-    dc.src = (const int32_t*)up(hc.src, (uint64_t)b->n_wfs * 4);
-    dc.caps = (const cdr_wf_caps*)up(hc.caps, n * sizeof(cdr_wf_caps));
-    dc.state.result = (cdr_wf_result*)up(hc.state.result, n * sizeof(cdr_wf_result));
-    dc.state.exec = (cdr_exec_info*)up(hc.state.exec, n * sizeof(cdr_exec_info));
-    dc.state.repl = (cdr_repl_state*)up(hc.state.repl, n * sizeof(cdr_repl_state));
-    dc.state.vh = (cdr_vh_item*)up(hc.state.vh, t.vh * sizeof(cdr_vh_item));
-    dc.state.act = (cdr_activity_info*)up(hc.state.act, t.act * sizeof(cdr_activity_info));
-    dc.state.timer = (cdr_timer_info*)up(hc.state.timer, t.timer * sizeof(cdr_timer_info));
-    dc.state.child = (cdr_child_info*)up(hc.state.child, t.child * sizeof(cdr_child_info));
-    dc.state.cancel = (cdr_cancel_info*)up(hc.state.cancel, t.cancel * sizeof(cdr_cancel_info));
-    dc.state.signal = (cdr_signal_info*)up(hc.state.signal, t.signal * sizeof(cdr_signal_info));
-    dc.state.rp = (cdr_reset_point*)up(hc.state.rp, t.rp * sizeof(cdr_reset_point));
-    dc.state.sa = (cdr_kv*)up(hc.state.sa, t.sa * sizeof(cdr_kv));
-    db.carry = (const cdr_carry*)up(&dc, sizeof(dc));
+    dc = hc;
+    dc.src = (const int32_t*)up(WS_CY_SRC, hc.src, (uint64_t)b->n_wfs * 4);
+    dc.caps = (const cdr_wf_caps*)up(WS_CY_CAPS, hc.caps, n * sizeof(cdr_wf_caps));
+    dc.state.result = (cdr_wf_result*)up(WS_CY_RESULT, hc.state.result, n * sizeof(cdr_wf_result));
+    dc.state.exec = (cdr_exec_info*)up(WS_CY_EXEC, hc.state.exec, n * sizeof(cdr_exec_info));
+    dc.state.repl = (cdr_repl_state*)up(WS_CY_REPL, hc.state.repl, n * sizeof(cdr_repl_state));
+    dc.state.vh = (cdr_vh_item*)up(WS_CY_VH, hc.state.vh, t.vh * sizeof(cdr_vh_item));
+    dc.state.act = (cdr_activity_info*)up(WS_CY_ACT, hc.state.act, t.act * sizeof(cdr_activity_info));
+    dc.state.timer = (cdr_timer_info*)up(WS_CY_TIMER, hc.state.timer, t.timer * sizeof(cdr_timer_info));
+    dc.state.child = (cdr_child_info*)up(WS_CY_CHILD, hc.state.child, t.child * sizeof(cdr_child_info));
+    dc.state.cancel = (cdr_cancel_info*)up(WS_CY_CANCEL, hc.state.cancel, t.cancel * sizeof(cdr_cancel_info));
+    dc.state.signal = (cdr_signal_info*)up(WS_CY_SIGNAL, hc.state.signal, t.signal * sizeof(cdr_signal_info));
+    dc.state.rp = (cdr_reset_point*)up(WS_CY_RP, hc.state.rp, t.rp * sizeof(cdr_reset_point));
+    dc.state.sa = (cdr_kv*)up(WS_CY_SA, hc.state.sa, t.sa * sizeof(cdr_kv));
+    dc.state.transfer = dc.state.timer_tasks = nullptr;
+    dc.state.n_tasks = nullptr;
+    dc.state.last_decision = nullptr;
+    db.carry = (const cdr_carry*)up(WS_CY_DESC, &dc, sizeof(dc));
   }
   db.n_wfs = b->n_wfs;
   db.empty_uuid = b->empty_uuid;
@@ -311,39 +346,39 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   db.now_ns = b->now_ns;
   db.uuid_seed = b->uuid_seed;
   cdr_out dout{};
-  dout.result = (cdr_wf_result*)dz((uint64_t)b->n_wfs * sizeof(cdr_wf_result));
-  dout.exec = (cdr_exec_info*)dz((uint64_t)b->n_wfs * sizeof(cdr_exec_info));
-  dout.repl = (cdr_repl_state*)dz((uint64_t)b->n_wfs * sizeof(cdr_repl_state));
-  dout.vh = (cdr_vh_item*)dz(tot->vh * sizeof(cdr_vh_item));
-  dout.act = (cdr_activity_info*)dz(tot->act * sizeof(cdr_activity_info));
-  dout.timer = (cdr_timer_info*)dz(tot->timer * sizeof(cdr_timer_info));
-  dout.child = (cdr_child_info*)dz(tot->child * sizeof(cdr_child_info));
-  dout.cancel = (cdr_cancel_info*)dz(tot->cancel * sizeof(cdr_cancel_info));
-  dout.signal = (cdr_signal_info*)dz(tot->signal * sizeof(cdr_signal_info));
-  dout.rp = (cdr_reset_point*)dz(tot->rp * sizeof(cdr_reset_point));
-  dout.sa = (cdr_kv*)dz(tot->sa * sizeof(cdr_kv));
+  dout.result = (cdr_wf_result*)dz(WS_O_RESULT, (uint64_t)b->n_wfs * sizeof(cdr_wf_result));
+  dout.exec = (cdr_exec_info*)dz(WS_O_EXEC, (uint64_t)b->n_wfs * sizeof(cdr_exec_info));
+  dout.repl = (cdr_repl_state*)dz(WS_O_REPL, (uint64_t)b->n_wfs * sizeof(cdr_repl_state));
+  dout.vh = (cdr_vh_item*)dz(WS_O_VH, tot->vh * sizeof(cdr_vh_item));
+  dout.act = (cdr_activity_info*)dz(WS_O_ACT, tot->act * sizeof(cdr_activity_info));
+  dout.timer = (cdr_timer_info*)dz(WS_O_TIMER, tot->timer * sizeof(cdr_timer_info));
+  dout.child = (cdr_child_info*)dz(WS_O_CHILD, tot->child * sizeof(cdr_child_info));
+  dout.cancel = (cdr_cancel_info*)dz(WS_O_CANCEL, tot->cancel * sizeof(cdr_cancel_info));
+  dout.signal = (cdr_signal_info*)dz(WS_O_SIGNAL, tot->signal * sizeof(cdr_signal_info));
+  dout.rp = (cdr_reset_point*)dz(WS_O_RP, tot->rp * sizeof(cdr_reset_point));
+  dout.sa = (cdr_kv*)dz(WS_O_SA, tot->sa * sizeof(cdr_kv));
+  if (out->last_decision)
+    dout.last_decision = (cdr_last_decision*)dz(WS_O_LD, (uint64_t)b->n_wfs * sizeof(cdr_last_decision));
   if (tasks || refresh) {
-    dout.transfer = (cdr_task*)dz(tot->xfer * sizeof(cdr_task));
-    dout.timer_tasks = (cdr_task*)dz(tot->ttask * sizeof(cdr_task));
-    dout.n_tasks = (uint32_t*)dz((uint64_t)b->n_wfs * 2 * sizeof(uint32_t));
+    dout.transfer = (cdr_task*)dz(WS_O_XFER, tot->xfer * sizeof(cdr_task));
+    dout.timer_tasks = (cdr_task*)dz(WS_O_TTASK, tot->ttask * sizeof(cdr_task));
+    dout.n_tasks = (uint32_t*)dz(WS_O_NTASKS, (uint64_t)b->n_wfs * 2 * sizeof(uint32_t));
   }
-  for (void* p : allocs)
-    if (!p) {
-      free_all();
-      return CDR_API_ENOMEM;
-    }
+  if (oom || dev_err) {
+    (void)hipStreamSynchronize(st);  // no copy may still read the host vectors
+    return oom ? CDR_API_ENOMEM : CDR_API_EDEVICE;
+  }
   if (refresh) {  // the replay itself emits no stateBuilder tasks
     cdr_out rout = dout;
     rout.transfer = rout.timer_tasks = nullptr;
     rout.n_tasks = nullptr;
-    rc = cdr_replay_sliced_async(ctx, &db, &rout, nullptr);
-    if (rc == CDR_API_OK) rc = cdr_refresh_tasks_async(ctx, &db, &dout, b->now_ns, rflags, nullptr);
+    rc = cdr_replay_sliced_async(ctx, &db, &rout, st);
+    if (rc == CDR_API_OK) rc = cdr_refresh_tasks_async(ctx, &db, &dout, b->now_ns, rflags, st);
   } else {
-    rc = cdr_replay_sliced_async(ctx, &db, &dout, nullptr);
+    rc = cdr_replay_sliced_async(ctx, &db, &dout, st);
   }
-  if (rc == CDR_API_OK && hipDeviceSynchronize() != hipSuccess) rc = CDR_API_EDEVICE;
   auto down = [&](void* dst, const void* src, uint64_t bytes) {
-    if (rc == CDR_API_OK && dst && bytes && hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+    if (rc == CDR_API_OK && dst && bytes && hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st) != hipSuccess)
       rc = CDR_API_EDEVICE;
   };
   down(out->result, dout.result, (uint64_t)b->n_wfs * sizeof(cdr_wf_result));
@@ -357,11 +392,13 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   down(out->signal, dout.signal, tot->signal * sizeof(cdr_signal_info));
   down(out->rp, dout.rp, tot->rp * sizeof(cdr_reset_point));
   down(out->sa, dout.sa, tot->sa * sizeof(cdr_kv));
+  down(out->last_decision, dout.last_decision, (uint64_t)b->n_wfs * sizeof(cdr_last_decision));
   if (tasks || refresh) {
     down(out->transfer, dout.transfer, tot->xfer * sizeof(cdr_task));
     down(out->timer_tasks, dout.timer_tasks, tot->ttask * sizeof(cdr_task));
     down(out->n_tasks, dout.n_tasks, (uint64_t)b->n_wfs * 2 * sizeof(uint32_t));
   }
-  free_all();
+  // the stream, not the device: other contexts' work is not waited for
+  if (hipStreamSynchronize(st) != hipSuccess && rc == CDR_API_OK) rc = CDR_API_EDEVICE;
   return rc;
 }

@@ -1,0 +1,70 @@
+// ctx.h — the replay context (cdr_ctx) shared by replay.hip and api.hip.
+//
+// One context per device and caller thread / stream (the analogue of one
+// stateBuilderProvider, historyReplicator.go:54): kernel-routing switches, timing
+// events, the side stream of the wave kernel, and the persistent workspaces of the
+// host-buffer entry points (cdr_replay_batch / cdr_rebuild_batch / cdr_replay_one):
+// device buffers that only grow, so a warmed-up context replays without hipMalloc,
+// and the host-side plan / pack / output buffers of cdr_replay_one.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "cdr/cdr.h"
+
+// device workspace slots of the host-buffer pipeline (api.hip replay_host)
+enum cdr_ws_slot {
+  WS_ROW0, WS_SLEN, WS_LANE, WS_SLAB, WS_ARENA, WS_SFLAGS, WS_SC_OFF, WS_SC_ACT, WS_SC_TIM, WS_SCRATCH,
+  WS_WFS, WS_CAPS, WS_KVS, WS_RPS,
+  WS_CY_SRC, WS_CY_CAPS, WS_CY_RESULT, WS_CY_EXEC, WS_CY_REPL, WS_CY_VH, WS_CY_ACT, WS_CY_TIMER, WS_CY_CHILD,
+  WS_CY_CANCEL, WS_CY_SIGNAL, WS_CY_RP, WS_CY_SA, WS_CY_DESC,
+  WS_O_RESULT, WS_O_EXEC, WS_O_REPL, WS_O_VH, WS_O_ACT, WS_O_TIMER, WS_O_CHILD, WS_O_CANCEL, WS_O_SIGNAL,
+  WS_O_RP, WS_O_SA, WS_O_XFER, WS_O_TTASK, WS_O_NTASKS, WS_O_LD,
+  WS_NUM
+};
+
+// host buffers of cdr_replay_one (valid until the next call on the context)
+struct cdr_one_host {
+  std::vector<cdr_wf_caps> caps;
+  std::vector<cdr_wf_result> result;
+  std::vector<cdr_exec_info> exec;
+  std::vector<cdr_repl_state> repl;
+  std::vector<cdr_vh_item> vh;
+  std::vector<cdr_activity_info> act;
+  std::vector<cdr_timer_info> timer;
+  std::vector<cdr_child_info> child;
+  std::vector<cdr_cancel_info> cancel;
+  std::vector<cdr_signal_info> signal;
+  std::vector<cdr_reset_point> rp;
+  std::vector<cdr_kv> sa;
+  std::vector<cdr_last_decision> ld;
+  cdr_out view{};
+};
+
+struct cdr_ctx {
+  int device;
+  int fast = 1;                        // cdr_set_fast_path
+  int reg = 1;                         // cdr_set_reg_path
+  uint32_t plan_mode = CDR_PLAN_WAVE;  // cdr_set_plan_mode
+  hipEvent_t ev[4];
+  bool timed;
+  // optional per-launch timing ring (bench): event pairs around every replay kernel
+  std::vector<hipEvent_t> ring;
+  uint32_t ring_used = 0;
+  // side stream for the wave kernel: its scalar-unit-bound waves co-run with the
+  // VALU-bound lane kernels instead of after them (fork/join by events)
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  int concurrent = 1;
+  // grow-only device workspace of the host-buffer calls
+  void* ws[WS_NUM] = {};
+  uint64_t ws_bytes[WS_NUM] = {};
+  cdr_one_host one;
+};
+
+// device buffer `slot` of at least `bytes` (grow-only; contents undefined); nullptr
+// when the device is out of memory (defined in replay.hip)
+void* cdr_ws_get(cdr_ctx* c, int slot, uint64_t bytes);

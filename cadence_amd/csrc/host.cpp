@@ -852,6 +852,8 @@ uint64_t cdr_struct_size(const char* name) {
       {"cdr_dev_batch", sizeof(cdr_dev_batch)},
       {"cdr_carry", sizeof(cdr_carry)},
       {"cdr_task", sizeof(cdr_task)},
+      {"cdr_last_decision", sizeof(cdr_last_decision)},
+      {"cdr_opts", sizeof(cdr_opts)},
       {"cdr_vh_token", sizeof(cdr_vh_token)},
       {"cdr_vh_branch", sizeof(cdr_vh_branch)},
       {"cdr_vhs", sizeof(cdr_vhs)},

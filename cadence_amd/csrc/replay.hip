@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "cdr/cdr.h"
+#include "ctx.h"
 
 #ifndef CDR_DEPTH
 #define CDR_DEPTH 1 /* events whose operand loads are in flight beyond the one processed */
@@ -168,6 +169,36 @@ __device__ __forceinline__ T gget(const GAS T* p) {
 #pragma unroll
   for (uint32_t i = 0; i < sizeof(T) / 8; i++) d[i] = s[i];
   return v;
+}
+
+// ---- lastDecision of the entry's last applyEvents call (stateBuilder.go:126,200,213,
+// 238,256,610).  Per lane, ld = CDR_LD_* source | LD_CAPTURED | event index << 3.  A
+// source event's decisionInfo equals the ExecutionInfo decision fields right after it
+// (UpdateDecision, mutableStateDecisionTaskManager.go:677-702) and those change again
+// only at a DecisionTaskCompleted / Failed / TimedOut or the next source event, so the
+// record is written just before such a clearing event (rare: both in one call) or once
+// after the loop; the call's first event resets it (lastDecision is a local of each call).
+#define LD_CAPTURED 4u
+__device__ __forceinline__ bool ld_pending(uint32_t ld) { return (ld & 3u) != 0u && !(ld & LD_CAPTURED); }
+__device__ __forceinline__ uint32_t ld_make(uint32_t src, uint32_t k) { return src | (k << 3); }
+__device__ __forceinline__ void ld_write(GAS cdr_last_decision* o, uint32_t ld, int64_t dv, int64_t dsched,
+                                         int64_t dstart, uint32_t dreq, int32_t dto, int64_t datt, int64_t dsc_ts,
+                                         int64_t dst_ts, int64_t dorig_ts) {
+  cdr_last_decision r;
+  const bool any = (ld & 3u) != 0u;
+  r.source = ld & 3u;
+  r.request_id = any ? dreq : 0u;
+  r.event_index = any ? (int64_t)(ld >> 3) : 0;
+  r.version = any ? dv : 0;
+  r.schedule_id = any ? dsched : 0;
+  r.started_id = any ? dstart : 0;
+  r.attempt = any ? datt : 0;
+  r.scheduled_ts = any ? dsc_ts : 0;
+  r.started_ts = any ? dst_ts : 0;
+  r.original_scheduled_ts = any ? dorig_ts : 0;
+  r.decision_timeout = any ? dto : 0;
+  r._pad = 0;
+  gput(o, r);
 }
 
 // Opaque copy of a wave-uniform base pointer: loads through it cannot be hoisted out
@@ -559,6 +590,8 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   int64_t dv = CDR_EMPTY_VERSION, dsched = CDR_EMPTY_EVENT_ID, dstart = CDR_EMPTY_EVENT_ID, datt = 0, dst_ts = 0,
           dsc_ts = 0, dorig_ts = 0;
   uint32_t dreq = EU;
+  uint32_t ld = 0;  // lastDecision bookkeeping (ld_write)
+  const bool want_ld = O_.last_decision != nullptr;
   int32_t dto = 0;
   // versions
   int64_t curv = D.failover_version;  // NDC currentVersion
@@ -770,6 +803,14 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     err_k = SEL(f_, k, err_k);          \
     stop_at_call_end |= f_;             \
   } while (0)
+  // lastDecision: the record of a pending source event, before a clearing event
+#define GLD_CAPTURE(mine_)                                                                                 \
+  do {                                                                                                     \
+    const bool c_ = (mine_) && ld_pending(ld);                                                             \
+    if (c_ && want_ld)                                                                                     \
+      ld_write(gp(O_.last_decision) + w, ld, dv, dsched, dstart, dreq, dto, datt, dsc_ts, dst_ts, dorig_ts); \
+    ld |= c_ ? LD_CAPTURED : 0u;                                                                           \
+  } while (0)
   const uint32_t srows = S.elems / CDR_SLICE_WIDTH;
   for (uint32_t k = 0; k < srows; k++) {
     if (__builtin_amdgcn_ballot_w64(!done) == 0) break;  // every lane finished
@@ -811,6 +852,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     const bool start_call = bf && !done;
     call_first_id = SEL(start_call, e.id, call_first_id);
     call_first_k = SEL(start_call, k, call_first_k);
+    ld = SEL(start_call, 0u, ld);
     prev_id = SEL(done, prev_id, e.id);
     prev_ver = SEL(done, prev_ver, e.ver);
     bool go = !done && !stop_at_call_end;  // rest of a failed call: only its last event matters (2DC)
@@ -868,6 +910,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
         dsc_ts = SEL(ms, e.ts, dsc_ts);
         dst_ts = SEL(ms, (int64_t)0, dst_ts);
         dorig_ts = SEL(ms, e.ts, dorig_ts);
+        ld = SEL(ms, ld_make(CDR_LD_SCHEDULED, k), ld);
         task_x(TK && ms, CDR_TT_DECISION, e.id, D.domain_id, task_list_now(), 0, 0, 0);  // :196-197
         const bool mt = mine && type == CDR_EV_DT_STARTED;  // :202-213 -> :200-253
         const bool f = mt && e.key != dsched;
@@ -879,6 +922,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
         dreq = SEL(ok, e.h, dreq);
         datt = SEL(ok, (int64_t)0, datt);
         dst_ts = SEL(ok, e.ts, dst_ts);
+        ld = SEL(ok, ld_make(CDR_LD_STARTED, k), ld);
         task_t(TK && ok, CDR_TT_DECISION_TIMEOUT, CDR_TIMEOUT_START_TO_CLOSE, e.key, e.ts + (int64_t)dto * NS_PER_S, 0);
         x_signals += (mine && type == CDR_EV_WF_SIGNALED) ? 1 : 0;                           // :473-476
         x_flags |= (mine && type == CDR_EV_WF_CANCEL_REQUESTED) ? CDR_XI_CANCEL_REQUESTED : 0u;  // :478-481
@@ -886,6 +930,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
       }
       switch (ut) {
         case CDR_EV_WF_STARTED: {  // stateBuilder.go:158-184 -> mutableStateBuilder.go:1639-1716
+          GLD_CAPTURE(mine);  // a later Started resets the decision fields
           // every lane reads a valid record (the first one for lanes of other types)
           const GAS cdr_attr_wf_started* a =
               gp((const cdr_attr_wf_started*)(B_.ev.arena + (uint64_t)(mine ? e.aux : 0)));
@@ -1010,6 +1055,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           dsc_ts = SEL(mine, e.ts, dsc_ts);
           dst_ts = SEL(mine, (int64_t)0, dst_ts);
           dorig_ts = SEL(mine, e.ts, dorig_ts);
+          ld = SEL(mine, ld_make(CDR_LD_SCHEDULED, k), ld);
           task_x(TK && mine, CDR_TT_DECISION, e.id, D.domain_id, task_list_now(), 0, 0, 0);  // :196-197
           break;
         case CDR_EV_DT_STARTED: {  // :202-213 -> :200-253
@@ -1022,11 +1068,13 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           dreq = SEL(ok, e.h, dreq);
           datt = SEL(ok, (int64_t)0, datt);
           dst_ts = SEL(ok, e.ts, dst_ts);
+          ld = SEL(ok, ld_make(CDR_LD_STARTED, k), ld);
           // scheduleDecisionTimerTask (:210-211; timerBuilder.go:322-331)
           task_t(TK && ok, CDR_TT_DECISION_TIMEOUT, CDR_TIMEOUT_START_TO_CLOSE, e.key, e.ts + (int64_t)dto * NS_PER_S, 0);
           break;
         }
         case CDR_EV_DT_COMPLETED: {  // :215-219 -> :255-262,659-674,789-800
+          GLD_CAPTURE(mine);
           dv = SEL(mine, CDR_EMPTY_VERSION, dv);
           dsched = SEL(mine, CDR_EMPTY_EVENT_ID, dsched);
           dstart = SEL(mine, CDR_EMPTY_EVENT_ID, dstart);
@@ -1069,6 +1117,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
         }
         case CDR_EV_DT_TIMED_OUT:  // :221-239 -> FailDecision :635-656 + transient :169-198
         case CDR_EV_DT_FAILED: {   // :241-257
+          GLD_CAPTURE(mine);
           const bool inc = ut == CDR_EV_DT_FAILED || e.n != CDR_TIMEOUT_SCHEDULE_TO_START;
           const int64_t now = B_.now_ns;
           const int64_t na = inc ? datt + 1 : 0;
@@ -1082,6 +1131,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           dorig_ts = SEL(mine, (int64_t)0, dorig_ts);
           dsc_ts = SEL(mine, (tr || inc) ? now : (int64_t)0, dsc_ts);
           datt = SEL(mine, na, datt);
+          ld = SEL(mine && tr, ld_make(CDR_LD_TRANSIENT, k), ld);
           task_x(TK && mine && tr, CDR_TT_DECISION, x_next_event, D.domain_id, task_list_now(), 0, 0, 0);  // :235,253
           break;
         }
@@ -1436,6 +1486,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   }
 #undef PFAIL
 #undef SEL
+#undef GLD_CAPTURE
   // ---- end of the last call
   if (len > 0 && (err == CDR_OK || stop_at_call_end)) {
     if (isRS) {
@@ -1562,6 +1613,8 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   }
   gput(gp(O_.result) + w, r);
   if (err != CDR_OK) return;
+  if (want_ld && !(ld & LD_CAPTURED))
+    ld_write(gp(O_.last_decision) + w, ld, dv, dsched, dstart, dreq, dto, datt, dsc_ts, dst_ts, dorig_ts);
   if (n_vh) gput(vh + (n_vh - 1), cdr_vh_item{vh_last_id, vh_last_ver});
   if (!(x_flags & CDR_XI_STARTED) && csrc < 0) {  // no WorkflowExecutionStarted: its fields keep their zero values
     X->domain_id = X->workflow_id = X->run_id = X->create_request_id = 0;
@@ -1686,22 +1739,8 @@ __global__ void k_finalize(cdr_dev_batch B, cdr_out O) {
 }
 
 // ============================================================ host API
-struct cdr_ctx {
-  int device;
-  int fast = 1;  // cdr_set_fast_path
-  int reg = 1;   // cdr_set_reg_path
-  uint32_t plan_mode = CDR_PLAN_WAVE;  // cdr_set_plan_mode
-  hipEvent_t ev[4];
-  bool timed;
-  // optional per-launch timing ring (bench): event pairs around every replay kernel
-  std::vector<hipEvent_t> ring;
-  uint32_t ring_used = 0;
-  // side stream for the wave kernel: its scalar-unit-bound waves co-run with the
-  // VALU-bound lane kernels instead of after them (fork/join by events)
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  int concurrent = 1;
-};
+// struct cdr_ctx: ctx.h
+
 
 #define HIPCHK(x)                                                                      \
   do {                                                                                 \
@@ -1712,14 +1751,48 @@ struct cdr_ctx {
     }                                                                                  \
   } while (0)
 
+void* cdr_ws_get(cdr_ctx* c, int slot, uint64_t bytes) {
+  if (!c || slot < 0 || slot >= WS_NUM) return nullptr;
+  if (bytes == 0) bytes = 8;
+  if (c->ws[slot] && c->ws_bytes[slot] >= bytes) return c->ws[slot];
+  if (c->ws[slot]) (void)hipFree(c->ws[slot]);
+  c->ws[slot] = nullptr;
+  c->ws_bytes[slot] = 0;
+  const uint64_t want = bytes + bytes / 8;  // headroom: a slowly growing caller reallocates rarely
+  void* p = nullptr;
+  if (hipMalloc(&p, want) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  c->ws[slot] = p;
+  c->ws_bytes[slot] = want;
+  return p;
+}
+
 extern "C" {
 
-cdr_ctx* cdr_create(int device) {
+void cdr_opts_default(cdr_opts* o) {
+  if (!o) return;
+  *o = cdr_opts{};
+  o->plan_mode = CDR_PLAN_WAVE;
+  o->fast_path = 1;
+  o->reg_path = 1;
+  o->concurrent = 1;
+}
+
+cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
+  cdr_opts o;
+  cdr_opts_default(&o);
+  if (opts) o = *opts;
+  if (o.plan_mode & ~(uint32_t)(CDR_PLAN_WAVE | CDR_PLAN_WAVE_ALL)) return nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return nullptr;
   if (hipSetDevice(device) != hipSuccess) return nullptr;
   cdr_ctx* c = new cdr_ctx();
   c->device = device;
+  c->fast = o.fast_path ? 1 : 0;
+  c->reg = o.reg_path ? 1 : 0;
+  c->plan_mode = o.plan_mode;
   for (int i = 0; i < 4; i++)
     if (hipEventCreate(&c->ev[i]) != hipSuccess) {
       delete c;
@@ -1731,6 +1804,11 @@ cdr_ctx* cdr_create(int device) {
       hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess)
     c->concurrent = 0;
   if (const char* e = std::getenv("CDR_SERIAL_KERNELS")) c->concurrent = c->concurrent && e[0] == '0';
+  c->concurrent = c->concurrent && o.concurrent;
+  if (o.workspace_bytes && !cdr_ws_get(c, WS_SLAB, o.workspace_bytes)) {
+    cdr_destroy(c);
+    return nullptr;
+  }
   return c;
 }
 
@@ -1749,7 +1827,7 @@ int cdr_set_reg_path(cdr_ctx* c, int enable) {
 }
 
 int cdr_set_plan_mode(cdr_ctx* c, uint32_t mode) {
-  if (!c || (mode & ~CDR_PLAN_WAVE)) return CDR_API_EINVAL;
+  if (!c || (mode & ~(uint32_t)(CDR_PLAN_WAVE | CDR_PLAN_WAVE_ALL))) return CDR_API_EINVAL;
   const uint32_t old = c->plan_mode;
   c->plan_mode = mode;
   return (int)old;
@@ -1764,6 +1842,8 @@ void cdr_destroy(cdr_ctx* c) {
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->fork) (void)hipEventDestroy(c->fork);
   if (c->join) (void)hipEventDestroy(c->join);
+  if (hipSetDevice(c->device) == hipSuccess)
+    for (void* p : c->ws) (void)hipFree(p);
   delete c;
 }
 

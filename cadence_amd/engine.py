@@ -260,6 +260,7 @@ class Outputs:
         self.exec = (abi.CdrExecInfo * n)()
         self.repl = (abi.CdrReplState * n)()
         self.tables = {t: (TABLE_TYPES[t] * max(1, getattr(pl.totals, t)))() for t in TABLES}
+        self.last_decision = (abi.CdrLastDecision * n)()  # applyEvents' lastDecision per entry
         self.tasks = None
         if tasks:  # stateBuilder transfer / timer task lists (cdr_task)
             self.alloc_tasks(pl)
@@ -277,6 +278,7 @@ class Outputs:
         o.repl = C.addressof(self.repl)
         for t in TABLES:
             setattr(o, t, C.addressof(self.tables[t]))
+        o.last_decision = C.addressof(self.last_decision)
         if self.tasks is not None:
             o.transfer = C.addressof(self.tasks["xfer"])
             o.timer_tasks = C.addressof(self.tasks["ttask"])
@@ -322,11 +324,13 @@ class Engine:
 
     def __init__(self, device: int = 0, fast_path: bool = True, wave: bool = True):
         L = abi.lib()
-        self.ctx = L.cdr_create(device)
+        opts = abi.CdrOpts()
+        L.cdr_opts_default(C.byref(opts))
+        opts.fast_path = 1 if fast_path else 0
+        opts.plan_mode = abi.PLAN_WAVE if wave else 0
+        self.ctx = L.cdr_create(device, C.byref(opts))
         if not self.ctx:
             raise RuntimeError("cdr_create failed: no usable HIP device (the engine has no CPU fallback)")
-        L.cdr_set_fast_path(self.ctx, 1 if fast_path else 0)
-        L.cdr_set_plan_mode(self.ctx, abi.PLAN_WAVE if wave else 0)
 
     def set_wave(self, enable: bool) -> bool:
         """Plan divergent histories into wave slices (one wavefront per workflow,
@@ -360,9 +364,33 @@ class Engine:
         pl = pl or plan(batch)
         out = Outputs(batch, pl, tasks)
         rc = abi.lib().cdr_replay_batch(self.ctx, C.byref(batch.cstruct()), pl.caps, C.byref(pl.totals),
-                                       C.byref(out.cstruct()))
+                                       C.byref(out.cstruct()), None)
         if rc:
             raise RuntimeError(f"cdr_replay_batch rc={rc}")
+        return out
+
+    def replay_one(self, batch: Batch) -> Outputs:
+        """One workflow through cdr_replay_one (the applyEvents shim's call): `batch`
+        holds its entry and, if it continues as new, the new run's (n_wfs 1 or 2).  The
+        context's view is copied into an Outputs."""
+        L = abi.lib()
+        view, caps = C.c_void_p(), C.c_void_p()
+        rc = L.cdr_replay_one(self.ctx, C.byref(batch.cstruct()), C.byref(view), C.byref(caps), None)
+        if rc:
+            raise RuntimeError(f"cdr_replay_one rc={rc}")
+        v = abi.CdrOut.from_address(view.value)
+        n = batch.n_wfs
+        cp = (abi.CdrWfCaps * n).from_address(caps.value)
+        pl = Plan((abi.CdrWfCaps * n)(), abi.CdrTotals())
+        C.memmove(pl.caps, cp, C.sizeof(pl.caps))
+        for t in TABLES:  # totals: the end of the last entry's slice of each table
+            setattr(pl.totals, t, max(getattr(c, t + "_off") + getattr(c, t + "_cap") for c in pl.caps))
+        out = Outputs(batch, pl)
+        for name, dst in (("result", out.result), ("exec", out.exec), ("repl", out.repl),
+                          ("last_decision", out.last_decision)):
+            C.memmove(dst, getattr(v, name), C.sizeof(dst))
+        for t in TABLES:
+            C.memmove(out.tables[t], getattr(v, t), C.sizeof(TABLE_TYPES[t]) * getattr(pl.totals, t))
         return out
 
     def encode_rows(self, batch: Batch, out: Outputs, table: str) -> bytes:
@@ -430,7 +458,7 @@ class Engine:
         flags = (abi.REFRESH_ADVANCED_VISIBILITY if advanced_visibility else 0) | (
         abi.REFRESH_SNAPSHOT_PASSIVE if snapshot else 0)
         rc = abi.lib().cdr_rebuild_batch(self.ctx, C.byref(batch.cstruct()), pl.caps, C.byref(pl.totals),
-                                        C.byref(out.cstruct()), flags)
+                                        C.byref(out.cstruct()), flags, None)
         if rc:
             raise RuntimeError(f"cdr_rebuild_batch rc={rc}")
         return out
@@ -458,6 +486,10 @@ def compare(batch: Batch, a: Outputs, b: Outputs, limit: int = 10):
                 bad.append(f"wf {w}: exec differs in {diffs}")
             if batch.wfs[w].builder == abi.BUILDER_2DC and _bytes(a.repl[w]) != _bytes(b.repl[w]):
                 bad.append(f"wf {w}: replication state differs")
+            la, lb = a.last_decision[w], b.last_decision[w]
+            if _bytes(la) != _bytes(lb):
+                bad.append(f"wf {w}: lastDecision differs in "
+                           f"{[f for f, _ in abi.CdrLastDecision._fields_ if getattr(la, f) != getattr(lb, f)]}")
             for t in TABLES:
                 na, nb = getattr(ra, TABLE_COUNT[t]), getattr(rb, TABLE_COUNT[t])
                 if na != nb:

@@ -272,7 +272,19 @@ int cdr_pack_slices(const cdr_batch* b, cdr_slices* out, int threads);
 /* ------------------------------------------------------------- device entry */
 
 typedef struct cdr_ctx cdr_ctx;
-cdr_ctx* cdr_create(int device);
+/* Context options (cdr_opts_default fills the defaults). */
+typedef struct cdr_opts {
+  uint32_t plan_mode;       /* CDR_PLAN_* of the host-buffer calls' planning (CDR_PLAN_WAVE) */
+  int32_t fast_path;        /* CDR_SLICE_FAST / REG / REG2 slices on their kernels (1) */
+  int32_t reg_path;         /* CDR_SLICE_REG / REG2 slices on k_replay_reg (1) */
+  int32_t concurrent;       /* wave-kernel slices on a side stream, concurrent with the lane kernels (1) */
+  uint64_t workspace_bytes; /* device bytes reserved at creation for the host-buffer calls' event slab
+                             * (0: on demand; the workspace only grows) */
+} cdr_opts;
+void cdr_opts_default(cdr_opts* opts);
+/* A context on HIP device `device` (opts NULL: defaults); NULL when the device is absent
+ * or its kernel image cannot load — there is no CPU fallback. */
+cdr_ctx* cdr_create(int device, const cdr_opts* opts);
 void cdr_destroy(cdr_ctx* ctx);
 
 /* Route CDR_SLICE_FAST slices to the fast-path kernel and CDR_SLICE_REG slices to the
@@ -292,11 +304,22 @@ int cdr_set_plan_mode(cdr_ctx* ctx, uint32_t mode);
  * kernel and the continue-as-new finalize kernel and returns. */
 int cdr_replay_sliced_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, void* stream);
 
-/* Whole pipeline for host-resident data: plan + pack + H2D + replay + D2H.
- * `caps` must come from cdr_plan_caps on the same batch; `out` points at host
- * buffers sized by its totals.  Synchronous. */
+/* Whole pipeline for host-resident data: plan + pack + H2D + replay + D2H on `stream`
+ * (a hipStream_t; NULL = the default stream).  `caps` must come from cdr_plan_caps on the
+ * same batch; `out` points at host buffers sized by its totals (out->last_decision, if
+ * set, at n_wfs records).  Device buffers come from the context's grow-only workspace:
+ * a warmed-up context allocates nothing.  Synchronous on `stream`; one call at a time
+ * per context. */
 int cdr_replay_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* totals,
-                     cdr_out* out);
+                     cdr_out* out, void* stream);
+
+/* The drop-in applyEvents shim's call: the sequence of applyEvents calls
+ * of ONE workflow — `b` holds its entry (0) and, when its history continues as new, the
+ * new run's entry (b->n_wfs 1 or 2).  The context plans the capacities itself and
+ * replays into its own host buffers: *view receives the outputs (tables at the
+ * offsets in *caps, last_decision set), valid until the next call on `ctx`.  Synchronous
+ * on `stream`. */
+int cdr_replay_one(cdr_ctx* ctx, const cdr_batch* b, const cdr_out** view, const cdr_wf_caps** caps, void* stream);
 
 /* refreshTasks (mutableStateTaskRefresher.go:66-160) over the rebuilt states of a
  * replay: run after cdr_replay_sliced_async on the same `in` / `out` (same stream).
@@ -325,9 +348,9 @@ int cdr_refresh_tasks_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out
 
 /* nDCStateRebuilder.rebuild's replay + refreshTasks for host-resident data: as
  * cdr_replay_batch, then cdr_refresh_tasks_async at b->now_ns.  out->transfer,
- * timer_tasks and n_tasks are required (sized by `totals`).  Synchronous. */
+ * timer_tasks and n_tasks are required (sized by `totals`).  Synchronous on `stream`. */
 int cdr_rebuild_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps, const cdr_totals* totals,
-                      cdr_out* out, uint32_t flags);
+                      cdr_out* out, uint32_t flags, void* stream);
 
 /* Persisted-format row encoders: the SQL persistence's per-row blobs,
  * thriftrw binary protocol (common/persistence/sql/blob.go:61-73, protocol.Binary) of

@@ -531,6 +531,27 @@ typedef struct cdr_task {
 static_assert(sizeof(cdr_task) == 64, "cdr_task");
 #endif
 
+/* applyEvents' second return value, lastDecision *decisionInfo (stateBuilder.go:126,
+ * 200,213,238,256,610), for the entry's last call: the decision the call's last
+ * DecisionTaskScheduled, DecisionTaskStarted or transient decision (after a
+ * DecisionTaskFailed / TimedOut) produced, or none (nil).  Its fields are the decision
+ * manager's decisionInfo (mutableStateDecisionTaskManager.go:143-253).  TaskList is not
+ * stored: for CDR_LD_SCHEDULED it is the DecisionTaskScheduled event's TaskList (event
+ * event_index of the entry), otherwise ExecutionInfo.TaskList (applyEvents clears
+ * stickiness, :116).  Written for CDR_OK entries when cdr_out.last_decision is set. */
+enum cdr_ld_source { CDR_LD_NONE = 0, CDR_LD_SCHEDULED = 1, CDR_LD_STARTED = 2, CDR_LD_TRANSIENT = 3 };
+typedef struct cdr_last_decision {
+  uint32_t source;     /* cdr_ld_source */
+  uint32_t request_id; /* handle (EmptyUUID until started) */
+  int64_t event_index; /* index of the producing event within the entry's events */
+  int64_t version, schedule_id, started_id, attempt;
+  int64_t scheduled_ts, started_ts, original_scheduled_ts;
+  int32_t decision_timeout, _pad;
+} cdr_last_decision;
+#ifdef __cplusplus
+static_assert(sizeof(cdr_last_decision) == 80, "cdr_last_decision");
+#endif
+
 /* per-workflow result: status + where each variable-length table lives */
 typedef struct cdr_wf_result {
   int32_t code;   /* cdr_status */
@@ -610,6 +631,7 @@ typedef struct cdr_out {
   cdr_task* transfer;      /* [totals.xfer] */
   cdr_task* timer_tasks;   /* [totals.ttask] */
   uint32_t* n_tasks;       /* [2 * n_wfs]: transfer, timer count of entry w */
+  cdr_last_decision* last_decision; /* [n_wfs] nullable: applyEvents' lastDecision */
 } cdr_out;
 
 /* Carry-in: replay onto a LOADED mutable state, the analogue of

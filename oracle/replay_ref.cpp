@@ -250,6 +250,8 @@ struct MutableState {
   uint64_t wf_key;
   int32_t retention_days;
   ExecutionInfo ei;
+  // applyEvents' lastDecision of the latest call (stateBuilder.go:126,200,213,238,256,610)
+  cdr_last_decision lastDecision{};
   bool hasRS = false;
   ReplicationState rs{};
   bool hasVH = false;
@@ -361,6 +363,23 @@ struct MutableState {
     ei.DecisionOriginalScheduledTimestamp = d.OriginalScheduledTimestamp;
   }
   bool HasPendingDecision() const { return ei.DecisionScheduleID != CDR_EMPTY_EVENT_ID; }
+  // the *decisionInfo a decision event returned: the decision fields it just set
+  // (TaskList is the event's or ExecutionInfo.TaskList: not recorded, schema.h)
+  cdr_last_decision snapDecision(uint32_t source, int64_t index) const {
+    cdr_last_decision d{};
+    d.source = source;
+    d.request_id = ei.DecisionRequestID;
+    d.event_index = index;
+    d.version = ei.DecisionVersion;
+    d.schedule_id = ei.DecisionScheduleID;
+    d.started_id = ei.DecisionStartedID;
+    d.attempt = ei.DecisionAttempt;
+    d.scheduled_ts = ei.DecisionScheduledTimestamp;
+    d.started_ts = ei.DecisionStartedTimestamp;
+    d.original_scheduled_ts = ei.DecisionOriginalScheduledTimestamp;
+    d.decision_timeout = ei.DecisionTimeout;
+    return d;
+  }
   // FailDecision (:635-656)
   void FailDecision(bool incrementAttempt) {
     ClearStickyness();
@@ -488,6 +507,7 @@ struct StateBuilder {
     const cdr_event& first = history[0];
     const cdr_event& last = history[n - 1];
     ms->ClearStickyness();
+    ms->lastDecision = cdr_last_decision{};  // var lastDecision *decisionInfo (:126)
     auto fail = [&](int32_t code, size_t i) {
       GoErr e;
       e.code = code;
@@ -627,6 +647,7 @@ struct StateBuilder {
                                        ev.timestamp, ev.timestamp};
           ms->UpdateDecision(d);
           ms->AddXfer(CDR_TT_DECISION, ev.event_id, domainID, ei.TaskList);  // :196-197
+          ms->lastDecision = ms->snapDecision(CDR_LD_SCHEDULED, index_base + (int64_t)i);  // :200
           break;
         }
         case CDR_EV_DT_STARTED: {  // :202-213 -> :200-253
@@ -645,6 +666,7 @@ struct StateBuilder {
           // scheduleDecisionTimerTask (:210-211, timerBuilder.go:322-331)
           ms->AddTimer(CDR_TT_DECISION_TIMEOUT, CDR_TIMEOUT_START_TO_CLOSE, scheduleID,
                        ev.timestamp + (int64_t)nd.DecisionTimeout * 1000000000LL, nd.Attempt);
+          ms->lastDecision = ms->snapDecision(CDR_LD_STARTED, index_base + (int64_t)i);  // :213
           break;
         }
         case CDR_EV_DT_COMPLETED: {  // :215-219 -> :255-262, :789-800
@@ -676,13 +698,17 @@ struct StateBuilder {
         }
         case CDR_EV_DT_TIMED_OUT:  // :221-239
           ms->FailDecision(ev.a.dt.timeout_type != CDR_TIMEOUT_SCHEDULE_TO_START);
-          if (ms->ReplicateTransientDecisionTaskScheduled())
+          if (ms->ReplicateTransientDecisionTaskScheduled()) {
             ms->AddXfer(CDR_TT_DECISION, ei.DecisionScheduleID, domainID, ei.TaskList);  // :235-236
+            ms->lastDecision = ms->snapDecision(CDR_LD_TRANSIENT, index_base + (int64_t)i);  // :238
+          }
           break;
         case CDR_EV_DT_FAILED:  // :241-257
           ms->FailDecision(true);
-          if (ms->ReplicateTransientDecisionTaskScheduled())
+          if (ms->ReplicateTransientDecisionTaskScheduled()) {
             ms->AddXfer(CDR_TT_DECISION, ei.DecisionScheduleID, domainID, ei.TaskList);  // :253-254
+            ms->lastDecision = ms->snapDecision(CDR_LD_TRANSIENT, index_base + (int64_t)i);  // :256
+          }
           break;
         case CDR_EV_AT_SCHEDULED: {  // :259-269 -> mutableStateBuilder.go:1982-2028
           const cdr_attr_at_scheduled& a = ev.a.at_sched;
@@ -953,6 +979,7 @@ static void sorted_values(const std::map<K, T>& m, std::vector<T>& out) {
 
 bool write_state(const MutableState& ms, const cdr_batch* b, uint32_t w, const cdr_wf_caps* caps, cdr_out* out) {
   (void)b;
+  if (out->last_decision) out->last_decision[w] = ms.lastDecision;
   const ExecutionInfo& ei = ms.ei;
   const cdr_wf_caps& cp = caps[w];
   cdr_wf_result& r = out->result[w];

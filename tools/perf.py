@@ -35,7 +35,7 @@ def main():
                            plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0))
     stream = torch.cuda.current_stream().cuda_stream
     libs = [(p, abi.load(p)) for p in args.libs]
-    ctxs = [L.cdr_create(0) for _, L in libs]
+    ctxs = [L.cdr_create(0, None) for _, L in libs]
     if args.no_reg:
         for (_, L), c in zip(libs, ctxs):
             L.cdr_set_reg_path(c, 0)

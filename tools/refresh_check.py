@@ -23,7 +23,7 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 20000
     torch.cuda.set_device(0)
     L = abi.lib()
-    ctx = L.cdr_create(0)
+    ctx = L.cdr_create(0, None)
     idx = np.arange(n, dtype=np.uint32)
     db = bench.DeviceBatch(torch, cfg, idx, 0x5EED0002)
     stream = torch.cuda.current_stream().cuda_stream
