@@ -236,6 +236,19 @@ def cpu_baseline(config, n_wfs, seed, min_seconds=10.0):
             "single_thread_events_per_s": res[1], "workflows_per_s": res[threads] / (n_ev / max(1, n_wfs))}
 
 
+def reduce_step(dist, torch, stats, elapsed: float):
+    """The multi-GPU step's only collective: the sum over ranks of the
+    int64 counters [events, entries, OK entries, cdr_checksum_async digest sum] (the
+    digest sum wraps mod 2^64, so the all-reduced value is the single-process sum) and
+    the max over ranks of the timed region.  `stats` is a 4-element int64 tensor on the
+    collective's device (cuda for RCCL, cpu for the gloo tests)."""
+    t_el = torch.tensor([elapsed], dtype=torch.float64, device=stats.device)
+    if dist:
+        dist.all_reduce(stats)
+        dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
+    return [int(x) for x in stats.tolist()], float(t_el.item())
+
+
 def lib_sha1() -> str:
     import hashlib
     return hashlib.sha1(open(abi.LIB_PATH, "rb").read()).hexdigest()
@@ -347,13 +360,7 @@ def main():
     L.cdr_checksum_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(csum.data_ptr()), C.c_void_p(stream))
     stats = torch.tensor([db.n_events, db.info.n_entries, n_ok, 0], dtype=torch.int64, device="cuda")
     stats[3] = csum[0]
-    t_el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if dist:
-        dist.all_reduce(stats)
-        dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
-    torch.cuda.synchronize()
-    elapsed = float(t_el.item())
-    tot_events, tot_wfs, tot_ok, checksum = [int(x) for x in stats.tolist()]
+    (tot_events, tot_wfs, tot_ok, checksum), elapsed = reduce_step(dist, torch, stats, elapsed)
     if tot_ok != tot_wfs:
         log(f"WARNING: {tot_wfs - tot_ok} workflows did not replay OK")
 

@@ -2,12 +2,12 @@
 
 The replay shards with no data-path collective: historyShardID = Fingerprint32(wid) %
 16384 (common/util.go:249-252), shards -> ranks greedily, each rank replays only its
-workflows, and one all-reduce (sum) of {events, workflows, ok, checksum} closes the
-step.  Here each rank replays its share with the CPU restatement (oracle/, the parity
-checker — no GPU in this container) and the all-reduced totals must equal a
-single-process replay of the whole population, workflow for workflow."""
-import hashlib
-import json
+workflows, and one all-reduce (sum) of {events, entries, ok, checksum} closes the step
+(bench.reduce_step, the function bench.main calls).  Here each rank replays its share
+with the CPU restatement (oracle/, the parity checker — no GPU in this container) and
+hashes it with the restatement of the product checksum (cdr_checksum_async's per-entry
+k_digest hash, oracle/digest_ref.cpp); the all-reduced totals must equal a
+single-process replay of the whole population."""
 import os
 import socket
 
@@ -22,15 +22,12 @@ TOTAL = 600
 SEED = 0x5EED0003
 
 
-def _wf_digest(batch, out, w) -> int:
-    s = json.dumps(engine.export_state(batch, out, w), sort_keys=True).encode()
-    return int.from_bytes(hashlib.sha256(s).digest()[:8], "little")
-
-
 def _stats(batch, out):
+    """[events, entries, OK entries, checksum] as bench.main builds them: the checksum is
+    cdr_checksum_async's (the sum of per-entry k_digest hashes), restated."""
     n_ev = len(batch.events)
     ok = sum(1 for w in range(batch.n_wfs) if out.result[w].code == abi.OK)
-    cs = sum(_wf_digest(batch, out, w) for w in range(batch.n_wfs)) & (2 ** 64 - 1)
+    _, cs = oracle.entry_digests(batch, out.plan, out)
     return [n_ev, batch.n_wfs, ok, cs - 2 ** 64 if cs >= 2 ** 63 else cs]
 
 
@@ -45,14 +42,14 @@ def _rank(rank, world, port, cfg, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        mine, _ = bench.assign_shards(TOTAL, world, rank)
+        mine, _ = bench.assign_shards(TOTAL, world, rank, bench.workflow_weights(cfg, TOTAL, SEED))
         b, out = _share(mine, cfg)
-        stats = torch.tensor(_stats(b, out), dtype=torch.int64)
-        dist.all_reduce(stats)
+        stats, elapsed = bench.reduce_step(dist, torch, torch.tensor(_stats(b, out), dtype=torch.int64),
+                                           1.0 + rank)
         owned = [None] * world
         dist.all_gather_object(owned, mine.tolist())
         if rank == 0:
-            q.put((stats.tolist(), owned))
+            q.put((stats, elapsed, owned))
     finally:
         dist.destroy_process_group()
 
@@ -72,7 +69,7 @@ def test_two_rank_shards_match_single_process(cfg):
     procs = [ctx.Process(target=_rank, args=(r, 2, port, cfg, q)) for r in range(2)]
     for p in procs:
         p.start()
-    stats, owned = q.get(timeout=240)
+    stats, elapsed, owned = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -80,9 +77,11 @@ def test_two_rank_shards_match_single_process(cfg):
     allw = np.sort(np.concatenate([np.array(o, np.int64) for o in owned]))
     assert np.array_equal(allw, np.arange(TOTAL))
     assert all(len(o) > 0 for o in owned)
-    # the all-reduced totals equal one process replaying everything
+    # the all-reduced totals equal one process replaying everything; the timed region is
+    # the slowest rank's
     b, out = _share(np.arange(TOTAL, dtype=np.uint32), cfg)
     assert stats == _stats(b, out)
+    assert elapsed == 2.0
 
 
 def test_shard_assignment_balances_events():
