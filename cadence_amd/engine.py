@@ -315,6 +315,9 @@ def _hip():
         L.hipFree.argtypes = [C.c_void_p]
         L.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
         L.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+        L.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+        L.hipStreamDestroy.argtypes = [C.c_void_p]
+        L.hipMemGetInfo.argtypes = [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
         _hip_lib = L
     return _hip_lib
 

@@ -645,7 +645,12 @@ typedef struct cdr_out {
  * pendingActivityInfoByActivityID rebuilt from the activity rows (ascending
  * scheduleID, the last duplicate activityID wins).  The caller keeps the fields the
  * records omit (schema.h OUTPUT); applyEvents clears stickiness, so a drop-in shim
- * zeroes Sticky* / Client* after the call. */
+ * zeroes Sticky* / Client* after the call.  SignalRequestedIDs and BufferedEvents pass
+ * through applyEvents unchanged — no Replicate* method reads or writes them (their only
+ * writers are AddSignalRequested / DeleteSignalRequested, mutableStateBuilder.go:
+ * 1455-1474, the active-side AddTimerCanceledEvent's checkAndClearTimerFiredEvent,
+ * :2959, and CloseTransaction*, :3925) — so the shim carries a loaded state's sets into
+ * the result as they are, and a fresh builder's are empty. */
 typedef struct cdr_carry {
   const int32_t* src;      /* [n_wfs of the batch] */
   const cdr_wf_caps* caps; /* [n_src] row offsets of the loaded states' tables */
