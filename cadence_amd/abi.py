@@ -193,6 +193,14 @@ CdrLastDecision = _S("cdr_last_decision", [
     ("started_id", i64), ("attempt", i64), ("scheduled_ts", i64), ("started_ts", i64),
     ("original_scheduled_ts", i64), ("decision_timeout", i32), ("_pad", i32)])
 LD_NONE, LD_SCHEDULED, LD_STARTED, LD_TRANSIENT = range(4)
+CdrIngestIn = _S("cdr_ingest_in", [(n, C.c_void_p) for n in (
+    "blob_bytes", "blob_off", "entry_blob0", "seed_bytes", "seed_off", "domain_map")] + [
+    ("n_blobs", u32), ("n_entries", u32), ("n_seeds", u32), ("n_domains", u32)])
+CdrIngestOut = _S("cdr_ingest_out", [(n, C.c_void_p) for n in (
+    "events", "kvs", "rps", "ev_off", "blob_status", "entry_status", "str_ref", "str_len")] + [
+    ("n_events", u64), ("n_kvs", u64), ("n_rps", u64), ("n_strings", u32), ("n_bad_blobs", u32)])
+DEC_STATUS = {0: "OK", 1: "MISSING_VERSION", 2: "INVALID_VERSION", 3: "TRUNCATED", 4: "DEPTH", 5: "NO_EVENTS",
+              6: "BAD_SIZE", 7: "BAD_TYPE"}
 CdrOpts = _S("cdr_opts", [("plan_mode", u32), ("fast_path", i32), ("reg_path", i32), ("concurrent", i32),
                           ("workspace_bytes", u64)])
 CdrVHToken = _S("cdr_vh_token", [("tree", u32), ("_pad", u32), ("branch_lo", u64), ("branch_hi", u64)])
@@ -286,7 +294,7 @@ MIRRORS = {
     "cdr_slices": CdrSlices, "cdr_dev_batch": CdrDevBatch, "cdr_carry": CdrCarry,
     "cdr_task": CdrTask, "cdr_vh_token": CdrVHToken, "cdr_vh_branch": CdrVHBranch, "cdr_vhs": CdrVHS,
     "cdr_ndc_task": CdrNdcTask, "cdr_ndc_decision": CdrNdcDecision, "cdr_last_decision": CdrLastDecision,
-    "cdr_opts": CdrOpts,
+    "cdr_opts": CdrOpts, "cdr_ingest_in": CdrIngestIn, "cdr_ingest_out": CdrIngestOut,
 }
 
 # C ABI entry points declared in include/cdr/cdr.h and include/cdr/synth.h
@@ -338,6 +346,9 @@ EXPORTS = {
     "cdr_synth_weights": (i32, [C.POINTER(CdrSynthParams), u64, C.c_void_p]),
     "cdr_synth_ndc_tasks": (i32, [C.POINTER(CdrSynthParams), i32, C.c_void_p, C.c_void_p, u32]),
     "cdr_struct_size": (u64, [C.c_char_p]),
+    "cdr_ingest_decode": (i32, [C.c_void_p, C.POINTER(CdrIngestIn), C.POINTER(CdrIngestOut), C.c_void_p]),
+    "cdr_synth_encode_history": (i32, [C.POINTER(CdrBatch), C.c_void_p, C.c_void_p, u32, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.POINTER(u64), C.POINTER(u32), i32]),
     "cdr_synth_size": (i32, [C.POINTER(CdrSynthParams), C.POINTER(CdrSynthSizes)]),
     "cdr_synth_fill": (i32, [C.POINTER(CdrSynthParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                              C.POINTER(CdrBatch)]),

@@ -23,6 +23,10 @@ enum cdr_ws_slot {
   WS_CY_CANCEL, WS_CY_SIGNAL, WS_CY_RP, WS_CY_SA, WS_CY_DESC,
   WS_O_RESULT, WS_O_EXEC, WS_O_REPL, WS_O_VH, WS_O_ACT, WS_O_TIMER, WS_O_CHILD, WS_O_CANCEL, WS_O_SIGNAL,
   WS_O_RP, WS_O_SA, WS_O_XFER, WS_O_TTASK, WS_O_NTASKS, WS_O_LD,
+  // cdr_ingest_decode (ingest.hip)
+  WS_IN_COUNTS, WS_IN_BASES, WS_IN_STATUS, WS_IN_ESTATUS, WS_IN_EVOFF, WS_IN_TKEY, WS_IN_TVAL, WS_IN_TREF,
+  WS_IN_TLEN, WS_IN_SKEY, WS_IN_SIDX, WS_IN_SKEY2, WS_IN_SIDX2, WS_IN_TMP, WS_IN_DOM, WS_IN_EVENTS, WS_IN_KVS,
+  WS_IN_RPS, WS_IN_STRREF, WS_IN_STRLEN, WS_IN_MISC,
   WS_NUM
 };
 
@@ -68,3 +72,4 @@ struct cdr_ctx {
 // device buffer `slot` of at least `bytes` (grow-only; contents undefined); nullptr
 // when the device is out of memory (defined in replay.hip)
 void* cdr_ws_get(cdr_ctx* c, int slot, uint64_t bytes);
+extern "C" int cdr_ctx_device(const cdr_ctx* c);  // replay.hip

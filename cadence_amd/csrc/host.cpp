@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "cdr/cdr.h"
+#include "cdr/ingest.h"
 #include "internal.h"
 
 namespace {
@@ -854,6 +855,8 @@ uint64_t cdr_struct_size(const char* name) {
       {"cdr_task", sizeof(cdr_task)},
       {"cdr_last_decision", sizeof(cdr_last_decision)},
       {"cdr_opts", sizeof(cdr_opts)},
+      {"cdr_ingest_in", sizeof(cdr_ingest_in)},
+      {"cdr_ingest_out", sizeof(cdr_ingest_out)},
       {"cdr_vh_token", sizeof(cdr_vh_token)},
       {"cdr_vh_branch", sizeof(cdr_vh_branch)},
       {"cdr_vhs", sizeof(cdr_vhs)},

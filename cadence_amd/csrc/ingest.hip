@@ -1,0 +1,929 @@
+// ingest.hip — on-device decode of thriftrw history blobs into the replay's input
+// records (cdr/ingest.h).
+//
+// One lane per blob (one history node = one applyEvents batch).  A thrift binary
+// value is only addressable after the one before it is parsed, so a blob is a
+// sequential walk; the parallelism is across blobs (a 1M-workflow population has tens
+// of millions of them).  Three passes read the bytes:
+//   1. k_blob_count   events, search-attribute pairs, reset points and string fields
+//                     per blob, and the decode status;
+//   2. k_blob_intern  every string into a device open-addressing table keyed by its
+//                     64-bit hash (atomicCAS on the key; seeds first, with their handles);
+//                     then the new strings are sorted by hash (hipcub radix sort) and
+//                     get handles n_seeds + rank;
+//   3. k_blob_fill    the cdr_event / cdr_kv / cdr_reset_point records at the offsets an
+//                     exclusive scan of pass 1's counts gives, handles looked up.
+// The parser is one template (the pass is its parameter), so the three walks agree on
+// every byte.  Wire format: go.uber.org/thriftrw protocol.Binary — a struct is fields
+// (type byte, big-endian i16 id, value) ending in a 0 byte; i16/i32/i64/double
+// big-endian; string/binary an i32 length and the bytes; list/set an element type, an
+// i32 count and the elements; map key type, value type, i32 count, pairs.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include <cstdio>
+#include <vector>
+
+#include "cdr/cdr.h"
+#include "cdr/ingest.h"
+#include "ctx.h"
+
+#define HIPCHK(x)                                                                                     \
+  do {                                                                                                \
+    hipError_t _e = (x);                                                                              \
+    if (_e != hipSuccess) {                                                                           \
+      fprintf(stderr, "cdr: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(_e), __FILE__, __LINE__); \
+      return CDR_API_EDEVICE;                                                                         \
+    }                                                                                                 \
+  } while (0)
+
+namespace {
+
+enum : uint32_t {
+  T_STOP = 0, T_BOOL = 2, T_BYTE = 3, T_DOUBLE = 4, T_I16 = 6, T_I32 = 8, T_I64 = 10, T_STRING = 11,
+  T_STRUCT = 12, T_MAP = 13, T_SET = 14, T_LIST = 15
+};
+constexpr uint32_t UNASSIGNED = 0xFFFFFFFFu;
+constexpr uint64_t SEED_REF = 1ull << 63;
+
+// ---------------------------------------------------------------- string table
+struct STab {
+  unsigned long long* key;  // 0 = empty slot
+  uint32_t* val;            // handle (UNASSIGNED until ranked)
+  uint64_t* ref;            // blob-byte offset of the first occurrence (| SEED_REF: seed byte offset)
+  uint32_t* len;
+  uint64_t mask;
+  uint32_t* overflow;
+};
+__device__ __forceinline__ uint64_t slot0(uint64_t h, uint64_t mask) { return cdr_mix64(h) & mask; }
+
+__device__ void tab_insert(const STab& T, uint64_t h, uint64_t ref, uint32_t len, uint32_t handle) {
+  uint64_t i = slot0(h, T.mask);
+  for (uint64_t probe = 0; probe <= T.mask; probe++, i = (i + 1) & T.mask) {
+    const unsigned long long k = atomicCAS(&T.key[i], 0ull, (unsigned long long)h);
+    if (k == 0ull) {  // this lane owns the slot
+      T.ref[i] = ref;
+      T.len[i] = len;
+      T.val[i] = handle;
+      return;
+    }
+    if (k == h) return;
+  }
+  atomicOr(T.overflow, 1u);  // sized at twice the string fields: never taken
+}
+
+__device__ uint32_t tab_lookup(const STab& T, uint64_t h) {
+  uint64_t i = slot0(h, T.mask);
+  for (uint64_t probe = 0; probe <= T.mask; probe++, i = (i + 1) & T.mask) {
+    const uint64_t k = T.key[i];
+    if (k == h) return T.val[i];
+    if (k == 0) break;
+  }
+  return 0;  // not interned (cannot happen after pass 2)
+}
+
+__device__ uint64_t hash_bytes(const uint8_t* p, uint64_t n) { return cdr_str_hash(p, n); }
+
+// ---------------------------------------------------------------- reader
+struct Rd {
+  const uint8_t* b;  // blob_bytes
+  uint64_t pos, end;
+  int32_t err;
+  __device__ bool ok() const { return err == CDR_DEC_OK; }
+  __device__ bool need(uint64_t n) {
+    if (err) return false;
+    if (end - pos < n) {
+      err = CDR_DEC_TRUNCATED;
+      pos = end;
+      return false;
+    }
+    return true;
+  }
+  __device__ uint32_t u8() {
+    if (!need(1)) return 0;
+    return b[pos++];
+  }
+  __device__ uint32_t be16() {
+    if (!need(2)) return 0;
+    const uint32_t v = ((uint32_t)b[pos] << 8) | b[pos + 1];
+    pos += 2;
+    return v;
+  }
+  __device__ uint32_t be32() {
+    if (!need(4)) return 0;
+    const uint32_t v = ((uint32_t)b[pos] << 24) | ((uint32_t)b[pos + 1] << 16) | ((uint32_t)b[pos + 2] << 8) | b[pos + 3];
+    pos += 4;
+    return v;
+  }
+  __device__ uint64_t be64() {
+    const uint64_t hi = be32();
+    return (hi << 32) | be32();
+  }
+  __device__ int32_t size() {  // a length / count: negative is a decode error
+    const int32_t n = (int32_t)be32();
+    if (n < 0 && !err) err = CDR_DEC_BAD_SIZE;
+    return n < 0 ? 0 : n;
+  }
+};
+
+__device__ uint32_t fixed_size(uint32_t t) {
+  switch (t) {
+    case T_BOOL: case T_BYTE: return 1;
+    case T_I16: return 2;
+    case T_I32: return 4;
+    case T_I64: case T_DOUBLE: return 8;
+    default: return 0;
+  }
+}
+
+// skip one value of wire type t (iterative: an explicit stack of open containers)
+__device__ void skip(Rd& r, uint32_t t) {
+  struct Fr {
+    uint32_t kind, t1, t2;
+    uint32_t n;  // remaining elements (maps: 2 per pair)
+  };
+  Fr st[CDR_THRIFT_MAX_DEPTH];
+  int d = 0;
+  uint32_t cur = t;
+  for (;;) {
+    if (!r.ok()) return;
+    // ---- one value of type cur
+    if (const uint32_t fs = fixed_size(cur)) {
+      if (r.need(fs)) r.pos += fs;
+    } else if (cur == T_STRING) {
+      const uint32_t n = (uint32_t)r.size();
+      if (r.need(n)) r.pos += n;
+    } else if (cur == T_STRUCT || cur == T_LIST || cur == T_SET || cur == T_MAP) {
+      if (d == CDR_THRIFT_MAX_DEPTH) {
+        r.err = CDR_DEC_DEPTH;
+        return;
+      }
+      Fr f{cur, 0, 0, 0};
+      if (cur == T_LIST || cur == T_SET) {
+        f.t1 = r.u8();
+        f.n = (uint32_t)r.size();
+      } else if (cur == T_MAP) {
+        f.t1 = r.u8();
+        f.t2 = r.u8();
+        f.n = 2u * (uint32_t)r.size();
+      }
+      st[d++] = f;
+    } else {
+      r.err = CDR_DEC_BAD_TYPE;
+      return;
+    }
+    // ---- the next value, from the innermost open container
+    bool have = false;
+    while (d > 0 && !have && r.ok()) {
+      Fr& f = st[d - 1];
+      if (f.kind == T_STRUCT) {
+        const uint32_t ft = r.u8();
+        if (ft == T_STOP) {
+          d--;
+          continue;
+        }
+        r.be16();
+        cur = ft;
+        have = true;
+      } else if (f.n == 0) {
+        d--;
+      } else {
+        cur = (f.kind == T_MAP && (f.n & 1u)) ? f.t2 : f.t1;
+        f.n--;
+        have = true;
+      }
+    }
+    if (!have) return;
+  }
+}
+
+// ---------------------------------------------------------------- one blob
+enum Pass { COUNT = 0, INTERN = 1, FILL = 2 };
+
+struct Ctx {  // per launch
+  const uint8_t* bytes;
+  const uint64_t* blob_off;
+  STab T;
+  const uint32_t* dom_id;  // [n_seeds]: ID handle of a domain name seed, UNASSIGNED otherwise
+  uint32_t n_seeds;
+  // pass outputs
+  uint32_t* counts;   // COUNT: [4 * n_blobs] events, kvs, rps, strings
+  const uint64_t* bases;  // FILL: [3 * n_blobs] event, kv, rp bases
+  int32_t* status;
+  cdr_event* events;
+  cdr_kv* kvs;
+  cdr_reset_point* rps;
+};
+
+template <int P>
+struct Blob {
+  const Ctx& C;
+  Rd r;
+  uint32_t n_ev = 0, n_kv = 0, n_rp = 0, n_str = 0;
+  uint64_t ev0 = 0, kv0 = 0, rp0 = 0;
+
+  __device__ Blob(const Ctx& c, uint32_t b) : C(c) {
+    r.b = c.bytes;
+    r.pos = c.blob_off[b];
+    r.end = c.blob_off[b + 1];
+    r.err = CDR_DEC_OK;
+    if (P == FILL) {
+      ev0 = c.bases[3ull * b];
+      kv0 = c.bases[3ull * b + 1];
+      rp0 = c.bases[3ull * b + 2];
+    }
+  }
+
+  // a string / binary value (the field's wire type already checked): its handle
+  __device__ uint32_t str() {
+    const uint32_t n = (uint32_t)r.size();
+    if (!r.need(n)) return 0;
+    const uint64_t at = r.pos;
+    r.pos += n;
+    if (n == 0) return 0;
+    n_str++;
+    if (P == COUNT) return 0;
+    const uint64_t h = hash_bytes(r.b + at, n);
+    if (P == INTERN) {
+      tab_insert(C.T, h, at, n, UNASSIGNED);
+      return 0;
+    }
+    return tab_lookup(C.T, h);
+  }
+  // a whole value of wire type t interned by its bytes (structures kept as one handle)
+  __device__ uint32_t raw(uint32_t t) {
+    const uint64_t at = r.pos;
+    skip(r, t);
+    if (!r.ok() || r.pos == at) return 0;
+    const uint32_t n = (uint32_t)(r.pos - at);
+    n_str++;
+    if (P == COUNT) return 0;
+    const uint64_t h = hash_bytes(r.b + at, n);
+    if (P == INTERN) {
+      tab_insert(C.T, h, at, n, UNASSIGNED);
+      return 0;
+    }
+    return tab_lookup(C.T, h);
+  }
+  __device__ uint32_t domain_id(uint32_t name, bool* missing) {
+    const uint32_t id = (P == FILL && name < C.n_seeds) ? C.dom_id[name] : UNASSIGNED;
+    *missing = id == UNASSIGNED;
+    return id == UNASSIGNED ? 0u : id;
+  }
+  // iterate the fields of a struct: f(field type, field id) must consume the value
+  template <class F>
+  __device__ void fields(F&& f) {
+    while (r.ok()) {
+      const uint32_t ft = r.u8();
+      if (!r.ok() || ft == T_STOP) return;
+      const uint32_t fid = r.be16();
+      if (!r.ok()) return;
+      f(ft, fid);
+    }
+  }
+  __device__ int64_t i64(uint32_t ft) {
+    if (ft != T_I64) {
+      skip(r, ft);
+      return 0;
+    }
+    return (int64_t)r.be64();
+  }
+  // name of a WorkflowType / TaskList / ActivityType (field 10)
+  __device__ uint32_t name_of(uint32_t ft) {
+    if (ft != T_STRUCT) {
+      skip(r, ft);
+      return 0;
+    }
+    uint32_t h = 0;
+    fields([&](uint32_t t, uint32_t id) {
+      if (id == 10 && t == T_STRING) h = str();
+      else skip(r, t);
+    });
+    return h;
+  }
+  // shared.WorkflowExecution{10 workflowId, 20 runId}
+  __device__ void execution(uint32_t ft, uint32_t* wid, uint32_t* rid) {
+    if (ft != T_STRUCT) {
+      skip(r, ft);
+      return;
+    }
+    fields([&](uint32_t t, uint32_t id) {
+      if (id == 10 && t == T_STRING) *wid = str();
+      else if (id == 20 && t == T_STRING) *rid = str();
+      else skip(r, t);
+    });
+  }
+  // RetryPolicy (shared.thrift RetryPolicy): the fields the record keeps
+  template <class A>
+  __device__ void retry(A& a) {
+    fields([&](uint32_t t, uint32_t id) {
+      if (id == 10 && t == T_I32) a.retry_initial_s = (int32_t)r.be32();
+      else if (id == 20 && t == T_DOUBLE) a.backoff_coefficient = __longlong_as_double((long long)r.be64());
+      else if (id == 30 && t == T_I32) a.retry_max_interval_s = (int32_t)r.be32();
+      else if (id == 40 && t == T_I32) a.retry_max_attempts = (int32_t)r.be32();
+      else if (id == 60 && t == T_I32) a.retry_expiration_s = (int32_t)r.be32();
+      else if (id == 50 && t == T_LIST) {  // nonRetriableErrorReasons: the list's bytes, empty -> 0
+        const uint64_t at = r.pos;
+        r.u8();
+        const int32_t cnt = r.size();
+        r.pos = r.ok() ? at : r.pos;
+        a.nonretriable = cnt > 0 ? raw(T_LIST) : (skip(r, T_LIST), 0u);
+      } else skip(r, t);
+    });
+  }
+  // SearchAttributes{10: map<string, binary>} -> kv rows; returns the pair count
+  __device__ uint32_t search_attrs(uint32_t* off) {
+    uint32_t cnt = 0;
+    *off = (uint32_t)(kv0 + n_kv);
+    fields([&](uint32_t t, uint32_t id) {
+      if (id != 10 || t != T_MAP) {
+        skip(r, t);
+        return;
+      }
+      const uint32_t kt = r.u8(), vt = r.u8();
+      const int32_t n = r.size();
+      for (int32_t i = 0; i < n && r.ok(); i++) {
+        if (kt == T_STRING && vt == T_STRING) {
+          const uint32_t k = str(), v = str();
+          if (P == FILL) C.kvs[kv0 + n_kv] = cdr_kv{k, v};
+          n_kv++;
+          cnt++;
+        } else {  // not a map<string, binary>: thriftrw reads no entries
+          skip(r, kt);
+          skip(r, vt);
+        }
+      }
+    });
+    return cnt;
+  }
+  // ResetPoints{10: list<ResetPointInfo>} -> reset-point rows; false when field 10 is absent
+  __device__ bool reset_points(uint32_t* off, uint32_t* len) {
+    bool have = false;
+    *off = (uint32_t)(rp0 + n_rp);
+    *len = 0;
+    fields([&](uint32_t t, uint32_t id) {
+      if (id != 10 || t != T_LIST) {
+        skip(r, t);
+        return;
+      }
+      const uint32_t et = r.u8();
+      const int32_t n = r.size();
+      if (et != T_STRUCT) {  // not a list of structs: no points
+        for (int32_t i = 0; i < n && r.ok(); i++) skip(r, et);
+        return;
+      }
+      have = true;
+      for (int32_t i = 0; i < n && r.ok(); i++) {
+        cdr_reset_point p{};
+        fields([&](uint32_t t2, uint32_t id2) {
+          if (id2 == 10 && t2 == T_STRING) {
+            p.binary_checksum = str();
+            p.flags |= CDR_RP_HAS_CHECKSUM;
+          } else if (id2 == 20 && t2 == T_STRING) {
+            p.run_id = str();
+            p.flags |= CDR_RP_HAS_RUN_ID;
+          } else if (id2 == 30 && t2 == T_I64) {
+            p.first_decision_completed_id = (int64_t)r.be64();
+            p.flags |= CDR_RP_HAS_FIRST_DC_ID;
+          } else if (id2 == 40 && t2 == T_I64) {
+            p.created_time_nano = (int64_t)r.be64();
+            p.flags |= CDR_RP_HAS_CREATED;
+          } else if (id2 == 50 && t2 == T_I64) {
+            p.expiring_time_nano = (int64_t)r.be64();
+            p.flags |= CDR_RP_HAS_EXPIRING;
+          } else if (id2 == 60 && t2 == T_BOOL) {
+            p.flags |= CDR_RP_HAS_RESETTABLE | (r.u8() ? CDR_RP_RESETTABLE : 0u);
+          } else skip(r, t2);
+        });
+        if (P == FILL) C.rps[rp0 + n_rp] = p;
+        n_rp++;
+        (*len)++;
+      }
+    });
+    return have;
+  }
+
+  // WorkflowExecutionStartedEventAttributes (shared.thrift, field 40 of HistoryEvent)
+  __device__ void started(cdr_attr_wf_started& s) {
+    fields([&](uint32_t t, uint32_t id) {
+      switch (id) {
+        case 10: s.workflow_type = name_of(t); break;
+        case 12:
+          if (t == T_STRING) {
+            bool miss;
+            s.flags |= CDR_SF_HAS_PARENT_DOMAIN;
+            s.parent_domain_id = domain_id(str(), &miss);
+            s.flags |= miss ? CDR_SF_PARENT_DOMAIN_MISSING : 0u;
+          } else skip(r, t);
+          break;
+        case 14:
+          if (t == T_STRUCT) s.flags |= CDR_SF_HAS_PARENT_EXEC;
+          execution(t, &s.parent_workflow_id, &s.parent_run_id);
+          break;
+        case 16:
+          if (t == T_I64) {
+            s.flags |= CDR_SF_HAS_PARENT_INITIATED;
+            s.parent_initiated_id = (int64_t)r.be64();
+          } else skip(r, t);
+          break;
+        case 20: s.task_list = name_of(t); break;
+        case 40: if (t == T_I32) s.exec_timeout_s = (int32_t)r.be32(); else skip(r, t); break;
+        case 50: if (t == T_I32) s.task_timeout_s = (int32_t)r.be32(); else skip(r, t); break;
+        case 54: if (t == T_STRING) s.continued_run_id = str(); else skip(r, t); break;
+        case 55:
+          if (t == T_I32) {  // ContinueAsNewInitiator: Decider 0, RetryPolicy 1, CronSchedule 2
+            const int32_t v = (int32_t)r.be32();
+            s.flags |= CDR_SF_HAS_INITIATOR | (v == 2 ? CDR_SF_CRON_INITIATOR : 0u) |
+                       (v == 1 ? CDR_SF_RETRY_INITIATOR : 0u) | (v == 0 ? CDR_SF_DECIDER_INITIATOR : 0u);
+          } else skip(r, t);
+          break;
+        case 70:
+          if (t == T_STRUCT) {
+            s.flags |= CDR_SF_HAS_RETRY;
+            retry(s);
+          } else skip(r, t);
+          break;
+        case 80: if (t == T_I32) s.attempt = (int32_t)r.be32(); else skip(r, t); break;
+        case 90: if (t == T_I64) s.expiration_ts = (int64_t)r.be64(); else skip(r, t); break;
+        case 100: if (t == T_STRING) s.cron_schedule = str(); else skip(r, t); break;
+        case 110: if (t == T_I32) s.first_decision_backoff_s = (int32_t)r.be32(); else skip(r, t); break;
+        case 120:
+          if (t == T_STRUCT) {
+            s.flags |= CDR_SF_HAS_MEMO;
+            s.memo = raw(T_STRUCT);
+          } else skip(r, t);
+          break;
+        case 121:
+          if (t == T_STRUCT) {
+            s.flags |= CDR_SF_HAS_SEARCH_ATTR;
+            s.search_attr_len = search_attrs(&s.search_attr_off);
+          } else skip(r, t);
+          break;
+        case 130:
+          if (t == T_STRUCT) {
+            if (reset_points(&s.reset_points_off, &s.reset_points_len)) s.flags |= CDR_SF_HAS_RESET_POINTS;
+            else s.reset_points_off = s.reset_points_len = 0;
+          } else skip(r, t);
+          break;
+        default: skip(r, t); break;
+      }
+    });
+  }
+
+  // StartChild / SignalExternal / RequestCancelExternal ...Initiated
+  __device__ void external(uint32_t attr, cdr_attr_external& x) {
+    // field ids: domain, workflowId (child), WorkflowExecution, workflowType (child),
+    // signalName, input, control, childWorkflowOnly, parentClosePolicy
+    const bool child = attr == 340, sig = attr == 420;
+    const uint32_t f_dom = child ? 10 : 20, f_we = child ? 0 : 30, f_wid = child ? 20 : 0;
+    const uint32_t f_in = child ? 50 : (sig ? 50 : 0), f_ctl = child ? 90 : (sig ? 60 : 40);
+    const uint32_t f_only = child ? 0 : (sig ? 70 : 50);
+    uint32_t dom_name = 0;
+    bool have_dom = false;
+    fields([&](uint32_t t, uint32_t id) {
+      if (id == f_dom && t == T_STRING) {
+        dom_name = str();
+        have_dom = true;
+      } else if (f_we && id == f_we) execution(t, &x.workflow_id, &x.run_id);
+      else if (f_wid && id == f_wid && t == T_STRING) x.workflow_id = str();
+      else if (child && id == 30) x.workflow_type = name_of(t);
+      else if (sig && id == 40 && t == T_STRING) x.signal_name = str();
+      else if (f_in && id == f_in && t == T_STRING) x.input = str();
+      else if (id == f_ctl && t == T_STRING) x.control = str();
+      else if (f_only && id == f_only && t == T_BOOL) x.flags |= r.u8() ? CDR_XF_CHILD_ONLY : 0u;
+      else if (child && id == 81 && t == T_I32) x.parent_close_policy = (int32_t)r.be32();
+      else skip(r, t);
+    });
+    (void)have_dom;
+    x.domain = dom_name;
+    bool miss;
+    x.target_domain_id = domain_id(dom_name, &miss);
+    x.flags |= miss ? CDR_XF_DOMAIN_MISSING : 0u;
+  }
+
+  // the attribute struct (HistoryEvent field `attr`) into the record's union
+  __device__ void attributes(uint32_t attr, cdr_event& e) {
+    // decision / activity events: field ids of scheduledEventId, startedEventId,
+    // requestId, activityId, timeoutType, attempt, binaryChecksum (0 = none)
+    struct Ids {
+      uint16_t attr;
+      uint8_t sched, started, req, aid, to, att, cks;
+    };
+    static constexpr Ids kIds[] = {
+        {90, 10, 0, 30, 0, 0, 0, 0},    // DecisionTaskStarted
+        {100, 20, 30, 0, 0, 0, 0, 50},  // DecisionTaskCompleted
+        {110, 10, 20, 0, 0, 30, 0, 0},  // DecisionTaskTimedOut
+        {120, 10, 20, 0, 0, 0, 0, 0},   // DecisionTaskFailed
+        {140, 10, 0, 30, 0, 0, 40, 0},  // ActivityTaskStarted
+        {150, 20, 30, 0, 0, 0, 0, 0},   // ActivityTaskCompleted
+        {160, 30, 40, 0, 0, 0, 0, 0},   // ActivityTaskFailed
+        {170, 10, 20, 0, 0, 30, 0, 0},  // ActivityTaskTimedOut
+        {200, 0, 0, 0, 10, 0, 0, 0},    // ActivityTaskCancelRequested
+        {210, 0, 0, 0, 10, 0, 0, 0},    // RequestCancelActivityTaskFailed
+        {220, 30, 40, 0, 0, 0, 0, 0},   // ActivityTaskCanceled
+    };
+    // child / external closes: initiatedEventId, WorkflowExecution
+    struct Ref {
+      uint16_t attr;
+      uint8_t init, we;
+    };
+    static constexpr Ref kRef[] = {
+        {310, 50, 40}, {320, 10, 30}, {350, 60, 0},  {360, 20, 30}, {370, 50, 30}, {380, 60, 40},
+        {390, 50, 30}, {400, 50, 30}, {410, 40, 20}, {430, 50, 40}, {440, 10, 30},
+    };
+    switch (attr) {
+      case 40: started(e.a.started); return;
+      case 80:
+        fields([&](uint32_t t, uint32_t id) {
+          if (id == 10) e.a.dt_sched.task_list = name_of(t);
+          else if (id == 20 && t == T_I32) e.a.dt_sched.start_to_close_s = (int32_t)r.be32();
+          else if (id == 30 && t == T_I64) e.a.dt_sched.attempt = (int64_t)r.be64();
+          else skip(r, t);
+        });
+        return;
+      case 130: {
+        cdr_attr_at_scheduled& a = e.a.at_sched;
+        fields([&](uint32_t t, uint32_t id) {
+          if (id == 10 && t == T_STRING) a.activity_id = str();
+          else if (id == 30) a.task_list = name_of(t);
+          else if (id == 45 && t == T_I32) a.s2c_s = (int32_t)r.be32();
+          else if (id == 50 && t == T_I32) a.s2s_s = (int32_t)r.be32();
+          else if (id == 55 && t == T_I32) a.stc_s = (int32_t)r.be32();
+          else if (id == 60 && t == T_I32) a.hb_s = (int32_t)r.be32();
+          else if (id == 110 && t == T_STRUCT) {
+            a.flags |= CDR_AF_HAS_RETRY;
+            retry(a);
+          } else skip(r, t);
+        });
+        return;
+      }
+      case 180: case 190: case 230: case 240: {
+        cdr_attr_timer& a = e.a.timer;
+        fields([&](uint32_t t, uint32_t id) {
+          if (id == 10 && t == T_STRING) a.timer_id = str();
+          else if (id == 20 && t == T_I64) {
+            const int64_t v = (int64_t)r.be64();
+            if (attr == 180) a.start_to_fire_s = v;
+            else if (attr != 240) a.started_event_id = v;
+          } else skip(r, t);
+        });
+        return;
+      }
+      case 300: case 340: case 420: external(attr, e.a.ext); return;
+      case 330:
+        fields([&](uint32_t t, uint32_t id) {
+          if (id == 10 && t == T_STRING) e.a.can.new_execution_run_id = str();
+          else skip(r, t);
+        });
+        return;
+      case 450:
+        fields([&](uint32_t t, uint32_t id) {
+          if (id == 20 && t == T_STRUCT) e.a.upsert.search_attr_len = search_attrs(&e.a.upsert.search_attr_off);
+          else skip(r, t);
+        });
+        return;
+      default: break;
+    }
+    for (const Ids& m : kIds) {
+      if (m.attr != attr) continue;
+      const bool act = attr >= 140;
+      fields([&](uint32_t t, uint32_t id) {
+        if (m.sched && id == m.sched && t == T_I64) {
+          const int64_t v = (int64_t)r.be64();
+          if (act) e.a.at.scheduled_event_id = v;
+          else e.a.dt.scheduled_event_id = v;
+        } else if (m.started && id == m.started && t == T_I64) {
+          const int64_t v = (int64_t)r.be64();
+          if (act) e.a.at.started_event_id = v;
+          else e.a.dt.started_event_id = v;
+        } else if (m.req && id == m.req && t == T_STRING) {
+          const uint32_t h = str();
+          if (act) e.a.at.request_id = h;
+          else e.a.dt.request_id = h;
+        } else if (m.aid && id == m.aid && t == T_STRING) {
+          e.a.at.activity_id = str();
+        } else if (m.to && id == m.to && t == T_I32) {
+          const int32_t v = (int32_t)r.be32();
+          if (act) e.a.at.timeout_type = v;
+          else e.a.dt.timeout_type = v;
+        } else if (m.att && id == m.att && t == T_I32) {
+          e.a.at.attempt = (int32_t)r.be32();
+        } else if (m.cks && id == m.cks && t == T_STRING) {
+          e.a.dt.binary_checksum = str();
+        } else skip(r, t);
+      });
+      return;
+    }
+    for (const Ref& m : kRef) {
+      if (m.attr != attr) continue;
+      fields([&](uint32_t t, uint32_t id) {
+        if (id == m.init && t == T_I64) e.a.ref.initiated_event_id = (int64_t)r.be64();
+        else if (m.we && id == m.we) {
+          uint32_t wid = 0;
+          execution(t, &wid, &e.a.ref.run_id);
+        } else skip(r, t);
+      });
+      return;
+    }
+    skip(r, T_STRUCT);  // an attribute struct the record form does not keep
+  }
+
+  // HistoryEvent (shared.thrift:868-916)
+  __device__ void event(bool first) {
+    cdr_event e;
+    uint64_t* z = reinterpret_cast<uint64_t*>(&e);
+#pragma unroll
+    for (uint32_t i = 0; i < sizeof(cdr_event) / 8; i++) z[i] = 0;
+    fields([&](uint32_t t, uint32_t id) {
+      switch (id) {
+        case 10: e.event_id = i64(t); break;
+        case 20: e.timestamp = i64(t); break;
+        case 30: if (t == T_I32) e.type = r.be32(); else skip(r, t); break;
+        case 35: e.version = i64(t); break;
+        case 36: e.task_id = i64(t); break;
+        default:
+          if (t == T_STRUCT && id >= 40 && id <= 450 && id % 10 == 0) attributes(id, e);
+          else skip(r, t);
+          break;
+      }
+    });
+    e.flags = first ? CDR_EVF_BATCH_FIRST : 0u;
+    if (P == FILL && r.ok()) {
+      cdr_event* d = C.events + ev0 + n_ev;
+      const uint64_t* s = reinterpret_cast<const uint64_t*>(&e);
+      uint64_t* o = reinterpret_cast<uint64_t*>(d);
+#pragma unroll
+      for (uint32_t i = 0; i < sizeof(cdr_event) / 8; i++) o[i] = s[i];
+    }
+    n_ev++;
+  }
+
+  // codec preamble + History{10: list<HistoryEvent>}
+  __device__ void run() {
+    if (r.end <= r.pos) {
+      r.err = CDR_DEC_MISSING_VERSION;
+      return;
+    }
+    if (r.u8() != CDR_THRIFT_PREAMBLE_V0) {
+      r.err = CDR_DEC_INVALID_VERSION;
+      return;
+    }
+    fields([&](uint32_t t, uint32_t id) {
+      if (id != 10 || t != T_LIST) {
+        skip(r, t);
+        return;
+      }
+      const uint32_t et = r.u8();
+      const int32_t n = r.size();
+      if (et != T_STRUCT) {  // not a list of structs: thriftrw reads no events
+        for (int32_t i = 0; i < n && r.ok(); i++) skip(r, et);
+        return;
+      }
+      // a repeated field 10 replaces the events read so far (FromWire assigns each occurrence)
+      n_ev = n_kv = n_rp = 0;
+      for (int32_t i = 0; i < n && r.ok(); i++) event(n_ev == 0);
+    });
+    if (r.ok() && n_ev == 0) r.err = CDR_DEC_NO_EVENTS;
+  }
+};
+
+template <int P>
+__global__ __launch_bounds__(256) void k_blob(Ctx C, uint32_t n_blobs) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n_blobs) return;
+  if (P != COUNT && C.status[b] != CDR_DEC_OK) return;  // a failed blob contributes nothing
+  Blob<P> x(C, b);
+  x.run();
+  if (P == COUNT) {
+    C.counts[4ull * b] = x.r.ok() ? x.n_ev : 0u;
+    C.counts[4ull * b + 1] = x.r.ok() ? x.n_kv : 0u;
+    C.counts[4ull * b + 2] = x.r.ok() ? x.n_rp : 0u;
+    C.counts[4ull * b + 3] = x.n_str;
+    C.status[b] = x.r.err;
+  }
+}
+
+__global__ void k_seed(STab T, const uint8_t* bytes, const uint64_t* off, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 || i >= n) return;  // seed 0 is "" (handle 0, never in the table)
+  const uint64_t a = off[i], len = off[i + 1] - a;
+  if (len == 0) return;
+  tab_insert(T, cdr_str_hash(bytes + a, len), a | SEED_REF, (uint32_t)len, i);
+}
+
+// seeds may collide with one another only by equal strings; the first claimant keeps its
+// handle, the table's value is what lookups return
+
+__global__ void k_collect_new(STab T, unsigned long long* keys, uint64_t* idx, uint32_t* n_new) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > T.mask) return;
+  if (T.key[i] != 0ull && T.val[i] == UNASSIGNED) {
+    const uint32_t j = atomicAdd(n_new, 1u);
+    keys[j] = T.key[i];
+    idx[j] = i;
+  }
+}
+
+__global__ void k_rank(STab T, const uint64_t* idx_sorted, uint32_t n_new, uint32_t n_seeds, uint64_t* str_ref,
+                       uint32_t* str_len) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_new) return;
+  const uint64_t s = idx_sorted[j];
+  const uint32_t h = n_seeds + j;
+  T.val[s] = h;
+  str_ref[h] = T.ref[s];
+  str_len[h] = T.len[s];
+}
+
+__global__ void k_seed_refs(const uint64_t* off, uint32_t n, uint64_t* str_ref, uint32_t* str_len) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  str_ref[i] = off[i] | SEED_REF;
+  str_len[i] = (uint32_t)(off[i + 1] - off[i]);
+}
+
+__global__ void k_domains(const uint32_t* map, uint32_t n_dom, uint32_t* dom_id, uint32_t n_seeds) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_dom) return;
+  const uint32_t name = map[2 * i], id = map[2 * i + 1];
+  if (name < n_seeds) dom_id[name] = id;
+}
+
+// per-blob counts (4 per blob) -> per-blob bases (3 per blob) via the scanned columns
+__global__ void k_split(const uint32_t* counts, uint64_t* cols, uint32_t n_blobs) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n_blobs) return;
+  for (int c = 0; c < 3; c++) cols[(uint64_t)c * n_blobs + b] = counts[4ull * b + c];
+}
+__global__ void k_bases(const uint64_t* scanned, uint64_t* bases, uint32_t n_blobs) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n_blobs) return;
+  for (int c = 0; c < 3; c++) bases[3ull * b + c] = scanned[(uint64_t)c * n_blobs + b];
+}
+__global__ void k_entries(const uint32_t* entry_blob0, uint32_t n_entries, const uint64_t* scanned_ev,
+                          const uint32_t* counts, uint32_t n_blobs, const int32_t* status, uint64_t* ev_off,
+                          int32_t* entry_status) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w > n_entries) return;
+  const uint32_t b0 = entry_blob0[w];
+  ev_off[w] = b0 < n_blobs ? scanned_ev[b0]
+                           : (n_blobs ? scanned_ev[n_blobs - 1] + counts[4ull * (n_blobs - 1)] : 0ull);
+  if (w == n_entries) return;
+  int32_t st = CDR_DEC_OK;
+  for (uint32_t b = b0; b < entry_blob0[w + 1] && st == CDR_DEC_OK; b++) st = status[b];
+  entry_status[w] = st;
+}
+
+template <class T>
+int ws(cdr_ctx* c, int slot, uint64_t n, T** p) {
+  *p = (T*)cdr_ws_get(c, slot, n * sizeof(T) + 8);
+  return *p ? CDR_API_OK : CDR_API_ENOMEM;
+}
+
+}  // namespace
+
+extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_ingest_out* out, void* stream) {
+  if (!ctx || !in || !out || !in->blob_off || !in->entry_blob0 || !in->seed_off || in->n_seeds == 0)
+    return CDR_API_EINVAL;
+  if (in->n_blobs && !in->blob_bytes) return CDR_API_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(cdr_ctx_device(ctx)));
+  const uint32_t nb = in->n_blobs, ne = in->n_entries;
+  *out = cdr_ingest_out{};
+  int rc;
+  uint32_t *counts, *misc;
+  int32_t *status, *estatus;
+  uint64_t *cols, *scanned, *bases, *ev_off;
+  if ((rc = ws(ctx, WS_IN_COUNTS, 4ull * nb + 4, &counts)) || (rc = ws(ctx, WS_IN_STATUS, nb + 1ull, &status)) ||
+      (rc = ws(ctx, WS_IN_ESTATUS, ne + 1ull, &estatus)) || (rc = ws(ctx, WS_IN_TMP, 3ull * nb + 3, &cols)) ||
+      (rc = ws(ctx, WS_IN_SKEY2, 3ull * nb + 3, &scanned)) || (rc = ws(ctx, WS_IN_BASES, 3ull * nb + 3, &bases)) ||
+      (rc = ws(ctx, WS_IN_EVOFF, ne + 1ull, &ev_off)) || (rc = ws(ctx, WS_IN_MISC, 16, &misc)))
+    return rc;
+  Ctx C{};
+  C.bytes = in->blob_bytes;
+  C.blob_off = in->blob_off;
+  C.counts = counts;
+  C.status = status;
+  C.n_seeds = in->n_seeds;
+  const dim3 blk(256);
+  auto grid = [](uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); };
+  // ---- pass 1: counts
+  if (nb) hipLaunchKernelGGL(k_blob<COUNT>, grid(nb), blk, 0, st, C, nb);
+  HIPCHK(hipGetLastError());
+  // string fields -> table capacity (2x, power of two)
+  uint64_t n_str_fields = 0;
+  {
+    std::vector<uint32_t> h(4ull * nb);
+    if (nb) HIPCHK(hipMemcpyAsync(h.data(), counts, 4ull * nb * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (uint32_t b = 0; b < nb; b++) n_str_fields += h[4ull * b + 3];
+  }
+  uint64_t cap = 1024;
+  while (cap < 2 * (n_str_fields + in->n_seeds)) cap <<= 1;
+  STab T{};
+  T.mask = cap - 1;
+  if ((rc = ws(ctx, WS_IN_TKEY, cap, (unsigned long long**)&T.key)) || (rc = ws(ctx, WS_IN_TVAL, cap, &T.val)) ||
+      (rc = ws(ctx, WS_IN_TREF, cap, &T.ref)) || (rc = ws(ctx, WS_IN_TLEN, cap, &T.len)))
+    return rc;
+  T.overflow = misc;
+  HIPCHK(hipMemsetAsync(T.key, 0, cap * 8, st));
+  HIPCHK(hipMemsetAsync(misc, 0, 64, st));
+  C.T = T;
+  // ---- pass 2: seeds, then every string of the blobs; rank the new ones by hash
+  hipLaunchKernelGGL(k_seed, grid(in->n_seeds), blk, 0, st, T, in->seed_bytes, in->seed_off, in->n_seeds);
+  if (nb) hipLaunchKernelGGL(k_blob<INTERN>, grid(nb), blk, 0, st, C, nb);
+  HIPCHK(hipGetLastError());
+  unsigned long long *k1, *k2;
+  uint64_t *i1, *i2;
+  if ((rc = ws(ctx, WS_IN_SKEY, n_str_fields + 1, &k1)) || (rc = ws(ctx, WS_IN_SIDX, n_str_fields + 1, &i1)) ||
+      (rc = ws(ctx, WS_IN_SIDX2, n_str_fields + 1, &i2)) ||
+      (rc = ws(ctx, WS_IN_STRREF, n_str_fields + in->n_seeds + 1, &out->str_ref)) ||
+      (rc = ws(ctx, WS_IN_STRLEN, n_str_fields + in->n_seeds + 1, &out->str_len)))
+    return rc;
+  // the sort's second key buffer (afterwards the seed -> domain ID map)
+  if ((rc = ws(ctx, WS_IN_DOM, (n_str_fields + 1) > in->n_seeds ? (n_str_fields + 1) * 2 : in->n_seeds * 2ull,
+               &k2)))
+    return rc;
+  hipLaunchKernelGGL(k_collect_new, grid(cap), blk, 0, st, T, k1, i1, misc + 1);
+  HIPCHK(hipGetLastError());
+  uint32_t hm[2];
+  HIPCHK(hipMemcpyAsync(hm, misc, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (hm[0]) return CDR_API_ENOMEM;  // table overflow: cannot happen at twice the fields
+  const uint32_t n_new = hm[1];
+  if (n_new) {
+    hipcub::DoubleBuffer<unsigned long long> kb(k1, k2);
+    hipcub::DoubleBuffer<uint64_t> vb(i1, i2);
+    size_t tmp_bytes = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kb, vb, (int)n_new, 0, 64, st));
+    // the records' slot is free until pass 3: the sort's temporary storage
+    void* sort_tmp = cdr_ws_get(ctx, WS_IN_EVENTS, tmp_bytes);
+    if (!sort_tmp) return CDR_API_ENOMEM;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(sort_tmp, tmp_bytes, kb, vb, (int)n_new, 0, 64, st));
+    hipLaunchKernelGGL(k_rank, grid(n_new), blk, 0, st, T, vb.Current(), n_new, in->n_seeds, out->str_ref,
+                       out->str_len);
+  }
+  hipLaunchKernelGGL(k_seed_refs, grid(in->n_seeds), blk, 0, st, in->seed_off, in->n_seeds, out->str_ref,
+                     out->str_len);
+  HIPCHK(hipGetLastError());
+  out->n_strings = in->n_seeds + n_new;
+  // domain names -> IDs (by seed handle), in the sort's second key buffer (free again)
+  uint32_t* dom_id = (uint32_t*)k2;
+  HIPCHK(hipMemsetAsync(dom_id, 0xFF, in->n_seeds * 4ull, st));
+  if (in->n_domains)
+    hipLaunchKernelGGL(k_domains, grid(in->n_domains), blk, 0, st, in->domain_map, in->n_domains, dom_id,
+                       in->n_seeds);
+  HIPCHK(hipGetLastError());
+  C.dom_id = dom_id;
+  // ---- offsets: exclusive scans of the per-blob event / kv / reset-point counts
+  if (nb) {
+    hipLaunchKernelGGL(k_split, grid(nb), blk, 0, st, counts, cols, nb);
+    size_t tmp_bytes = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cols, scanned, (int)nb, st));
+    void* scan_tmp = cdr_ws_get(ctx, WS_IN_SKEY, tmp_bytes > (n_str_fields + 1) * 8 ? tmp_bytes : 8);
+    if (!scan_tmp) return CDR_API_ENOMEM;
+    for (int c = 0; c < 3; c++)
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tmp_bytes, cols + (uint64_t)c * nb,
+                                              scanned + (uint64_t)c * nb, (int)nb, st));
+    hipLaunchKernelGGL(k_bases, grid(nb), blk, 0, st, scanned, bases, nb);
+  }
+  hipLaunchKernelGGL(k_entries, grid(ne + 1ull), blk, 0, st, in->entry_blob0, ne, scanned, counts, nb, status,
+                     ev_off, estatus);
+  HIPCHK(hipGetLastError());
+  // totals
+  uint64_t tot[3] = {0, 0, 0};
+  if (nb) {
+    uint64_t last[3];
+    uint32_t lc[4];
+    for (int c = 0; c < 3; c++)
+      HIPCHK(hipMemcpyAsync(&last[c], scanned + (uint64_t)c * nb + (nb - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(lc, counts + 4ull * (nb - 1), 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (int c = 0; c < 3; c++) tot[c] = last[c] + lc[c];
+  }
+  if ((rc = ws(ctx, WS_IN_EVENTS, tot[0] + 1, &out->events)) || (rc = ws(ctx, WS_IN_KVS, tot[1] + 1, &out->kvs)) ||
+      (rc = ws(ctx, WS_IN_RPS, tot[2] + 1, &out->rps)))
+    return rc;
+  // ---- pass 3: the records
+  C.bases = bases;
+  C.events = out->events;
+  C.kvs = out->kvs;
+  C.rps = out->rps;
+  if (nb) hipLaunchKernelGGL(k_blob<FILL>, grid(nb), blk, 0, st, C, nb);
+  HIPCHK(hipGetLastError());
+  out->ev_off = ev_off;
+  out->blob_status = status;
+  out->entry_status = estatus;
+  out->n_events = tot[0];
+  out->n_kvs = tot[1];
+  out->n_rps = tot[2];
+  // bad blobs
+  {
+    std::vector<int32_t> h(nb);
+    if (nb) HIPCHK(hipMemcpyAsync(h.data(), status, nb * 4ull, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (uint32_t b = 0; b < nb; b++) out->n_bad_blobs += h[b] != CDR_DEC_OK;
+  }
+  return CDR_API_OK;
+}

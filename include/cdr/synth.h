@@ -62,6 +62,17 @@ int cdr_synth_ndc_tasks(const cdr_synth_params* p, int fork, cdr_ndc_task* tasks
 /* history shard of synthetic workflow ids "wf-<i>", i in [0, n): farmhash
  * Fingerprint32 % num_shards (common/util.go:249-252) */
 int cdr_synth_shards(uint64_t n, int32_t num_shards, int32_t* out);
+/* Synthetic persisted histories (cadence_amd/csrc/thrift_enc.cpp): every entry of `b`
+ * written as the reference stores it — one blob per applyEvents call, preambleVersion0
+ * (0x59) + thriftrw shared.History{10: list<HistoryEvent>} — the input of
+ * cdr_ingest_decode (cdr/ingest.h).  Handle h is the string str_bytes[str_off[h],
+ * str_off[h+1]) for h < n_str, else "h%08x"; a parent domain is named "dn:" + its ID's
+ * string.  Sizes only when blob_bytes is NULL (*n_bytes, *n_blobs); otherwise
+ * blob_off[n_blobs + 1] and entry_blob0[n_wfs + 1] are filled too. */
+int cdr_synth_encode_history(const cdr_batch* b, const uint8_t* str_bytes, const uint64_t* str_off,
+                             uint32_t n_str, uint8_t* blob_bytes, uint64_t* blob_off, uint32_t* entry_blob0,
+                             uint64_t* n_bytes, uint32_t* n_blobs, int threads);
+
 #ifdef __cplusplus
 }
 #endif
