@@ -347,6 +347,8 @@ EXPORTS = {
     "cdr_synth_ndc_tasks": (i32, [C.POINTER(CdrSynthParams), i32, C.c_void_p, C.c_void_p, u32]),
     "cdr_struct_size": (u64, [C.c_char_p]),
     "cdr_ingest_decode": (i32, [C.c_void_p, C.POINTER(CdrIngestIn), C.POINTER(CdrIngestOut), C.c_void_p]),
+    "cdr_ingest_plan": (i32, [C.c_void_p, C.POINTER(CdrIngestOut), C.POINTER(CdrBatch), u32, C.POINTER(CdrDevBatch),
+                              C.c_void_p, C.POINTER(CdrTotals), C.c_void_p]),
     "cdr_synth_encode_history": (i32, [C.POINTER(CdrBatch), C.c_void_p, C.c_void_p, u32, C.c_void_p, C.c_void_p,
                                        C.c_void_p, C.POINTER(u64), C.POINTER(u32), i32]),
     "cdr_synth_size": (i32, [C.POINTER(CdrSynthParams), C.POINTER(CdrSynthSizes)]),

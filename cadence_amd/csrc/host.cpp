@@ -19,24 +19,9 @@
 #include "cdr/cdr.h"
 #include "cdr/ingest.h"
 #include "internal.h"
+#include "pack_event.h"
 
 namespace {
-
-// Arena record sizes (8-byte words) of the types that carry one.
-inline uint32_t arena_words_for(uint32_t type) {
-  switch (type) {
-    case CDR_EV_WF_STARTED:
-      return (sizeof(cdr_attr_wf_started) + 7) / 8;
-    case CDR_EV_AT_SCHEDULED:
-      return (sizeof(cdr_attr_at_scheduled) + 7) / 8;
-    case CDR_EV_CHILD_INITIATED:  // read only by task emission (target execution)
-    case CDR_EV_RCE_INITIATED:
-    case CDR_EV_SE_INITIATED:
-      return (sizeof(cdr_attr_external) + 7) / 8;
-    default:
-      return 0;
-  }
-}
 
 int hw_threads(int threads) {
   if (threads > 0) return threads;
@@ -77,7 +62,7 @@ void parallel_for(uint64_t n, int threads, F&& f) {
 
 namespace cdr_internal {
 
-uint32_t arena_words_for(uint32_t type) { return ::arena_words_for(type); }
+uint32_t arena_words_for(uint32_t type) { return cdr_arena_words_for(type); }
 
 void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* out, const cdr_kv* kvs,
               const cdr_reset_point* rps) {
@@ -273,160 +258,12 @@ void task_caps(const cdr_event* ev, uint64_t n, uint32_t* xfer, uint32_t* ttask)
   *ttask = t;
 }
 
-// one event (or padding when e == nullptr) into element i of the slab row `row`;
-// attribute records go to the arena at *apos
-void put_event(uint8_t* row, uint32_t i, const cdr_event* ep, bool first, uint64_t* apos_p, uint64_t* arena) {
-  int64_t* eid = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_EVENT_ID));
-  int64_t* ver = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_VERSION));
-  int64_t* ts = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_TIMESTAMP));
-  int64_t* task = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_TASK_ID));
-  int64_t* key = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_KEY));
-  int64_t* aux = reinterpret_cast<int64_t*>(row + cdr_col_off(CDR_COL_AUX));
-  uint32_t* tf = reinterpret_cast<uint32_t*>(row + cdr_col_off(CDR_COL_TYPE_FLAGS));
-  uint32_t* hh = reinterpret_cast<uint32_t*>(row + cdr_col_off(CDR_COL_H));
-  int32_t* nn = reinterpret_cast<int32_t*>(row + cdr_col_off(CDR_COL_N));
-  if (!ep) {
-    tf[i] = CDR_EV_PAD;
-    eid[i] = ver[i] = ts[i] = task[i] = key[i] = aux[i] = 0;
-    hh[i] = 0;
-    nn[i] = 0;
-    return;
-  }
-  uint64_t& apos = *apos_p;
-  {
-    const cdr_event& e = *ep;
-    uint32_t flags = (e.flags & CDR_EVF_BATCH_FIRST) || first ? CDR_SEF_BATCH_FIRST : 0;
-    if (!first) {  // the entry's events are contiguous: ep - 1 is the previous one
-      flags |= (uint64_t)e.event_id == (uint64_t)ep[-1].event_id + 1 ? CDR_SEF_ID_NEXT : 0u;
-      flags |= e.version == ep[-1].version ? CDR_SEF_VER_SAME : 0u;
-    }
-    int64_t kk = 0, ax = 0;
-    uint32_t h = 0;
-    int32_t n = 0;
-    switch (e.type) {
-      case CDR_EV_WF_STARTED:
-        ax = (int64_t)apos;
-        std::memcpy(arena + apos, &e.a.started, sizeof(cdr_attr_wf_started));
-        apos += arena_words_for(e.type);
-        break;
-      case CDR_EV_DT_SCHEDULED:
-        ax = e.a.dt_sched.attempt;
-        n = e.a.dt_sched.start_to_close_s;
-        break;
-      case CDR_EV_DT_STARTED:
-        kk = e.a.dt.scheduled_event_id;
-        h = e.a.dt.request_id;
-        break;
-      case CDR_EV_DT_COMPLETED:
-        kk = e.a.dt.scheduled_event_id;
-        ax = e.a.dt.started_event_id;
-        h = e.a.dt.binary_checksum;
-        break;
-      case CDR_EV_DT_TIMED_OUT:
-        n = e.a.dt.timeout_type;
-        break;
-      case CDR_EV_AT_SCHEDULED: {
-        // the four timeouts travel in the columns (the replay loop never reads the
-        // arena record; only the final emission of a still-pending activity does)
-        const cdr_attr_at_scheduled& a = e.a.at_sched;
-        kk = (int64_t)((uint64_t)a.activity_id | ((uint64_t)(uint32_t)a.stc_s << 32));
-        h = (uint32_t)a.s2c_s;
-        n = a.s2s_s;
-        ax = (int64_t)((apos & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)a.hb_s << 32));
-        std::memcpy(arena + apos, &a, sizeof(cdr_attr_at_scheduled));
-        apos += arena_words_for(e.type);
-        break;
-      }
-      case CDR_EV_AT_STARTED:
-        kk = e.a.at.scheduled_event_id;
-        h = e.a.at.request_id;
-        break;
-      case CDR_EV_AT_COMPLETED:
-      case CDR_EV_AT_FAILED:
-      case CDR_EV_AT_TIMED_OUT:
-      case CDR_EV_AT_CANCELED:
-        kk = e.a.at.scheduled_event_id;
-        break;
-      case CDR_EV_AT_CANCEL_REQUESTED:
-      case CDR_EV_AT_REQ_CANCEL_FAILED:
-        kk = e.a.at.activity_id;
-        break;
-      case CDR_EV_TIMER_STARTED:
-        kk = e.a.timer.timer_id;
-        ax = e.a.timer.start_to_fire_s;
-        break;
-      case CDR_EV_TIMER_FIRED:
-      case CDR_EV_TIMER_CANCELED:
-      case CDR_EV_CANCEL_TIMER_FAILED:
-        kk = e.a.timer.timer_id;
-        break;
-      case CDR_EV_CHILD_INITIATED:
-        kk = e.a.ext.domain | ((uint64_t)(apos & 0xFFFFFFFFull) << 32);
-        std::memcpy(arena + apos, &e.a.ext, sizeof(cdr_attr_external));
-        apos += arena_words_for(e.type);
-        ax = e.a.ext.workflow_type;
-        h = e.a.ext.workflow_id;
-        n = e.a.ext.parent_close_policy;
-        if (e.a.ext.flags & CDR_XF_DOMAIN_MISSING) flags |= CDR_SEF_DOMAIN_MISSING;
-        break;
-      case CDR_EV_RCE_INITIATED:
-        kk = e.a.ext.domain | ((uint64_t)(apos & 0xFFFFFFFFull) << 32);
-        std::memcpy(arena + apos, &e.a.ext, sizeof(cdr_attr_external));
-        apos += arena_words_for(e.type);
-        if (e.a.ext.flags & CDR_XF_DOMAIN_MISSING) flags |= CDR_SEF_DOMAIN_MISSING;
-        break;
-      case CDR_EV_SE_INITIATED:
-        kk = e.a.ext.domain | ((uint64_t)(apos & 0xFFFFFFFFull) << 32);
-        std::memcpy(arena + apos, &e.a.ext, sizeof(cdr_attr_external));
-        apos += arena_words_for(e.type);
-        ax = (int64_t)(((uint64_t)e.a.ext.input << 32) | e.a.ext.control);
-        h = e.a.ext.signal_name;
-        if (e.a.ext.flags & CDR_XF_DOMAIN_MISSING) flags |= CDR_SEF_DOMAIN_MISSING;
-        break;
-      case CDR_EV_CHILD_STARTED:
-        kk = e.a.ref.initiated_event_id;
-        h = e.a.ref.run_id;
-        break;
-      case CDR_EV_CHILD_START_FAILED:
-      case CDR_EV_CHILD_COMPLETED:
-      case CDR_EV_CHILD_FAILED:
-      case CDR_EV_CHILD_CANCELED:
-      case CDR_EV_CHILD_TIMED_OUT:
-      case CDR_EV_CHILD_TERMINATED:
-      case CDR_EV_RCE_FAILED:
-      case CDR_EV_EXT_CANCEL_REQUESTED:
-      case CDR_EV_SE_FAILED:
-      case CDR_EV_EXT_SIGNALED:
-        kk = e.a.ref.initiated_event_id;
-        break;
-      case CDR_EV_UPSERT_SA:
-        ax = e.a.upsert.search_attr_off;
-        h = e.a.upsert.search_attr_len;
-        break;
-      case CDR_EV_WF_CONTINUED_AS_NEW:
-        h = e.a.can.new_execution_run_id;
-        break;
-      default:
-        break;
-    }
-    tf[i] = cdr_type_flags(e.type, flags);
-    eid[i] = e.event_id;
-    ver[i] = e.version;
-    ts[i] = e.timestamp;
-    task[i] = e.task_id;
-    key[i] = kk;
-    aux[i] = ax;
-    hh[i] = h;
-    nn[i] = n;
-  }
-}
-
 void pack_lane(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t len, uint32_t l, uint64_t apos,
                const cdr_slices* o) {
   uint8_t* const blk0 = const_cast<uint8_t*>(o->slab) + row0 * CDR_ROW_BYTES;
   uint64_t* arena = const_cast<uint64_t*>(o->arena);
   for (uint32_t k = 0; k < len; k++)
-    put_event(blk0 + (uint64_t)k * CDR_ROW_BYTES, l, k < n_ev ? ev + k : nullptr, k == 0, &apos, arena);
+    cdr_put_event(blk0 + (uint64_t)k * CDR_ROW_BYTES, l, k < n_ev ? ev + k : nullptr, k == 0, &apos, arena);
 }
 
 // a wave slice: event k of the one workflow in row k/64, lane k%64 (cdr.h)
@@ -435,7 +272,7 @@ void pack_chunked(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t ro
   uint8_t* const blk0 = const_cast<uint8_t*>(o->slab) + row0 * CDR_ROW_BYTES;
   uint64_t* arena = const_cast<uint64_t*>(o->arena);
   for (uint64_t k = 0; k < (uint64_t)rows * CDR_SLICE_WIDTH; k++)
-    put_event(blk0 + (k / CDR_SLICE_WIDTH) * CDR_ROW_BYTES, (uint32_t)(k % CDR_SLICE_WIDTH),
+    cdr_put_event(blk0 + (k / CDR_SLICE_WIDTH) * CDR_ROW_BYTES, (uint32_t)(k % CDR_SLICE_WIDTH),
               k < n_ev ? ev + k : nullptr, k == 0, &apos, arena);
 }
 
@@ -655,7 +492,7 @@ int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n
 
 uint64_t cdr_plan_arena_words(const cdr_batch* b) {
   uint64_t w = 0;
-  for (uint64_t i = 0; i < b->n_events; i++) w += arena_words_for(b->events[i].type);
+  for (uint64_t i = 0; i < b->n_events; i++) w += cdr_arena_words_for(b->events[i].type);
   return w;
 }
 
@@ -666,7 +503,7 @@ int cdr_pack_slices(const cdr_batch* b, cdr_slices* o, int threads) {
   for (uint32_t w = 0; w < b->n_wfs; w++) {
     const cdr_wf_desc& d = b->wfs[w];
     uint64_t words = 0;
-    for (uint64_t k = 0; k < d.ev_len; k++) words += arena_words_for(b->events[d.ev_off + k].type);
+    for (uint64_t k = 0; k < d.ev_len; k++) words += cdr_arena_words_for(b->events[d.ev_off + k].type);
     arena_base[w + 1] = arena_base[w] + words;
   }
   if (arena_base[b->n_wfs] > o->arena_words) return CDR_API_EINVAL;

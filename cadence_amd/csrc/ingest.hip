@@ -927,3 +927,355 @@ extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_inge
   }
   return CDR_API_OK;
 }
+
+// ======================================================================== plan + pack
+// cdr_plan_caps restated per entry on the device (host.cpp caps_one / task_caps): the
+// live sets of the wave kernel's lane tables tracked up to CDR_WAVE_SLOTS + 1 keys (one
+// past any bound a flag tests), the reset-point checksum and search-attribute key lists
+// of the register-table envelope up to CDR_REG_NRP / CDR_REG_NSA + 1.
+#include "pack_event.h"
+
+namespace {
+
+template <int CAP>
+struct Live {
+  int64_t k[CAP];
+  uint32_t n = 0, max = 0;
+  bool over = false;
+  __device__ void add(int64_t key, bool unique) {
+    if (over) return;
+    if (unique)
+      for (uint32_t i = 0; i < n; i++)
+        if (k[i] == key) return;
+    if (n == CAP) {
+      over = true;
+      max = CAP + 1;
+      return;
+    }
+    k[n++] = key;
+    max = n > max ? n : max;
+  }
+  __device__ void del(int64_t key) {
+    if (over) return;
+    for (uint32_t i = 0; i < n; i++)
+      if (k[i] == key) {
+        k[i] = k[--n];
+        return;
+      }
+  }
+  __device__ bool has(int64_t key) const {
+    for (uint32_t i = 0; i < n; i++)
+      if (k[i] == key) return true;
+    return false;
+  }
+  __device__ uint32_t size() const { return over ? CAP + 1 : n; }
+};
+
+__global__ __launch_bounds__(64) void k_caps(const cdr_event* events, const uint64_t* ev_off, const cdr_wf_desc* wfs,
+                                              const cdr_kv* kvs, const cdr_reset_point* rps, uint32_t n_wfs,
+                                              cdr_wf_caps* caps, uint64_t* arena_words) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n_wfs) return;
+  const cdr_event* ev = events + ev_off[w];
+  const uint64_t n = ev_off[w + 1] - ev_off[w];
+  const uint32_t builder = wfs[w].builder;
+  cdr_wf_caps c;
+  {
+    uint64_t* z = reinterpret_cast<uint64_t*>(&c);
+    for (uint32_t i = 0; i < sizeof(cdr_wf_caps) / 8; i++) z[i] = 0;
+  }
+  bool fast = builder != CDR_BUILDER_2DC && n > 0 && ev[0].type == CDR_EV_WF_STARTED;
+  bool have_ver = false;
+  int64_t last_ver = 0;
+  uint32_t vh = 0;
+  int64_t live = 0, live_max = 0;
+  Live<CDR_WAVE_SLOTS + 1> lv0, lv1, lv2, lv3;  // timers (timer id), children, cancels, signals
+  bool reg = n > 0 && n < (1u << 20);
+  int64_t last_id = 0;
+  uint64_t call_start = 0;
+  Live<CDR_REG_NRP + 1> rp_cks;
+  Live<CDR_REG_NSA + 1> sa_keys;
+  uint32_t x = 0, t = 0;  // task bounds
+  uint64_t aw = 0;
+  for (uint64_t k = 0; k < n; k++) {
+    const cdr_event& e = ev[k];
+    const uint32_t type = e.type;
+    if (k == 0 || (e.flags & CDR_EVF_BATCH_FIRST)) call_start = k;
+    reg = reg && e.event_id > last_id && e.event_id < (1ll << 31) && k - call_start < 4096;
+    last_id = e.event_id;
+    if (type == CDR_EV_WF_STARTED) {  // a second Started resets the row lists
+      const cdr_attr_wf_started& a = e.a.started;
+      rp_cks = Live<CDR_REG_NRP + 1>();
+      sa_keys = Live<CDR_REG_NSA + 1>();
+      if (a.flags & CDR_SF_HAS_RESET_POINTS)
+        for (uint32_t q = 0; q < a.reset_points_len; q++) {
+          const cdr_reset_point& p = rps[a.reset_points_off + q];
+          rp_cks.add((p.flags & CDR_RP_HAS_CHECKSUM) ? p.binary_checksum : 0u, false);
+        }
+      if (a.flags & CDR_SF_HAS_SEARCH_ATTR)
+        for (uint32_t q = 0; q < a.search_attr_len; q++) sa_keys.add(kvs[a.search_attr_off + q].key, false);
+    } else if (type == CDR_EV_DT_COMPLETED && e.a.dt.binary_checksum) {
+      rp_cks.add(e.a.dt.binary_checksum, true);
+    } else if (type == CDR_EV_UPSERT_SA) {
+      for (uint32_t q = 0; q < e.a.upsert.search_attr_len && sa_keys.size() <= CDR_REG_NSA; q++)
+        sa_keys.add(kvs[e.a.upsert.search_attr_off + q].key, true);
+    }
+    if (type == CDR_EV_AT_SCHEDULED) {
+      ++live;
+      live_max = live > live_max ? live : live_max;
+    }
+    if (type == CDR_EV_AT_COMPLETED || type == CDR_EV_AT_FAILED || type == CDR_EV_AT_TIMED_OUT ||
+        type == CDR_EV_AT_CANCELED)
+      live = live > 0 ? live - 1 : 0;
+    switch (type) {
+      case CDR_EV_TIMER_STARTED: lv0.add(e.a.timer.timer_id, true); break;
+      case CDR_EV_TIMER_FIRED: case CDR_EV_TIMER_CANCELED: lv0.del(e.a.timer.timer_id); break;
+      case CDR_EV_CHILD_INITIATED: lv1.add(e.event_id, false); break;
+      case CDR_EV_CHILD_START_FAILED: case CDR_EV_CHILD_COMPLETED: case CDR_EV_CHILD_FAILED:
+      case CDR_EV_CHILD_CANCELED: case CDR_EV_CHILD_TIMED_OUT: case CDR_EV_CHILD_TERMINATED:
+        lv1.del(e.a.ref.initiated_event_id);
+        break;
+      case CDR_EV_RCE_INITIATED: lv2.add(e.event_id, false); break;
+      case CDR_EV_RCE_FAILED: case CDR_EV_EXT_CANCEL_REQUESTED: lv2.del(e.a.ref.initiated_event_id); break;
+      case CDR_EV_SE_INITIATED: lv3.add(e.event_id, false); break;
+      case CDR_EV_SE_FAILED: case CDR_EV_EXT_SIGNALED: lv3.del(e.a.ref.initiated_event_id); break;
+      default: break;
+    }
+    fast = fast && type < 64 && (CDR_FAST_TYPES & (1ull << type)) && (k == 0 || type != CDR_EV_WF_STARTED);
+    if (!have_ver || e.version > last_ver) {
+      vh++;
+      last_ver = e.version;
+      have_ver = true;
+    }
+    switch (type) {
+      case CDR_EV_WF_STARTED:
+        c.rp_cap += e.a.started.reset_points_len;
+        c.sa_cap += e.a.started.search_attr_len;
+        x += 1;
+        t += 2;
+        break;
+      case CDR_EV_DT_COMPLETED: if (e.a.dt.binary_checksum) c.rp_cap++; break;
+      case CDR_EV_AT_SCHEDULED: c.act_cap++; break;
+      case CDR_EV_TIMER_STARTED: c.timer_cap++; break;
+      case CDR_EV_CHILD_INITIATED: c.child_cap++; break;
+      case CDR_EV_RCE_INITIATED: c.cancel_cap++; break;
+      case CDR_EV_SE_INITIATED: c.signal_cap++; break;
+      case CDR_EV_UPSERT_SA: c.sa_cap += e.a.upsert.search_attr_len; break;
+      default: break;
+    }
+    switch (type) {  // task_caps (host.cpp): transfer / timer tasks an event can append
+      case CDR_EV_DT_SCHEDULED: case CDR_EV_DT_TIMED_OUT: case CDR_EV_DT_FAILED: case CDR_EV_CHILD_INITIATED:
+      case CDR_EV_RCE_INITIATED: case CDR_EV_SE_INITIATED: case CDR_EV_UPSERT_SA:
+        x += 1;
+        break;
+      case CDR_EV_AT_SCHEDULED: case CDR_EV_WF_COMPLETED: case CDR_EV_WF_FAILED: case CDR_EV_WF_TIMED_OUT:
+      case CDR_EV_WF_CANCELED: case CDR_EV_WF_TERMINATED: case CDR_EV_WF_CONTINUED_AS_NEW:
+        x += 1;
+        t += 1;
+        break;
+      case CDR_EV_DT_STARTED: case CDR_EV_AT_STARTED: case CDR_EV_AT_COMPLETED: case CDR_EV_AT_FAILED:
+      case CDR_EV_AT_TIMED_OUT: case CDR_EV_AT_CANCELED: case CDR_EV_TIMER_STARTED: case CDR_EV_TIMER_FIRED:
+      case CDR_EV_TIMER_CANCELED:
+        t += 1;
+        break;
+      default: break;
+    }
+    aw += cdr_arena_words_for(type);
+  }
+  c.vh_cap = vh;
+  c.act_live = (uint32_t)live_max;
+  c.timer_live = lv0.over ? c.timer_cap : lv0.max;  // past the tracked bound: every TimerStarted
+  c.flags = (fast && live_max <= 1) ? CDR_CAP_FAST : 0u;
+  const uint32_t W = CDR_WAVE_SLOTS;
+  if (!(c.flags & CDR_CAP_FAST) && live_max <= (int64_t)W && lv0.max <= W && lv1.max <= W && lv2.max <= W &&
+      lv3.max <= W)
+    c.flags |= CDR_CAP_WAVE;
+  if ((c.flags & CDR_CAP_WAVE) && live_max <= (int64_t)CDR_LANE_MAX_ACT && lv0.max <= CDR_LANE_MAX_TIMERS &&
+      lv1.max + lv2.max + lv3.max <= CDR_LANE_MAX_EXT && n <= CDR_LANE_MAX_LEN)
+    c.flags |= CDR_CAP_LANE;
+  reg = reg && !(c.flags & CDR_CAP_FAST) && lv0.max <= CDR_REG_NT && lv1.max <= CDR_REG_NX &&
+        lv2.max <= CDR_REG_NX && lv3.max <= CDR_REG_NX && rp_cks.size() <= CDR_REG_NRP &&
+        sa_keys.size() <= CDR_REG_NSA;
+  if (reg && live_max <= (int64_t)CDR_REG_NA) c.flags |= CDR_CAP_REG;
+  else if (reg && live_max <= (int64_t)CDR_REG2_NA) c.flags |= CDR_CAP_REG2;
+  c.xfer_cap = x + 1;  // + refreshTasks' UpsertWorkflowSearchAttributes task
+  c.ttask_cap = t;
+  caps[w] = c;
+  arena_words[w] = aw;
+}
+
+// one thread per lane of a lane slice, one per wave slice (its events in row-major order)
+__global__ __launch_bounds__(64) void k_pack(const cdr_event* events, const cdr_wf_desc* wfs, const uint64_t* abase,
+                                              const int32_t* lane_wf, const uint32_t* slice_len,
+                                              const uint64_t* slice_row0, const uint32_t* slice_flags,
+                                              uint8_t* slab, uint64_t* arena) {
+  const uint32_t s = blockIdx.x, l = threadIdx.x;
+  const uint64_t row0 = slice_row0[s];
+  const uint32_t len = slice_len[s];
+  uint8_t* blk0 = slab + row0 * CDR_ROW_BYTES;
+  if (slice_flags[s] & CDR_SLICE_WAVE) {
+    const int32_t w = lane_wf[(uint64_t)s * CDR_SLICE_WIDTH];
+    const cdr_event* ev = events + wfs[w].ev_off;
+    const uint64_t n = wfs[w].ev_len;
+    // one walk in event order (arena positions are the prefix of the entry's records)
+    if (l == 0) {
+      uint64_t apos = abase[w];
+      for (uint64_t k = 0; k < (uint64_t)len * CDR_SLICE_WIDTH; k++)
+        cdr_put_event(blk0 + (k / CDR_SLICE_WIDTH) * CDR_ROW_BYTES, (uint32_t)(k % CDR_SLICE_WIDTH),
+                      k < n ? ev + k : nullptr, k == 0, &apos, arena);
+    }
+    return;
+  }
+  const int32_t w = lane_wf[(uint64_t)s * CDR_SLICE_WIDTH + l];
+  uint64_t apos = w >= 0 ? abase[w] : 0;
+  const cdr_event* ev = w >= 0 ? events + wfs[w].ev_off : nullptr;
+  const uint64_t n = w >= 0 ? wfs[w].ev_len : 0;
+  for (uint32_t k = 0; k < len; k++)
+    cdr_put_event(blk0 + (uint64_t)k * CDR_ROW_BYTES, l, k < n ? ev + k : nullptr, k == 0, &apos, arena);
+}
+
+}  // namespace
+
+extern "C" int cdr_ingest_plan(cdr_ctx* ctx, const cdr_ingest_out* dec, const cdr_batch* meta, uint32_t plan_mode,
+                               cdr_dev_batch* db, cdr_wf_caps* caps, cdr_totals* totals, void* stream) {
+  if (!ctx || !dec || !meta || !db || !caps || !totals || (meta->n_wfs && !meta->wfs)) return CDR_API_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(cdr_ctx_device(ctx)));
+  const uint32_t n = meta->n_wfs;
+  int rc;
+  // ---- entries with the decode's event ranges
+  std::vector<uint64_t> off(n + 1ull);
+  HIPCHK(hipMemcpyAsync(off.data(), dec->ev_off, (n + 1ull) * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<cdr_wf_desc> wfs(meta->wfs, meta->wfs + n);
+  for (uint32_t w = 0; w < n; w++) {
+    wfs[w].ev_off = off[w];
+    wfs[w].ev_len = off[w + 1] - off[w];
+  }
+  cdr_wf_desc* d_wfs;
+  cdr_wf_caps* d_caps;
+  uint64_t *d_aw, *d_abase;
+  if ((rc = ws(ctx, WS_PL_WFS, n, &d_wfs)) || (rc = ws(ctx, WS_PL_CAPS, n, &d_caps)) ||
+      (rc = ws(ctx, WS_PL_AWORDS, n, &d_aw)) || (rc = ws(ctx, WS_PL_ABASE, n + 1ull, &d_abase)))
+    return rc;
+  if (n) HIPCHK(hipMemcpyAsync(d_wfs, wfs.data(), n * sizeof(cdr_wf_desc), hipMemcpyHostToDevice, st));
+  // ---- capacities and eligibility, one lane per entry
+  if (n)
+    hipLaunchKernelGGL(k_caps, dim3((n + 63) / 64), dim3(64), 0, st, dec->events, dec->ev_off, d_wfs, dec->kvs,
+                       dec->rps, n, d_caps, d_aw);
+  HIPCHK(hipGetLastError());
+  std::vector<uint64_t> aw(n);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(caps, d_caps, n * sizeof(cdr_wf_caps), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(aw.data(), d_aw, n * 8ull, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  // ---- offsets (cdr_plan_caps's running sums) and arena bases, on the host
+  cdr_totals t{};
+  std::vector<uint64_t> abase(n + 1ull, 0);
+  for (uint32_t w = 0; w < n; w++) {
+    cdr_wf_caps& c = caps[w];
+    c.xfer_off = t.xfer;
+    t.xfer += c.xfer_cap;
+    c.ttask_off = t.ttask;
+    t.ttask += c.ttask_cap;
+    c.act_off = t.act;
+    t.act += c.act_cap;
+    c.timer_off = t.timer;
+    t.timer += c.timer_cap;
+    c.child_off = t.child;
+    t.child += c.child_cap;
+    c.cancel_off = t.cancel;
+    t.cancel += c.cancel_cap;
+    c.signal_off = t.signal;
+    t.signal += c.signal_cap;
+    c.vh_off = t.vh;
+    t.vh += c.vh_cap;
+    c.rp_off = t.rp;
+    t.rp += c.rp_cap;
+    c.sa_off = t.sa;
+    t.sa += c.sa_cap;
+    abase[w + 1] = abase[w] + aw[w];
+  }
+  *totals = t;
+  if (abase[n] >= (1ull << 32)) return CDR_API_EINVAL;  // u32 arena offsets (cdr.h)
+  // ---- the slice plan (host, per-entry records only)
+  uint32_t ns = 0, n_wave = 0;
+  uint64_t rows = 0;
+  if ((rc = cdr_plan_slices_ex(wfs.data(), caps, n, plan_mode, nullptr, nullptr, nullptr, nullptr, &ns, &rows,
+                               &n_wave)))
+    return rc;
+  std::vector<int32_t> lane(ns * (size_t)CDR_SLICE_WIDTH);
+  std::vector<uint32_t> slen(ns), sflags(ns), sc_act(ns), sc_tim(ns);
+  std::vector<uint64_t> row0(ns), sc_off(ns);
+  if ((rc = cdr_plan_slices_ex(wfs.data(), caps, n, plan_mode, lane.data(), slen.data(), row0.data(), sflags.data(),
+                               &ns, &rows, &n_wave)))
+    return rc;
+  uint64_t sc_words = 0;
+  uint32_t n_fast = 0;
+  if ((rc = cdr_plan_scratch(caps, lane.data(), ns, sc_off.data(), sc_act.data(), sc_tim.data(), sflags.data(),
+                             &sc_words, &n_fast)))
+    return rc;
+  int32_t* d_lane;
+  uint32_t *d_slen, *d_sflags, *d_scact, *d_sctim;
+  uint64_t *d_row0, *d_scoff, *d_scratch, *d_arena;
+  uint8_t* d_slab;
+  if ((rc = ws(ctx, WS_PL_LANE, lane.size(), &d_lane)) || (rc = ws(ctx, WS_PL_SLEN, ns, &d_slen)) ||
+      (rc = ws(ctx, WS_PL_SFLAGS, ns, &d_sflags)) || (rc = ws(ctx, WS_PL_SCACT, ns, &d_scact)) ||
+      (rc = ws(ctx, WS_PL_SCTIM, ns, &d_sctim)) || (rc = ws(ctx, WS_PL_ROW0, ns, &d_row0)) ||
+      (rc = ws(ctx, WS_PL_SCOFF, ns, &d_scoff)) || (rc = ws(ctx, WS_PL_SCRATCH, sc_words, &d_scratch)) ||
+      (rc = ws(ctx, WS_PL_ARENA, abase[n] + 1, &d_arena)) ||
+      (rc = ws(ctx, WS_PL_SLAB, rows * (uint64_t)CDR_ROW_BYTES, &d_slab)))
+    return rc;
+  auto h2d = [&](void* d, const void* h, uint64_t bytes) -> int {
+    if (bytes) HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
+    return CDR_API_OK;
+  };
+  if ((rc = h2d(d_lane, lane.data(), lane.size() * 4ull)) || (rc = h2d(d_slen, slen.data(), ns * 4ull)) ||
+      (rc = h2d(d_sflags, sflags.data(), ns * 4ull)) || (rc = h2d(d_scact, sc_act.data(), ns * 4ull)) ||
+      (rc = h2d(d_sctim, sc_tim.data(), ns * 4ull)) || (rc = h2d(d_row0, row0.data(), ns * 8ull)) ||
+      (rc = h2d(d_scoff, sc_off.data(), ns * 8ull)) || (rc = h2d(d_abase, abase.data(), (n + 1ull) * 8)) ||
+      (rc = h2d(d_caps, caps, n * sizeof(cdr_wf_caps))))
+    return rc;
+  HIPCHK(hipMemsetAsync(d_scratch, 0, sc_words * 8 + 8, st));
+  // ---- the slab and the arena, on the device
+  if (ns)
+    hipLaunchKernelGGL(k_pack, dim3(ns), dim3(CDR_SLICE_WIDTH), 0, st, dec->events, d_wfs, d_abase, d_lane, d_slen,
+                       d_row0, d_sflags, d_slab, d_arena);
+  HIPCHK(hipGetLastError());
+  cdr_dev_batch b{};
+  b.ev.n_slices = ns;
+  b.ev.n_rows = rows;
+  b.ev.arena_words = abase[n];
+  b.ev.slice_row0 = d_row0;
+  b.ev.slice_len = d_slen;
+  b.ev.lane_wf = d_lane;
+  b.ev.slab = d_slab;
+  b.ev.arena = d_arena;
+  b.ev.slice_scratch_off = d_scoff;
+  b.ev.slice_act_slots = d_scact;
+  b.ev.slice_tim_slots = d_sctim;
+  b.ev.slice_flags = d_sflags;
+  b.scratch = d_scratch;
+  b.wfs = d_wfs;
+  b.caps = d_caps;
+  b.kvs = dec->kvs;
+  b.rps = dec->rps;
+  b.n_wfs = n;
+  b.empty_uuid = meta->empty_uuid;
+  for (uint32_t i = 0; i < ns; i++) {
+    b.max_act_slots = sc_act[i] > b.max_act_slots ? sc_act[i] : b.max_act_slots;
+    b.max_tim_slots = sc_tim[i] > b.max_tim_slots ? sc_tim[i] : b.max_tim_slots;
+    b.n_reg_slices += (sflags[i] & CDR_SLICE_REG) ? 1u : 0u;
+    b.n_reg2_slices += (sflags[i] & CDR_SLICE_REG2) ? 1u : 0u;
+  }
+  b.n_fast_slices = n_fast;
+  b.n_wave_slices = n_wave;
+  b.cluster = meta->cluster;
+  b.now_ns = meta->now_ns;
+  b.uuid_seed = meta->uuid_seed;
+  b.carry = nullptr;
+  *db = b;
+  HIPCHK(hipStreamSynchronize(st));
+  return CDR_API_OK;
+}

@@ -105,6 +105,7 @@ class Decoded:
     entry_status: np.ndarray
     strings: list
     n_bad_blobs: int
+    raw: object = None  # the cdr_ingest_out (device pointers, valid until the context's next ingest)
 
 
 def decode(eng: engine.Engine, enc: Encoded) -> Decoded:
@@ -164,7 +165,7 @@ def decode(eng: engine.Engine, enc: Encoded) -> Decoded:
         events = events if out.n_events else (abi.CdrEvent * 0)()
         kvs = kvs if out.n_kvs else (abi.CdrKV * 0)()
         rps = rps if out.n_rps else (abi.CdrResetPoint * 0)()
-        return Decoded(events, kvs, rps, ev_off, bst, est, strings, out.n_bad_blobs)
+        return Decoded(events, kvs, rps, ev_off, bst, est, strings, out.n_bad_blobs, out)
     finally:
         for p in ptrs:
             hip.hipFree(p)
@@ -185,3 +186,49 @@ def to_batch(src: engine.Batch, enc: Encoded, dec: Decoded) -> engine.Batch:
     strings = [s.decode("latin-1") for s in dec.strings]
     return engine.Batch(events=dec.events, wfs=wfs, kvs=dec.kvs, rps=dec.rps, cluster=src.cluster,
                         now_ns=src.now_ns, uuid_seed=src.uuid_seed, empty_uuid=1, strings=strings)
+
+
+def replay_on_device(eng: engine.Engine, src: engine.Batch, enc: Encoded, dec: Decoded,
+                     plan_mode: int = abi.PLAN_WAVE) -> engine.Outputs:
+    """cdr_ingest_plan (device caps + host slice plan + device pack) on the decode still
+    resident in the context, then cdr_replay_sliced_async; host copies of the outputs
+    (an engine.Outputs whose plan is the device-computed capacities)."""
+    hip = engine._hip()
+    L = abi.lib()
+    meta = to_batch(src, enc, dec)
+    mb = meta.cstruct()
+    n = src.n_wfs
+    caps = (abi.CdrWfCaps * max(1, n))()
+    tot = abi.CdrTotals()
+    db = abi.CdrDevBatch()
+    rc = L.cdr_ingest_plan(eng.ctx, C.byref(dec.raw), C.byref(mb), plan_mode, C.byref(db), caps, C.byref(tot), None)
+    if rc:
+        raise RuntimeError(f"cdr_ingest_plan rc={rc}")
+    pl = engine.Plan(caps, tot)
+    out = engine.Outputs(meta, pl)
+    ptrs = []
+
+    def dz(nbytes):
+        p = C.c_void_p()
+        assert hip.hipMalloc(C.byref(p), C.c_size_t(max(8, nbytes))) == 0
+        ptrs.append(p)
+        hip.hipMemset(p, 0, C.c_size_t(max(8, nbytes)))
+        return p.value
+    try:
+        dev = abi.CdrOut()
+        host = out.cstruct()
+        sizes = {"result": C.sizeof(out.result), "exec": C.sizeof(out.exec), "repl": C.sizeof(out.repl),
+                 "last_decision": C.sizeof(out.last_decision)}
+        for t in engine.TABLES:
+            sizes[t] = C.sizeof(out.tables[t])
+        for k, nb in sizes.items():
+            setattr(dev, k, dz(nb))
+        rc = L.cdr_replay_sliced_async(eng.ctx, C.byref(db), C.byref(dev), None)
+        if rc:
+            raise RuntimeError(f"cdr_replay_sliced_async rc={rc}")
+        for k, nb in sizes.items():
+            assert hip.hipMemcpy(C.c_void_p(getattr(host, k)), C.c_void_p(getattr(dev, k)), C.c_size_t(nb), 2) == 0
+        return out
+    finally:
+        for p in ptrs:
+            hip.hipFree(p)

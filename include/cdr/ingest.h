@@ -92,6 +92,21 @@ typedef struct cdr_ingest_out { /* device buffers owned by the context, valid un
  * size the outputs).  `out` receives device pointers into the context's workspace. */
 int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_ingest_out* out, void* stream);
 
+/* Plan and pack a decoded batch for the replay, on the device: each entry's capacities
+ * and kernel eligibility (cdr_plan_caps restated, one lane per entry: k_caps), the slice
+ * plan on the host from those per-entry records alone (cdr_plan_slices_ex,
+ * cdr_plan_scratch), then the SELL-64 slab and attribute arena (k_pack, the packer's
+ * cdr_put_event per cell).  `meta` gives the entries (meta->wfs[w], n_wfs = the decode's
+ * entries; ev_off / ev_len are taken from the decode), cluster, now_ns, uuid_seed and
+ * empty_uuid; its events / kvs / rps are not read.  Fills *db with device pointers into
+ * the context's workspace (valid until its next ingest) and the host arrays caps[n_wfs]
+ * (offsets set) and *totals, which size the replay's outputs.  Entries whose decode
+ * failed replay as empty histories (CDR_E_HISTORY_EMPTY): check entry_status.  Not
+ * restated from the host planner: the continue-as-new run-id check and the
+ * CDR_LANE_MAX tuning override.  Synchronous on `stream`. */
+int cdr_ingest_plan(cdr_ctx* ctx, const cdr_ingest_out* dec, const cdr_batch* meta, uint32_t plan_mode,
+                    cdr_dev_batch* db, cdr_wf_caps* caps, cdr_totals* totals, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
