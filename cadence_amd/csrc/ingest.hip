@@ -83,13 +83,39 @@ __device__ uint32_t tab_lookup(const STab& T, uint64_t h) {
   return 0;  // not interned (cannot happen after pass 2)
 }
 
-__device__ uint64_t hash_bytes(const uint8_t* p, uint64_t n) { return cdr_str_hash(p, n); }
-
 // ---------------------------------------------------------------- reader
+// Bytes come through a 16-byte aligned window held in registers (one global_load_dwordx4
+// per 16 bytes instead of a load per byte); the last 16 bytes of the buffer, which an
+// aligned window could overrun, are read byte by byte.
 struct Rd {
   const uint8_t* b;  // blob_bytes
   uint64_t pos, end;
+  uint64_t total;    // bytes in blob_bytes
+  uint64_t wb;       // window address (16-aligned), ~0 = empty
+  uint64_t w0, w1;
   int32_t err;
+  __device__ void init(const uint8_t* base, uint64_t p, uint64_t e, uint64_t t) {
+    b = base;
+    pos = p;
+    end = e;
+    total = t;
+    wb = ~0ull;
+    err = CDR_DEC_OK;
+  }
+  __device__ uint32_t at(uint64_t p) {
+    // the window is aligned in the address space (the buffer itself need not be)
+    const uint64_t addr = (uint64_t)(uintptr_t)(b + p), a = addr & ~15ull;
+    if (a != wb) {
+      const uint64_t lo = (uint64_t)(uintptr_t)b;
+      if (a < lo || a + 16 > lo + total) return b[p];
+      const uint4 v = *reinterpret_cast<const uint4*>((uintptr_t)a);
+      w0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
+      w1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
+      wb = a;
+    }
+    const uint32_t o = (uint32_t)(addr - a);
+    return (uint32_t)(((o < 8) ? (w0 >> (8 * o)) : (w1 >> (8 * (o - 8)))) & 0xFFu);
+  }
   __device__ bool ok() const { return err == CDR_DEC_OK; }
   __device__ bool need(uint64_t n) {
     if (err) return false;
@@ -102,17 +128,17 @@ struct Rd {
   }
   __device__ uint32_t u8() {
     if (!need(1)) return 0;
-    return b[pos++];
+    return at(pos++);
   }
   __device__ uint32_t be16() {
     if (!need(2)) return 0;
-    const uint32_t v = ((uint32_t)b[pos] << 8) | b[pos + 1];
+    const uint32_t v = (at(pos) << 8) | at(pos + 1);
     pos += 2;
     return v;
   }
   __device__ uint32_t be32() {
     if (!need(4)) return 0;
-    const uint32_t v = ((uint32_t)b[pos] << 24) | ((uint32_t)b[pos + 1] << 16) | ((uint32_t)b[pos + 2] << 8) | b[pos + 3];
+    const uint32_t v = (at(pos) << 24) | (at(pos + 1) << 16) | (at(pos + 2) << 8) | at(pos + 3);
     pos += 4;
     return v;
   }
@@ -124,6 +150,13 @@ struct Rd {
     const int32_t n = (int32_t)be32();
     if (n < 0 && !err) err = CDR_DEC_BAD_SIZE;
     return n < 0 ? 0 : n;
+  }
+  // cdr_str_hash of bytes [p, p + n), through the window
+  __device__ uint64_t hash(uint64_t p, uint64_t n) {
+    uint64_t h = 0xCBF29CE484222325ull;
+    for (uint64_t i = 0; i < n; i++) h = (h ^ at(p + i)) * 0x100000001B3ull;
+    h = cdr_mix64(h ^ (n * 0x9E3779B97F4A7C15ull));
+    return h ? h : 1u;
   }
 };
 
@@ -204,11 +237,13 @@ enum Pass { COUNT = 0, INTERN = 1, FILL = 2 };
 struct Ctx {  // per launch
   const uint8_t* bytes;
   const uint64_t* blob_off;
+  uint64_t total;  // bytes in `bytes`
   STab T;
   const uint32_t* dom_id;  // [n_seeds]: ID handle of a domain name seed, UNASSIGNED otherwise
   uint32_t n_seeds;
   // pass outputs
   uint32_t* counts;   // COUNT: [4 * n_blobs] events, kvs, rps, strings
+  unsigned long long* totals;  // COUNT: string fields, failed blobs
   const uint64_t* bases;  // FILL: [3 * n_blobs] event, kv, rp bases
   int32_t* status;
   cdr_event* events;
@@ -224,10 +259,7 @@ struct Blob {
   uint64_t ev0 = 0, kv0 = 0, rp0 = 0;
 
   __device__ Blob(const Ctx& c, uint32_t b) : C(c) {
-    r.b = c.bytes;
-    r.pos = c.blob_off[b];
-    r.end = c.blob_off[b + 1];
-    r.err = CDR_DEC_OK;
+    r.init(c.bytes, c.blob_off[b], c.blob_off[b + 1], c.total);
     if (P == FILL) {
       ev0 = c.bases[3ull * b];
       kv0 = c.bases[3ull * b + 1];
@@ -244,7 +276,7 @@ struct Blob {
     if (n == 0) return 0;
     n_str++;
     if (P == COUNT) return 0;
-    const uint64_t h = hash_bytes(r.b + at, n);
+    const uint64_t h = r.hash(at, n);
     if (P == INTERN) {
       tab_insert(C.T, h, at, n, UNASSIGNED);
       return 0;
@@ -259,7 +291,7 @@ struct Blob {
     const uint32_t n = (uint32_t)(r.pos - at);
     n_str++;
     if (P == COUNT) return 0;
-    const uint64_t h = hash_bytes(r.b + at, n);
+    const uint64_t h = r.hash(at, n);
     if (P == INTERN) {
       tab_insert(C.T, h, at, n, UNASSIGNED);
       return 0;
@@ -691,16 +723,30 @@ struct Blob {
 template <int P>
 __global__ __launch_bounds__(256) void k_blob(Ctx C, uint32_t n_blobs) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n_blobs) return;
-  if (P != COUNT && C.status[b] != CDR_DEC_OK) return;  // a failed blob contributes nothing
-  Blob<P> x(C, b);
-  x.run();
-  if (P == COUNT) {
-    C.counts[4ull * b] = x.r.ok() ? x.n_ev : 0u;
-    C.counts[4ull * b + 1] = x.r.ok() ? x.n_kv : 0u;
-    C.counts[4ull * b + 2] = x.r.ok() ? x.n_rp : 0u;
-    C.counts[4ull * b + 3] = x.n_str;
-    C.status[b] = x.r.err;
+  uint64_t n_str = 0;
+  uint32_t bad = 0;
+  if (b < n_blobs && (P == COUNT || C.status[b] == CDR_DEC_OK)) {  // a failed blob contributes nothing
+    Blob<P> x(C, b);
+    x.run();
+    if (P == COUNT) {
+      C.counts[4ull * b] = x.r.ok() ? x.n_ev : 0u;
+      C.counts[4ull * b + 1] = x.r.ok() ? x.n_kv : 0u;
+      C.counts[4ull * b + 2] = x.r.ok() ? x.n_rp : 0u;
+      C.counts[4ull * b + 3] = x.n_str;
+      C.status[b] = x.r.err;
+      n_str = x.n_str;
+      bad = x.r.ok() ? 0u : 1u;
+    }
+  }
+  if (P == COUNT) {  // totals: string fields (the table's size) and failed blobs, one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) {
+      n_str += __shfl_down(n_str, o, 64);
+      bad += __shfl_down(bad, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      if (n_str) atomicAdd(C.totals, (unsigned long long)n_str);
+      if (bad) atomicAdd(C.totals + 1, (unsigned long long)bad);
+    }
   }
 }
 
@@ -803,22 +849,28 @@ extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_inge
   Ctx C{};
   C.bytes = in->blob_bytes;
   C.blob_off = in->blob_off;
+  if (nb) {
+    HIPCHK(hipMemcpyAsync(&C.total, in->blob_off + nb, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   C.counts = counts;
   C.status = status;
   C.n_seeds = in->n_seeds;
   const dim3 blk(256);
   auto grid = [](uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); };
   // ---- pass 1: counts
+  // misc (u32 words): [0] table overflow, [1] new strings; u64 words 2-3: string fields, failed blobs
+  uint64_t* tot2 = reinterpret_cast<uint64_t*>(misc) + 2;
+  HIPCHK(hipMemsetAsync(misc, 0, 64, st));
+  C.totals = reinterpret_cast<unsigned long long*>(tot2);
   if (nb) hipLaunchKernelGGL(k_blob<COUNT>, grid(nb), blk, 0, st, C, nb);
   HIPCHK(hipGetLastError());
   // string fields -> table capacity (2x, power of two)
-  uint64_t n_str_fields = 0;
-  {
-    std::vector<uint32_t> h(4ull * nb);
-    if (nb) HIPCHK(hipMemcpyAsync(h.data(), counts, 4ull * nb * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    for (uint32_t b = 0; b < nb; b++) n_str_fields += h[4ull * b + 3];
-  }
+  uint64_t htot[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(htot, tot2, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t n_str_fields = htot[0];
+  out->n_bad_blobs = (uint32_t)htot[1];
   uint64_t cap = 1024;
   while (cap < 2 * (n_str_fields + in->n_seeds)) cap <<= 1;
   STab T{};
@@ -828,7 +880,6 @@ extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_inge
     return rc;
   T.overflow = misc;
   HIPCHK(hipMemsetAsync(T.key, 0, cap * 8, st));
-  HIPCHK(hipMemsetAsync(misc, 0, 64, st));
   C.T = T;
   // ---- pass 2: seeds, then every string of the blobs; rank the new ones by hash
   hipLaunchKernelGGL(k_seed, grid(in->n_seeds), blk, 0, st, T, in->seed_bytes, in->seed_off, in->n_seeds);
@@ -918,13 +969,7 @@ extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_inge
   out->n_events = tot[0];
   out->n_kvs = tot[1];
   out->n_rps = tot[2];
-  // bad blobs
-  {
-    std::vector<int32_t> h(nb);
-    if (nb) HIPCHK(hipMemcpyAsync(h.data(), status, nb * 4ull, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    for (uint32_t b = 0; b < nb; b++) out->n_bad_blobs += h[b] != CDR_DEC_OK;
-  }
+  HIPCHK(hipStreamSynchronize(st));
   return CDR_API_OK;
 }
 
