@@ -238,6 +238,7 @@ CAP_FAST = 0x1
 CAP_WAVE = 0x2
 PLAN_WAVE = 0x1
 PLAN_WAVE_ALL = 0x2  # with PLAN_WAVE: lane-friendly (CAP_LANE) entries on the wave kernel too
+PLAN_NO_LONG = 0x4  # with PLAN_WAVE: keep long lane-capable histories in lane slices (CDR_PLAN_NO_LONG)
 CAP_LANE = 0x4
 CAP_REG = 0x8
 CAP_REG2 = 0x10

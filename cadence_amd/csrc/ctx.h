@@ -61,10 +61,11 @@ struct cdr_ctx {
   // optional per-launch timing ring (bench): event pairs around every replay kernel
   std::vector<hipEvent_t> ring;
   uint32_t ring_used = 0;
-  // side stream for the wave kernel: its scalar-unit-bound waves co-run with the
-  // VALU-bound lane kernels instead of after them (fork/join by events)
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  // side streams for the wave kernel and the 12-activity register kernel: their
+  // waves (the longest histories; scalar-unit-bound / single-wave-per-SIMD) co-run with
+  // the main lane kernels instead of after them (fork/join by events)
+  hipStream_t side = nullptr, side2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
   int concurrent = 1;
   // grow-only device workspace of the host-buffer calls
   void* ws[WS_NUM] = {};

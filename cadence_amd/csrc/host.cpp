@@ -360,9 +360,29 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   if ((mode & CDR_PLAN_WAVE) && !caps && n_wfs) return CDR_API_EINVAL;
   std::vector<uint32_t> lanes, waves;
   lanes.reserve(n_wfs);
+  // long histories: a lane slice advances one event per step, so a history much longer
+  // than the batch's lane work per resident wave (its steps / CDR_LANE_RESIDENT) sets
+  // the lane kernels' critical path alone; on a wave of its own it replays ~10x faster
+  // per event and co-runs with the lane slices (replay.hip, side stream)
+  uint64_t long_thr = UINT64_MAX;
+  if ((mode & CDR_PLAN_WAVE) && !(mode & CDR_PLAN_NO_LONG)) {
+    static const uint32_t* lp = [] {
+      static uint32_t v[2] = {CDR_LONG_MIN, CDR_LONG_FACTOR};
+      if (const char* e = std::getenv("CDR_LONG"))  // tuning override "min,factor"
+        std::sscanf(e, "%u,%u", &v[0], &v[1]);
+      return v;
+    }();
+    uint64_t lane_ev = 0;
+    for (uint32_t w = 0; w < n_wfs; w++)
+      if (!(caps[w].flags & CDR_CAP_WAVE) || (caps[w].flags & (CDR_CAP_LANE | CDR_CAP_REG | CDR_CAP_REG2)))
+        lane_ev += wfs[w].ev_len;
+    const uint64_t per_slot = lane_ev / ((uint64_t)CDR_SLICE_WIDTH * CDR_LANE_RESIDENT);
+    long_thr = std::max<uint64_t>(lp[0], (uint64_t)lp[1] * per_slot);
+  }
   for (uint32_t w = 0; w < n_wfs; w++)
     ((mode & CDR_PLAN_WAVE) && (caps[w].flags & CDR_CAP_WAVE) &&
-             ((mode & CDR_PLAN_WAVE_ALL) || !(caps[w].flags & (CDR_CAP_LANE | CDR_CAP_REG | CDR_CAP_REG2)))
+             ((mode & CDR_PLAN_WAVE_ALL) || !(caps[w].flags & (CDR_CAP_LANE | CDR_CAP_REG | CDR_CAP_REG2)) ||
+              (uint64_t)wfs[w].ev_len > long_thr)
          ? waves
          : lanes)
         .push_back(w);

@@ -1784,7 +1784,7 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
   cdr_opts o;
   cdr_opts_default(&o);
   if (opts) o = *opts;
-  if (o.plan_mode & ~(uint32_t)(CDR_PLAN_WAVE | CDR_PLAN_WAVE_ALL)) return nullptr;
+  if (o.plan_mode & ~(uint32_t)(CDR_PLAN_WAVE | CDR_PLAN_WAVE_ALL | CDR_PLAN_NO_LONG)) return nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return nullptr;
   if (hipSetDevice(device) != hipSuccess) return nullptr;
@@ -1800,8 +1800,10 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
     }
   c->timed = false;
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join2, hipEventDisableTiming) != hipSuccess)
     c->concurrent = 0;
   if (const char* e = std::getenv("CDR_SERIAL_KERNELS")) c->concurrent = c->concurrent && e[0] == '0';
   c->concurrent = c->concurrent && o.concurrent;
@@ -1827,7 +1829,7 @@ int cdr_set_reg_path(cdr_ctx* c, int enable) {
 }
 
 int cdr_set_plan_mode(cdr_ctx* c, uint32_t mode) {
-  if (!c || (mode & ~(uint32_t)(CDR_PLAN_WAVE | CDR_PLAN_WAVE_ALL))) return CDR_API_EINVAL;
+  if (!c || (mode & ~(uint32_t)(CDR_PLAN_WAVE | CDR_PLAN_WAVE_ALL | CDR_PLAN_NO_LONG))) return CDR_API_EINVAL;
   const uint32_t old = c->plan_mode;
   c->plan_mode = mode;
   return (int)old;
@@ -1840,8 +1842,10 @@ void cdr_destroy(cdr_ctx* c) {
   for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
   for (hipEvent_t e : c->ring) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->side2) (void)hipStreamDestroy(c->side2);
   if (c->fork) (void)hipEventDestroy(c->fork);
   if (c->join) (void)hipEventDestroy(c->join);
+  if (c->join2) (void)hipEventDestroy(c->join2);
   if (hipSetDevice(c->device) == hipSuccess)
     for (void* p : c->ws) (void)hipFree(p);
   delete c;
@@ -1873,32 +1877,37 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
   cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u};
+  // kernel streams: the wave kernel (the batch's longest histories, one wave each,
+  // scalar-unit-bound) and the 12-activity register kernel (one wave per SIMD) go
+  // first, each on a side stream, so that their long slices start at once and co-run
+  // with the main-stream lane kernels (fast / register / general) instead of after them
+  const bool reg1 = blocks && reg && in->n_reg_slices;
+  const bool reg2 = blocks && reg && in->n_reg2_slices;
+  const bool main_work = (blocks && fast) || reg1 || (blocks && general);
+  const bool fork_w = c->concurrent && blocks && wave && (main_work || reg2);
+  const bool fork_r2 = c->concurrent && reg2 && (main_work || (blocks && wave));
+  if (fork_w || fork_r2) {
+    HIPCHK(hipEventRecord(c->fork, st));
+    if (fork_w) HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
+    if (fork_r2) HIPCHK(hipStreamWaitEvent(c->side2, c->fork, 0));
+  }
+  if (blocks && wave) hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, fork_w ? c->side : st, L);
+  HIPCHK(hipGetLastError());
+  if (fork_w) HIPCHK(hipEventRecord(c->join, c->side));
+  if (reg2) {
+    typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
+    hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), dim3(blocks),
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, fork_r2 ? c->side2 : st, L);
+  }
+  HIPCHK(hipGetLastError());
+  if (fork_r2) HIPCHK(hipEventRecord(c->join2, c->side2));
   if (blocks && fast)
     hipLaunchKernelGGL(k_replay_fast, dim3(blocks), dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, st, L);
   HIPCHK(hipGetLastError());
-  if (blocks && reg && in->n_reg_slices) {
+  if (reg1) {
     typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
     hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), dim3(blocks),
                        dim3(CDR_SLICE_WIDTH), LY::bytes, st, L);
-  }
-  HIPCHK(hipGetLastError());
-  if (blocks && reg && in->n_reg2_slices) {
-    typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
-    hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), dim3(blocks),
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, st, L);
-  }
-  HIPCHK(hipGetLastError());
-  // the wave kernel on the side stream when lane slices also run: both kernels' waves
-  // share the CUs (wave slices: scalar unit; lane slices: VALU)
-  const bool fork = c->concurrent && blocks && wave && general;
-  if (fork) {
-    HIPCHK(hipEventRecord(c->fork, st));
-    HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
-    hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, c->side, L);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->join, c->side));
-  } else if (blocks && wave) {
-    hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
   }
   HIPCHK(hipGetLastError());
   if (blocks && general) {
@@ -1915,7 +1924,8 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       hipLaunchKernelGGL((k_replay<false, false>), dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
   }
   HIPCHK(hipGetLastError());
-  if (fork) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
+  if (fork_w) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
+  if (fork_r2) HIPCHK(hipStreamWaitEvent(st, c->join2, 0));
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used + 1] : c->ev[1], st));
   if (ring) {
     // keep ev[0..1] meaningful for cdr_last_kernel_ms as well

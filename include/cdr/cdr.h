@@ -248,6 +248,14 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
 /* with CDR_PLAN_WAVE: also the CDR_CAP_LANE entries get wave slices (by default they
  * stay in lane slices, where they replay cheaper) */
 #define CDR_PLAN_WAVE_ALL 0x2u
+/* with CDR_PLAN_WAVE the planner also gives a wave slice to every CDR_CAP_WAVE entry
+ * whose history is longer than max(CDR_LONG_MIN, CDR_LONG_FACTOR x the lane events per
+ * resident lane slot, i.e. lane events / (64 x CDR_LANE_RESIDENT)): such a history
+ * alone would set the lane kernels' critical path.  This bit turns that rule off. */
+#define CDR_PLAN_NO_LONG 0x4u
+#define CDR_LONG_MIN 1024u
+#define CDR_LONG_FACTOR 2u
+#define CDR_LANE_RESIDENT 2048u
 int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
                        int32_t* lane_wf, uint32_t* slice_len, uint64_t* slice_row0, uint32_t* slice_flags,
                        uint32_t* n_slices, uint64_t* n_rows, uint32_t* n_wave);

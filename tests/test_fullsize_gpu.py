@@ -50,6 +50,7 @@ def _gpu_digests(ctx, cfg, index_map, seed, plan_mode, reg):
     (3, abi.PLAN_WAVE, True),
     (3, abi.PLAN_WAVE | abi.PLAN_WAVE_ALL, True),
     (4, abi.PLAN_WAVE, True),
+    (4, abi.PLAN_WAVE | abi.PLAN_NO_LONG, True),  # long histories kept in register-table lane slices
     (5, abi.PLAN_WAVE, True),
     (5, abi.PLAN_WAVE, False),  # register-table slices on the general kernel
 ])
@@ -71,3 +72,5 @@ def test_fullsize_entry_digests(engine_gpu, cfg, plan_mode, reg):
         assert kinds["reg"] > 0, kinds
     if cfg in (4, 5) and not plan_mode & abi.PLAN_WAVE_ALL:
         assert kinds["reg2"] > 0, kinds
+    if cfg in (4, 5) and plan_mode == abi.PLAN_WAVE:  # the long-history rule (cdr.h CDR_PLAN_NO_LONG)
+        assert kinds["wave"] > 0, kinds

@@ -241,3 +241,21 @@ def test_lane_friendly_entries_stay_in_lane_slices():
     keep = [w for w in range(b.n_wfs) if (pl.caps[w].flags & abi.CAP_WAVE) and
             (pl.caps[w].flags & (abi.CAP_LANE | abi.CAP_REG | abi.CAP_REG2))]
     assert n_def == n_all - len(keep)
+
+
+def test_long_histories_get_wave_slices():
+    """CDR_PLAN_WAVE's long-history rule (cdr.h CDR_PLAN_NO_LONG): a lane-capable history
+    longer than max(CDR_LONG_MIN, CDR_LONG_FACTOR x lane events per resident slot) gets a
+    wave slice of its own; CDR_PLAN_NO_LONG keeps it in a lane slice."""
+    b = engine.synth_batch(4, 3000, seed=13)
+    pl = engine.plan(b)
+    lanecap = abi.CAP_LANE | abi.CAP_REG | abi.CAP_REG2
+    flags = [pl.caps[w].flags for w in range(b.n_wfs)]
+    lens = [int(b.wfs[w].ev_len) for w in range(b.n_wfs)]
+    lane_ev = sum(n for f, n in zip(flags, lens) if not (f & abi.CAP_WAVE) or (f & lanecap))
+    thr = max(1024, 2 * (lane_ev // (64 * 2048)))
+    divergent = sum(1 for f in flags if (f & abi.CAP_WAVE) and not (f & lanecap))
+    long_ = sum(1 for f, n in zip(flags, lens) if (f & abi.CAP_WAVE) and (f & lanecap) and n > thr)
+    assert long_ > 0
+    assert engine.slice_kinds(b, pl, abi.PLAN_WAVE)[1] == divergent + long_
+    assert engine.slice_kinds(b, pl, abi.PLAN_WAVE | abi.PLAN_NO_LONG)[1] == divergent

@@ -15,6 +15,6 @@ wait
 for spec in "$@"; do
   name=${spec%%:*}
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$ROOT/variants/libcdr_$name.so" \
-      "$ROOT/variants/replay_$name.o" "$OBJ/api.o" "$OBJ/host.o" "$OBJ/synth.o" -lpthread
+      "$ROOT/variants/replay_$name.o" $(ls "$OBJ"/*.o | grep -v '/replay\.o$') -lpthread
   echo "built variants/libcdr_$name.so"
 done
