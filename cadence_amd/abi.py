@@ -243,6 +243,15 @@ CAP_LANE = 0x4
 CAP_REG = 0x8
 CAP_REG2 = 0x10
 
+# variable-size row blobs (cdr.h cdr_encode_blobs_async)
+CdrStrtab = _S("cdr_strtab", [("bytes", C.c_void_p), ("off", C.c_void_p), ("n", u32), ("_pad", u32)])
+CdrExecPersist = _S("cdr_exec_persist", [
+    ("start_version", i64), ("current_version", i64), ("start_time", i64), ("last_updated_time", i64),
+    ("history_size", i64), ("sticky_s2s_timeout", i64), ("execution_context", u32), ("sticky_task_list", u32),
+    ("client_library_version", u32), ("client_feature_version", u32), ("client_impl", u32), ("_pad", u32)])
+ZERO_TIME_NANOS = -6795364578871345152
+BLOB_STATUS = {0: "OK", 1: "E_UUID", 2: "E_HANDLE", 3: "E_MEMO"}
+
 # slice-major slab of event columns (cdr.h enum cdr_col): name, dtype, in order
 SLAB_COLS = (("event_id", np.int64), ("version", np.int64), ("timestamp", np.int64), ("task_id", np.int64),
              ("key", np.int64), ("aux", np.int64), ("type_flags", np.uint32), ("h", np.uint32), ("n", np.int32))
@@ -326,6 +335,9 @@ EXPORTS = {
                                 C.POINTER(CdrOut), u32, C.c_void_p]),
     "cdr_encode_rows_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
                                     C.c_void_p]),
+    "cdr_encode_blobs_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut),
+                                     C.POINTER(CdrStrtab), C.c_void_p, C.c_void_p, u64, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p]),
     "cdr_compact_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
                                 C.c_void_p, C.c_void_p]),
     "cdr_checksum_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p, C.c_void_p]),

@@ -30,6 +30,8 @@ enum cdr_ws_slot {
   // cdr_ingest_plan (ingest.hip)
   WS_PL_CAPS, WS_PL_AWORDS, WS_PL_ABASE, WS_PL_WFS, WS_PL_LANE, WS_PL_SLEN, WS_PL_ROW0, WS_PL_SFLAGS, WS_PL_SCOFF,
   WS_PL_SCACT, WS_PL_SCTIM, WS_PL_SCRATCH, WS_PL_SLAB, WS_PL_ARENA,
+  // cdr_encode_blobs_async (encode_var.hip)
+  WS_ENC_SIZES, WS_ENC_TMP,
   WS_NUM
 };
 

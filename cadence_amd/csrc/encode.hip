@@ -8,7 +8,8 @@
 //   big-endian length + bytes; the struct ends with a 0 stop byte (blob.go:61-73,
 //   go.uber.org/thriftrw protocol.Binary; pinned by common/codec/version0Thriftrw_test.go
 //   :42-64 through oracle/thrift_binary.py).
-// One wavefront per entry, one lane per row, 16-B aligned stores into fixed-stride slots;
+// One thread per entry (its lane writes the entry's rows one after another), 16-B aligned
+// stores into fixed-stride slots;
 // HBM-bound byte work: a TimerInfo row is 40 B in, 45 B out; a RequestCancelInfo row
 // 40 B in, 66 B out.
 #include <hip/hip_runtime.h>
@@ -58,9 +59,9 @@ __device__ __forceinline__ uint8_t cancel_byte(const cdr_cancel_info& x, uint32_
   return (uint8_t)(nib < 10 ? '0' + nib : 'a' + nib - 10);
 }
 
-// one wavefront per entry, one lane per row: the blob is assembled in registers (the
-// byte loop unrolls to constant positions) and written with aligned 16-B stores into its
-// CDR_BLOB_*_STRIDE slot
+// one row's blob, by the entry's own lane: assembled in registers (the byte loop unrolls
+// to constant positions) and written with aligned 16-B stores into its CDR_BLOB_*_STRIDE
+// slot
 template <uint32_t BYTES, uint32_t STRIDE, class Row, class ByteFn>
 __device__ __forceinline__ void put_blob(const Row& row, uint8_t* dst, ByteFn byte_at) {
   uint4* d = reinterpret_cast<uint4*>(dst);

@@ -712,6 +712,8 @@ uint64_t cdr_struct_size(const char* name) {
       {"cdr_task", sizeof(cdr_task)},
       {"cdr_last_decision", sizeof(cdr_last_decision)},
       {"cdr_opts", sizeof(cdr_opts)},
+      {"cdr_strtab", sizeof(cdr_strtab)},
+      {"cdr_exec_persist", sizeof(cdr_exec_persist)},
       {"cdr_ingest_in", sizeof(cdr_ingest_in)},
       {"cdr_ingest_out", sizeof(cdr_ingest_out)},
       {"cdr_vh_token", sizeof(cdr_vh_token)},

@@ -163,7 +163,8 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
       saux = E.i64(ks, CDR_COL_AUX);
     }
     constexpr uint64_t kStartWords = (sizeof(cdr_attr_wf_started) + 7) / 8;
-    if ((uint64_t)saux + kStartWords > B.ev.arena_words) {  // malformed input: no attribute record
+    if (saux < 0 || B.ev.arena_words < kStartWords ||
+        (uint64_t)saux > B.ev.arena_words - kStartWords) {  // malformed input: no attribute record (no wrap)
       code = CDR_E_BAD_INPUT;
       break;
     }

@@ -452,6 +452,90 @@ class Engine:
             for p in ptrs:
                 hip.hipFree(p)
 
+    def encode_blobs(self, batch: Batch, out: Outputs, table: str, strings: list, persist=None,
+                     cluster_names=None):
+        """Variable-size sqlblobs row blobs through cdr_encode_blobs_async (size pass +
+        scan, then the write pass) for table "act", "child", "signal" or "exec", with
+        `strings[h]` (bytes) the string table: ({row: blob}, {row: CDR_BLOB_* status}) for
+        the rows of OK entries (exec: row = entry).  `persist` is a cdr_exec_persist array
+        and `cluster_names` a list of handles (table "exec")."""
+        tid = {"act": 0, "child": 2, "signal": 4, "exec": 5}[table]
+        hip = _hip()
+        pl = out.plan
+        ptrs = []
+
+        def dalloc(nbytes):
+            p = C.c_void_p()
+            if hip.hipMalloc(C.byref(p), C.c_size_t(max(8, nbytes))) != 0:
+                raise RuntimeError("hipMalloc failed")
+            ptrs.append(p)
+            return p
+
+        def up(x, nb=None):
+            nb = C.sizeof(x) if nb is None else nb
+            p = dalloc(nb)
+            if nb and hip.hipMemcpy(p, x if isinstance(x, int) else C.addressof(x), C.c_size_t(nb), 1) != 0:
+                raise RuntimeError("hipMemcpy H2D failed")
+            return p
+
+        def down(p, nb):
+            host = (C.c_uint8 * max(1, nb))()
+            if nb and hip.hipMemcpy(host, p, C.c_size_t(nb), 2) != 0:
+                raise RuntimeError("hipMemcpy D2H failed")
+            return bytes(host)[:nb]
+        try:
+            lens = np.array([len(s) for s in strings], np.uint64)
+            off = np.zeros(len(strings) + 1, np.uint64)
+            np.cumsum(lens, out=off[1:])
+            blob = np.frombuffer(b"".join(strings) or b"\0", np.uint8)
+            st = abi.CdrStrtab(n=len(strings))
+            st.bytes = up(blob.ctypes.data, blob.nbytes).value
+            st.off = up(off.ctypes.data, off.nbytes).value
+            db = abi.CdrDevBatch()
+            db.n_wfs = batch.n_wfs
+            db.caps = up(pl.caps)
+            db.wfs = up(batch.wfs)
+            db.cluster = batch.cluster
+            o = abi.CdrOut()
+            o.result = up(out.result)
+            for t in ("exec", "repl"):
+                setattr(o, t, up(getattr(out, t)))
+            for t in ("act", "child", "signal", "vh", "rp", "sa"):
+                setattr(o, t, up(out.tables[t]))
+            n_rows = batch.n_wfs if table == "exec" else max(1, getattr(pl.totals, table))
+            pp = up(persist) if persist is not None else None
+            cn = up((C.c_uint32 * max(1, len(cluster_names or [])))(*(cluster_names or [])))
+            row_off = dalloc(8 * (n_rows + 1))
+            status = dalloc(4 * n_rows)
+            L = abi.lib()
+            rc = L.cdr_encode_blobs_async(self.ctx, tid, C.byref(db), C.byref(o), C.byref(st), pp, cn, n_rows,
+                                          row_off, None, status, None)
+            if rc:
+                raise RuntimeError(f"cdr_encode_blobs_async (sizes) rc={rc}")
+            offs = np.frombuffer(down(row_off, 8 * (n_rows + 1)), np.uint64)
+            total = int(offs[-1])
+            blobs = dalloc(total)
+            rc = L.cdr_encode_blobs_async(self.ctx, tid, C.byref(db), C.byref(o), C.byref(st), pp, cn, n_rows,
+                                          row_off, blobs, status, None)
+            if rc:
+                raise RuntimeError(f"cdr_encode_blobs_async (write) rc={rc}")
+            raw = down(blobs, total)
+            stat = np.frombuffer(down(status, 4 * n_rows), np.int32)
+            got, codes = {}, {}
+            cnt = {"act": "n_activity", "child": "n_child", "signal": "n_signal"}.get(table)
+            for w in range(batch.n_wfs):
+                if out.result[w].code != abi.OK:
+                    continue
+                rows = [w] if table == "exec" else [getattr(pl.caps[w], table + "_off") + j
+                                                     for j in range(getattr(out.result[w], cnt))]
+                for r in rows:
+                    got[r] = raw[int(offs[r]):int(offs[r + 1])]
+                    codes[r] = int(stat[r])
+            return got, codes
+        finally:
+            for p in ptrs:
+                hip.hipFree(p)
+
     def rebuild(self, batch: Batch, pl: Plan | None = None, advanced_visibility: bool = True, snapshot: bool = False) -> Outputs:
         """nDCStateRebuilder.rebuild's device half through cdr_rebuild_batch: replay
         (every kernel) then refreshTasks (refresh.hip) with now = batch.now_ns; the

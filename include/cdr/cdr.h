@@ -381,6 +381,55 @@ int cdr_rebuild_batch(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps,
 int cdr_encode_rows_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out, uint8_t* blobs,
                           void* stream);
 
+/* The variable-size row blobs (encode_var.hip):
+ *   table 0  ActivityInfo        (sqlblobs.thrift:136-168, workflowStateMaps.go:48-83)
+ *   table 2  ChildExecutionInfo  (sqlblobs.thrift:170-184, workflowStateMaps.go:371-385)
+ *   table 4  SignalInfo          (sqlblobs.thrift:186-193, workflowStateMaps.go:632-639)
+ *   table 5  WorkflowExecutionInfo of the execution row (sqlblobs.thrift:73-134,
+ *            buildExecutionRow sqlExecutionManagerUtil.go:1197-1308), one row per entry
+ * Strings come from a device string table (handle h's bytes are bytes[off[h], off[h+1]),
+ * handle 0 = "" / nil).  Its conventions: a plain string or binary field is its bytes; a
+ * NonRetriableErrors handle holds the wire body of the list<string> (element type, i32
+ * count, elements) and a Memo handle the wire body of the Memo struct — what
+ * cdr_ingest_decode interns.  UUID-typed binaries (ParentDomainID, ParentRunID,
+ * StartedRunID) are MustParseUUID of their strings; ID strings the replay generates
+ * (CreateRequestID, SignalRequestID, the branch ID) are RFC 4122 text of their 128 bits.
+ * Go's map iteration order is random, so the reference has no fixed byte order for the
+ * map fields (LastReplicationInfo, SearchAttributes, Memo): they are written in cluster-
+ * index, row and input order.  Not carried by the replay projection, and so written as a
+ * fresh replay leaves them: ScheduledEvent / StartedEvent / InitiatedEvent (nil),
+ * CompletionEvent (nil), the branch's ancestors ([]); the execution row's fields outside
+ * the projection come from cdr_exec_persist.
+ * Two calls: with blobs == NULL, a size pass and an exclusive scan write row_off[0..n_rows]
+ * (device, n_rows + 1: row r's blob is bytes [row_off[r], row_off[r+1]) — zero-length for
+ * rows past an entry's count and for entries that did not replay OK) and per-row
+ * CDR_BLOB_* status codes into row_status (device, nullable); the caller reads
+ * row_off[n_rows] (the total), allocates `blobs` and calls again to write them.  Rows are
+ * the table's capacity rows (caps.*_off + j; n_rows = the table's total capacity), for
+ * table 5 the entries (n_rows = n_wfs); cluster_names[i] (device) is the handle of cluster
+ * i's name, the LastReplicationInfo key of 2DC entries.  Asynchronous on `stream`. */
+typedef struct cdr_strtab {
+  const uint8_t* bytes; /* device */
+  const uint64_t* off;  /* device, n + 1 */
+  uint32_t n, _pad;
+} cdr_strtab;
+/* per-entry inputs of buildExecutionRow outside the replay projection */
+typedef struct cdr_exec_persist {
+  int64_t start_version, current_version; /* buildExecutionRow's startVersion / currentVersion */
+  int64_t start_time, last_updated_time;  /* UnixNano (CDR_ZERO_TIME_NANOS: Go's zero time) */
+  int64_t history_size, sticky_s2s_timeout;
+  uint32_t execution_context, sticky_task_list; /* handles */
+  uint32_t client_library_version, client_feature_version, client_impl, _pad;
+} cdr_exec_persist;
+#define CDR_ZERO_TIME_NANOS (-6795364578871345152ll) /* time.Time{}.UnixNano() */
+#define CDR_BLOB_OK 0
+#define CDR_BLOB_E_UUID 1   /* MustParseUUID would panic on the string */
+#define CDR_BLOB_E_HANDLE 2 /* a handle past the string table */
+#define CDR_BLOB_E_MEMO 3   /* the Memo handle does not hold a Memo struct body */
+int cdr_encode_blobs_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out,
+                           const cdr_strtab* strs, const cdr_exec_persist* persist, const uint32_t* cluster_names,
+                           uint64_t n_rows, uint64_t* row_off, uint8_t* blobs, int32_t* row_status, void* stream);
+
 /* Stream compaction of the per-workflow pending tables into dense tables
  * (device pointers): for each table, rows [caps.off, caps.off + result.n) of every
  * workflow are copied to dense[row_base[w] ...]; row_base is an exclusive scan of
