@@ -234,6 +234,7 @@ SLICE_FAST = 0x1
 SLICE_WAVE = 0x2
 SLICE_REG = 0x4
 SLICE_REG2 = 0x8
+SLICE_REG0 = 0x10
 CAP_FAST = 0x1
 CAP_WAVE = 0x2
 PLAN_WAVE = 0x1
@@ -242,6 +243,7 @@ PLAN_NO_LONG = 0x4  # with PLAN_WAVE: keep long lane-capable histories in lane s
 CAP_LANE = 0x4
 CAP_REG = 0x8
 CAP_REG2 = 0x10
+CAP_REG0 = 0x20
 
 # variable-size row blobs (cdr.h cdr_encode_blobs_async)
 CdrStrtab = _S("cdr_strtab", [("bytes", C.c_void_p), ("off", C.c_void_p), ("n", u32), ("_pad", u32)])
@@ -278,6 +280,7 @@ CdrDevBatch = _S("cdr_dev_batch", [
     ("ev", CdrSlices), ("scratch", C.c_void_p), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
     ("n_wfs", u32), ("empty_uuid", u32), ("max_act_slots", u32), ("max_tim_slots", u32),
     ("n_fast_slices", u32), ("n_wave_slices", u32), ("n_reg_slices", u32), ("n_reg2_slices", u32),
+    ("n_reg0_slices", u32), ("_pad_reg0", u32),
     ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64), ("carry", C.c_void_p)])
 
 # ------------------------------------------------------------------ synth

@@ -63,11 +63,14 @@ struct cdr_ctx {
   // optional per-launch timing ring (bench): event pairs around every replay kernel
   std::vector<hipEvent_t> ring;
   uint32_t ring_used = 0;
-  // side streams for the wave kernel and the 12-activity register kernel: their
-  // waves (the longest histories; scalar-unit-bound / single-wave-per-SIMD) co-run with
-  // the main lane kernels instead of after them (fork/join by events)
-  hipStream_t side = nullptr, side2 = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
+  // side streams, one per replay kernel class (wave, 12-activity register, general,
+  // small-table register, fast, 6-activity register): the classes' slices co-run instead
+  // of one kernel after another (fork/join by events on the caller's stream).
+  // Concurrency beyond the HIP runtime's hardware queues (GPU_MAX_HW_QUEUES, default 4)
+  // serialises on a shared queue.
+  static constexpr int N_SIDE = 6;
+  hipStream_t side[N_SIDE] = {};
+  hipEvent_t fork = nullptr, join[N_SIDE] = {};
   int concurrent = 1;
   // grow-only device workspace of the host-buffer calls
   void* ws[WS_NUM] = {};

@@ -94,7 +94,8 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   for (uint64_t k = 0; k < n; k++) {
     const cdr_event& e = ev[k];
     if (k == 0 || (e.flags & CDR_EVF_BATCH_FIRST)) call_start = k;
-    reg = reg && e.event_id > last_id && e.event_id < (1ll << 31) && k - call_start < 4096;
+    reg = reg && e.event_id > last_id && e.event_id < (1ll << 31) && e.version < (1ll << 31) &&
+          k - call_start < 4096;
     last_id = e.event_id;
     if (e.type == CDR_EV_WF_STARTED) {  // rows from the start attributes (a second Started resets them)
       const cdr_attr_wf_started& a = e.a.started;
@@ -202,6 +203,9 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
         sa_keys.size() <= CDR_REG_NSA;
   if (reg && live_max <= (int64_t)CDR_REG_NA) c.flags |= CDR_CAP_REG;
   else if (reg && live_max <= (int64_t)CDR_REG2_NA) c.flags |= CDR_CAP_REG2;
+  if ((c.flags & CDR_CAP_REG) && live_max <= (int64_t)CDR_REG0_NA && lv_max[0] <= CDR_REG0_NT &&
+      lv_max[1] <= CDR_REG0_NX && lv_max[2] <= CDR_REG0_NX && lv_max[3] <= CDR_REG0_NX)
+    c.flags |= CDR_CAP_REG0;
   *out = c;
 }
 
@@ -324,7 +328,7 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
       c.sa_cap += r.n_search_attr;
       c.act_live += r.n_activity;
       c.timer_live += r.n_timer;
-      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_REG | CDR_CAP_REG2);
+      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_REG | CDR_CAP_REG2 | CDR_CAP_REG0);
     }
     cdr_internal::task_caps(b->events + d.ev_off, d.ev_len, &c.xfer_cap, &c.ttask_cap);
     c.xfer_off = t.xfer;
@@ -363,29 +367,35 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   // long histories: a lane slice advances one event per step, so a history much longer
   // than the batch's lane work per resident wave (its steps / CDR_LANE_RESIDENT) sets
   // the lane kernels' critical path alone; on a wave of its own it replays ~10x faster
-  // per event and co-runs with the lane slices (replay.hip, side stream)
-  uint64_t long_thr = UINT64_MAX;
+  // per event and co-runs with the lane slices (replay.hip, side stream).  The
+  // 12-activity register kernel runs one wave per SIMD, so its threshold is lower.
+  uint64_t long_thr = UINT64_MAX, long_thr2 = UINT64_MAX;
   if ((mode & CDR_PLAN_WAVE) && !(mode & CDR_PLAN_NO_LONG)) {
     static const uint32_t* lp = [] {
-      static uint32_t v[2] = {CDR_LONG_MIN, CDR_LONG_FACTOR};
-      if (const char* e = std::getenv("CDR_LONG"))  // tuning override "min,factor"
-        std::sscanf(e, "%u,%u", &v[0], &v[1]);
+      static uint32_t v[3] = {CDR_LONG_MIN, CDR_LONG_FACTOR, CDR_LONG_REG2_DIV};
+      if (const char* e = std::getenv("CDR_LONG"))  // tuning override "min,factor,reg2 divisor"
+        std::sscanf(e, "%u,%u,%u", &v[0], &v[1], &v[2]);
       return v;
     }();
     uint64_t lane_ev = 0;
     for (uint32_t w = 0; w < n_wfs; w++)
-      if (!(caps[w].flags & CDR_CAP_WAVE) || (caps[w].flags & (CDR_CAP_LANE | CDR_CAP_REG | CDR_CAP_REG2)))
+      if (!(caps[w].flags & CDR_CAP_WAVE) || (caps[w].flags & (CDR_CAP_REG | CDR_CAP_REG2)))
         lane_ev += wfs[w].ev_len;
     const uint64_t per_slot = lane_ev / ((uint64_t)CDR_SLICE_WIDTH * CDR_LANE_RESIDENT);
     long_thr = std::max<uint64_t>(lp[0], (uint64_t)lp[1] * per_slot);
+    long_thr2 = std::max<uint64_t>(lp[0] / 2, long_thr / std::max(1u, lp[2]));
   }
-  for (uint32_t w = 0; w < n_wfs; w++)
-    ((mode & CDR_PLAN_WAVE) && (caps[w].flags & CDR_CAP_WAVE) &&
-             ((mode & CDR_PLAN_WAVE_ALL) || !(caps[w].flags & (CDR_CAP_LANE | CDR_CAP_REG | CDR_CAP_REG2)) ||
-              (uint64_t)wfs[w].ev_len > long_thr)
+  // wave slices: every CDR_CAP_WAVE entry no register-table kernel takes (the general
+  // lane kernel is the slow fallback for what fits neither), and the long ones
+  for (uint32_t w = 0; w < n_wfs; w++) {
+    const uint32_t f = caps ? caps[w].flags : 0u;
+    const uint64_t thr = (f & CDR_CAP_REG) ? long_thr : long_thr2;
+    ((mode & CDR_PLAN_WAVE) && (f & CDR_CAP_WAVE) &&
+             ((mode & CDR_PLAN_WAVE_ALL) || !(f & (CDR_CAP_REG | CDR_CAP_REG2)) || (uint64_t)wfs[w].ev_len > thr)
          ? waves
          : lanes)
         .push_back(w);
+  }
   // longest first: a slice's rows = its longest lane, so neighbours in length
   // share slices and padding stays small (SELL-C-sigma with sigma = batch); wave
   // slices longest first too, so the longest histories start first
@@ -400,9 +410,10 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   auto group = [&](uint32_t a) {
     return !caps                               ? 0u
            : (caps[a].flags & CDR_CAP_FAST)  ? 0u
-           : (caps[a].flags & CDR_CAP_REG)   ? 1u
-           : (caps[a].flags & CDR_CAP_REG2)  ? 2u
-                                             : 3u;
+           : (caps[a].flags & CDR_CAP_REG0)  ? 1u
+           : (caps[a].flags & CDR_CAP_REG)   ? 2u
+           : (caps[a].flags & CDR_CAP_REG2)  ? 3u
+                                             : 4u;
   };
   auto lane_order = [&](uint32_t a, uint32_t c) {
     const uint32_t ga = group(a), gc = group(c);
@@ -484,25 +495,28 @@ int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n
       continue;
     }
     uint32_t a = 0, t = 0, lanes = 0;
-    bool fast = true, reg = true, reg2 = true;
+    bool fast = true, reg0 = true, reg = true, reg2 = true;
     for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
       const int32_t w = lane_wf[(size_t)s * CDR_SLICE_WIDTH + l];
       if (w < 0) continue;
       a = std::max(a, caps[w].act_live);
       t = std::max(t, caps[w].timer_live);
       fast = fast && (caps[w].flags & CDR_CAP_FAST);
+      reg0 = reg0 && (caps[w].flags & CDR_CAP_REG0);
       reg = reg && (caps[w].flags & CDR_CAP_REG);
       reg2 = reg2 && (caps[w].flags & (CDR_CAP_REG | CDR_CAP_REG2));
       lanes++;
     }
     fast = fast && lanes > 0;
-    reg = reg && lanes > 0 && !fast;
-    reg2 = reg2 && lanes > 0 && !fast && !reg;
+    reg0 = reg0 && lanes > 0 && !fast;
+    reg = reg && lanes > 0 && !fast && !reg0;
+    reg2 = reg2 && lanes > 0 && !fast && !reg0 && !reg;
     nf += fast ? 1u : 0u;
     if (scratch_off) scratch_off[s] = off;
     if (act_slots) act_slots[s] = a;
     if (tim_slots) tim_slots[s] = t;
-    if (slice_flags) slice_flags[s] = fast ? CDR_SLICE_FAST : reg ? CDR_SLICE_REG : reg2 ? CDR_SLICE_REG2 : 0u;
+    if (slice_flags)
+      slice_flags[s] = fast ? CDR_SLICE_FAST : reg0 ? CDR_SLICE_REG0 : reg ? CDR_SLICE_REG : reg2 ? CDR_SLICE_REG2 : 0u;
     off += ((uint64_t)a * CDR_ACT_PLANES + (uint64_t)t * CDR_TIM_PLANES) * CDR_SLICE_WIDTH;
   }
   *total_words = off;

@@ -1046,7 +1046,8 @@ __global__ __launch_bounds__(64) void k_caps(const cdr_event* events, const uint
     const cdr_event& e = ev[k];
     const uint32_t type = e.type;
     if (k == 0 || (e.flags & CDR_EVF_BATCH_FIRST)) call_start = k;
-    reg = reg && e.event_id > last_id && e.event_id < (1ll << 31) && k - call_start < 4096;
+    reg = reg && e.event_id > last_id && e.event_id < (1ll << 31) && e.version < (1ll << 31) &&
+          k - call_start < 4096;
     last_id = e.event_id;
     if (type == CDR_EV_WF_STARTED) {  // a second Started resets the row lists
       const cdr_attr_wf_started& a = e.a.started;
@@ -1143,6 +1144,9 @@ __global__ __launch_bounds__(64) void k_caps(const cdr_event* events, const uint
         sa_keys.size() <= CDR_REG_NSA;
   if (reg && live_max <= (int64_t)CDR_REG_NA) c.flags |= CDR_CAP_REG;
   else if (reg && live_max <= (int64_t)CDR_REG2_NA) c.flags |= CDR_CAP_REG2;
+  if ((c.flags & CDR_CAP_REG) && live_max <= (int64_t)CDR_REG0_NA && lv0.max <= CDR_REG0_NT &&
+      lv1.max <= CDR_REG0_NX && lv2.max <= CDR_REG0_NX && lv3.max <= CDR_REG0_NX)
+    c.flags |= CDR_CAP_REG0;
   c.xfer_cap = x + 1;  // + refreshTasks' UpsertWorkflowSearchAttributes task
   c.ttask_cap = t;
   caps[w] = c;
@@ -1313,6 +1317,7 @@ extern "C" int cdr_ingest_plan(cdr_ctx* ctx, const cdr_ingest_out* dec, const cd
     b.max_tim_slots = sc_tim[i] > b.max_tim_slots ? sc_tim[i] : b.max_tim_slots;
     b.n_reg_slices += (sflags[i] & CDR_SLICE_REG) ? 1u : 0u;
     b.n_reg2_slices += (sflags[i] & CDR_SLICE_REG2) ? 1u : 0u;
+    b.n_reg0_slices += (sflags[i] & CDR_SLICE_REG0) ? 1u : 0u;
   }
   b.n_fast_slices = n_fast;
   b.n_wave_slices = n_wave;

@@ -534,7 +534,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     const uint32_t sf = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_flags[s]);
     if (sf & CDR_SLICE_WAVE) return;  // k_replay_wave
     if (KA()->fast && (sf & CDR_SLICE_FAST)) return;
-    if (KA()->reg && (sf & (CDR_SLICE_REG | CDR_SLICE_REG2))) return;  // k_replay_reg
+    if (KA()->reg && (sf & (CDR_SLICE_REG | CDR_SLICE_REG2 | CDR_SLICE_REG0))) return;  // k_replay_reg
   }
   const uint64_t row0_ = KA()->B.ev.slice_row0[s];
   const uint64_t row0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(row0_ >> 32)) << 32) |
@@ -1799,11 +1799,17 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
       return nullptr;
     }
   c->timed = false;
-  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->join2, hipEventDisableTiming) != hipSuccess)
+  // the classes whose slices are few and long (wave, 12-activity register, general) get
+  // high-priority streams: their workgroups are dispatched before the bulk classes fill
+  // the CUs (a 256-VGPR wave finds no room beside two 238-VGPR ones)
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+  bool sides_ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+  for (int i = 0; i < cdr_ctx::N_SIDE; i++)
+    sides_ok = sides_ok &&
+               hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, i < 3 ? prio_hi : prio_lo) == hipSuccess &&
+               hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming) == hipSuccess;
+  if (!sides_ok)
     c->concurrent = 0;
   if (const char* e = std::getenv("CDR_SERIAL_KERNELS")) c->concurrent = c->concurrent && e[0] == '0';
   c->concurrent = c->concurrent && o.concurrent;
@@ -1841,11 +1847,11 @@ void cdr_destroy(cdr_ctx* c) {
   if (!c) return;
   for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
   for (hipEvent_t e : c->ring) (void)hipEventDestroy(e);
-  if (c->side) (void)hipStreamDestroy(c->side);
-  if (c->side2) (void)hipStreamDestroy(c->side2);
+  for (int i = 0; i < cdr_ctx::N_SIDE; i++) {
+    if (c->side[i]) (void)hipStreamDestroy(c->side[i]);
+    if (c->join[i]) (void)hipEventDestroy(c->join[i]);
+  }
   if (c->fork) (void)hipEventDestroy(c->fork);
-  if (c->join) (void)hipEventDestroy(c->join);
-  if (c->join2) (void)hipEventDestroy(c->join2);
   if (hipSetDevice(c->device) == hipSuccess)
     for (void* p : c->ws) (void)hipFree(p);
   delete c;
@@ -1868,64 +1874,77 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   if (tasks && (in->n_wave_slices > 0 || !out->timer_tasks || !out->n_tasks)) return CDR_API_EINVAL;
   const bool fast = c->fast && in->n_fast_slices > 0 && !tasks;
   // register-table kernel: LastReplicationInfo kept for clusters < CDR_REG_NCL only
-  const bool reg = c->fast && c->reg && in->n_reg_slices + in->n_reg2_slices > 0 && !tasks &&
+  const bool reg = c->fast && c->reg && in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices > 0 && !tasks &&
                    in->cluster.n_clusters <= (int)CDR_REG_NCL;
   const bool wave = in->n_wave_slices > 0;
-  const bool general = (fast ? in->n_fast_slices : 0u) + (reg ? in->n_reg_slices + in->n_reg2_slices : 0u) +
+  const bool general = (fast ? in->n_fast_slices : 0u) +
+                           (reg ? in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices : 0u) +
                            in->n_wave_slices <
                        in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
   cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u};
-  // kernel streams: the wave kernel (the batch's longest histories, one wave each,
-  // scalar-unit-bound) and the 12-activity register kernel (one wave per SIMD) go
-  // first, each on a side stream, so that their long slices start at once and co-run
-  // with the main-stream lane kernels (fast / register / general) instead of after them
+  // kernel streams: each replay kernel class present gets a side stream of its own
+  // (all forked from the caller's stream, so none is dispatched ahead of the others but
+  // by priority), launched longest-first: the wave kernel (the batch's longest histories, one wave each, scalar-unit-
+  // bound), the 12-activity register kernel (one wave per SIMD), the general kernel (the
+  // few histories no specialised kernel takes), the small-table register kernel, the
+  // fast kernel — so that no class's slices wait for another's kernel to finish
   const bool reg1 = blocks && reg && in->n_reg_slices;
+  const bool reg0 = blocks && reg && in->n_reg0_slices;
   const bool reg2 = blocks && reg && in->n_reg2_slices;
-  const bool main_work = (blocks && fast) || reg1 || (blocks && general);
-  const bool fork_w = c->concurrent && blocks && wave && (main_work || reg2);
-  const bool fork_r2 = c->concurrent && reg2 && (main_work || (blocks && wave));
-  if (fork_w || fork_r2) {
-    HIPCHK(hipEventRecord(c->fork, st));
-    if (fork_w) HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
-    if (fork_r2) HIPCHK(hipStreamWaitEvent(c->side2, c->fork, 0));
-  }
-  if (blocks && wave) hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, fork_w ? c->side : st, L);
+  const bool wv = blocks && wave, gen = blocks && general, fst = blocks && fast;
+  const bool on[cdr_ctx::N_SIDE] = {wv, reg2, gen, reg0, fst, reg1};
+  int kinds = 0;
+  for (bool o : on) kinds += o ? 1 : 0;
+  bool fk[cdr_ctx::N_SIDE];
+  bool any_fork = false;
+  for (int i = 0; i < cdr_ctx::N_SIDE; i++) any_fork |= (fk[i] = c->concurrent && on[i] && kinds > 1);
+  if (any_fork) HIPCHK(hipEventRecord(c->fork, st));
+  for (int i = 0; i < cdr_ctx::N_SIDE; i++)
+    if (fk[i]) HIPCHK(hipStreamWaitEvent(c->side[i], c->fork, 0));
+  auto sx = [&](int i) { return fk[i] ? c->side[i] : st; };
+  if (wv) hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, sx(0), L);
   HIPCHK(hipGetLastError());
-  if (fork_w) HIPCHK(hipEventRecord(c->join, c->side));
   if (reg2) {
     typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
     hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), dim3(blocks),
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, fork_r2 ? c->side2 : st, L);
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), L);
   }
   HIPCHK(hipGetLastError());
-  if (fork_r2) HIPCHK(hipEventRecord(c->join2, c->side2));
-  if (blocks && fast)
-    hipLaunchKernelGGL(k_replay_fast, dim3(blocks), dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, st, L);
+  if (gen) {
+    if (tasks)
+      hipLaunchKernelGGL((k_replay<true, true>), dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, sx(2), L);
+    else
+      hipLaunchKernelGGL((k_replay<true, false>), dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, sx(2), L);
+  }
+  HIPCHK(hipGetLastError());
+  if (gen && spill) {
+    if (tasks)
+      hipLaunchKernelGGL((k_replay<false, true>), dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, sx(2), L);
+    else
+      hipLaunchKernelGGL((k_replay<false, false>), dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, sx(2), L);
+  }
+  HIPCHK(hipGetLastError());
+  if (reg0) {  // the small-table variant, at 3 waves per SIMD
+    typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
+    hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), dim3(blocks),
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), L);
+  }
+  HIPCHK(hipGetLastError());
+  if (fst) hipLaunchKernelGGL(k_replay_fast, dim3(blocks), dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), L);
   HIPCHK(hipGetLastError());
   if (reg1) {
     typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
     hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), dim3(blocks),
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, st, L);
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), L);
   }
   HIPCHK(hipGetLastError());
-  if (blocks && general) {
-    if (tasks)
-      hipLaunchKernelGGL((k_replay<true, true>), dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, L);
-    else
-      hipLaunchKernelGGL((k_replay<true, false>), dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, st, L);
-  }
-  HIPCHK(hipGetLastError());
-  if (blocks && general && spill) {
-    if (tasks)
-      hipLaunchKernelGGL((k_replay<false, true>), dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
-    else
-      hipLaunchKernelGGL((k_replay<false, false>), dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, st, L);
-  }
-  HIPCHK(hipGetLastError());
-  if (fork_w) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
-  if (fork_r2) HIPCHK(hipStreamWaitEvent(st, c->join2, 0));
+  for (int i = 0; i < cdr_ctx::N_SIDE; i++)
+    if (fk[i]) {
+      HIPCHK(hipEventRecord(c->join[i], c->side[i]));
+      HIPCHK(hipStreamWaitEvent(st, c->join[i], 0));
+    }
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used + 1] : c->ev[1], st));
   if (ring) {
     // keep ev[0..1] meaningful for cdr_last_kernel_ms as well

@@ -113,6 +113,8 @@ class DeviceBatch:
         db.n_reg_slices = self.n_reg
         self.n_reg2 = int(((self.h_sflags & abi.SLICE_REG2) != 0).sum())
         db.n_reg2_slices = self.n_reg2
+        self.n_reg0 = int(((self.h_sflags & abi.SLICE_REG0) != 0).sum())
+        db.n_reg0_slices = self.n_reg0
         db.empty_uuid = meta.empty_uuid
         db.cluster = meta.cluster
         db.now_ns = meta.now_ns

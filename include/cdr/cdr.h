@@ -132,6 +132,9 @@ typedef struct cdr_slices {
 /* every lane's history has CDR_CAP_REG2 or CDR_CAP_REG: the register-table kernel's
  * variant with CDR_REG2_NA activity slots */
 #define CDR_SLICE_REG2 0x8u
+/* every lane's history has CDR_CAP_REG0: the register-table variant with the small tables
+ * (CDR_REG0_*) at 3 waves per SIMD */
+#define CDR_SLICE_REG0 0x10u
 /* event types the fast-path kernel replays (bit = cdr_event_type) */
 #define CDR_FAST_TYPES                                                                                       \
   (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_WF_COMPLETED) | CDR_TB(CDR_EV_WF_FAILED) |                      \
@@ -218,6 +221,8 @@ typedef struct cdr_dev_batch {
   uint32_t n_wave_slices; /* slices with CDR_SLICE_WAVE (cdr_plan_slices_ex) */
   uint32_t n_reg_slices;  /* slices with CDR_SLICE_REG (cdr_plan_scratch) */
   uint32_t n_reg2_slices; /* slices with CDR_SLICE_REG2 (cdr_plan_scratch) */
+  uint32_t n_reg0_slices; /* slices with CDR_SLICE_REG0 (cdr_plan_scratch) */
+  uint32_t _pad_reg0;
   cdr_cluster_meta cluster;
   int64_t now_ns;
   uint64_t uuid_seed;
@@ -241,20 +246,23 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
                     uint64_t* slice_row0, uint32_t* n_slices, uint64_t* n_rows);
 
 /* As cdr_plan_slices, with a mode: CDR_PLAN_WAVE gives every entry whose caps carry
- * CDR_CAP_WAVE a wave slice of its own (after the lane slices, longest first) and
+ * CDR_CAP_WAVE and neither register-table cap (CDR_CAP_REG / REG2) a wave slice of its
+ * own (after the lane slices, longest first) and
  * marks it in slice_flags (nullable; the other slices get 0).  `caps` may be NULL
  * when mode is 0.  Returns the number of wave slices via *n_wave (nullable). */
 #define CDR_PLAN_WAVE 0x1u
-/* with CDR_PLAN_WAVE: also the CDR_CAP_LANE entries get wave slices (by default they
+/* with CDR_PLAN_WAVE: also the register-table entries get wave slices (by default they
  * stay in lane slices, where they replay cheaper) */
 #define CDR_PLAN_WAVE_ALL 0x2u
 /* with CDR_PLAN_WAVE the planner also gives a wave slice to every CDR_CAP_WAVE entry
- * whose history is longer than max(CDR_LONG_MIN, CDR_LONG_FACTOR x the lane events per
- * resident lane slot, i.e. lane events / (64 x CDR_LANE_RESIDENT)): such a history
+ * whose history is longer than T = max(CDR_LONG_MIN, CDR_LONG_FACTOR x the lane events
+ * per resident lane slot, i.e. lane events / (64 x CDR_LANE_RESIDENT)) — T /
+ * CDR_LONG_REG2_DIV (at least CDR_LONG_MIN / 2) for CDR_CAP_REG2 entries: such a history
  * alone would set the lane kernels' critical path.  This bit turns that rule off. */
 #define CDR_PLAN_NO_LONG 0x4u
 #define CDR_LONG_MIN 1024u
 #define CDR_LONG_FACTOR 2u
+#define CDR_LONG_REG2_DIV 2u
 #define CDR_LANE_RESIDENT 2048u
 int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
                        int32_t* lane_wf, uint32_t* slice_len, uint64_t* slice_row0, uint32_t* slice_flags,

@@ -596,13 +596,20 @@ typedef struct cdr_wf_caps {
 #define CDR_REG_NA 6u
 #define CDR_REG_NT 10u
 #define CDR_REG_NX 4u
-#define CDR_REG_NRP 8u
+#define CDR_REG_NRP 6u
 #define CDR_REG_NSA 8u
 #define CDR_REG_NCL 4u /* 2DC: LastReplicationInfo kept for clusters < 4 (batch with more: general kernel) */
 /* the same envelope with up to CDR_REG2_NA live activities (long activity-heavy
  * histories, C4/C5 tails): the kernel's second variant, at lower occupancy */
 #define CDR_CAP_REG2 0x10u
 #define CDR_REG2_NA 12u
+/* the envelope's small corner (at most CDR_REG0_NA live activities, CDR_REG0_NT live user
+ * timers, CDR_REG0_NX live children / request-cancels / signals each): the variant whose
+ * tables leave room for 3 waves per SIMD (168 VGPRs); such entries carry CDR_CAP_REG too */
+#define CDR_CAP_REG0 0x20u
+#define CDR_REG0_NA 3u
+#define CDR_REG0_NT 5u
+#define CDR_REG0_NX 3u
 #define CDR_LANE_MAX_ACT 6u
 #define CDR_LANE_MAX_TIMERS 10u
 #define CDR_LANE_MAX_EXT 8u

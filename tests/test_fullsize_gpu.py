@@ -39,7 +39,7 @@ def _gpu_digests(ctx, cfg, index_map, seed, plan_mode, reg):
         L.cdr_set_reg_path(ctx, 1)
     assert rc == 0, rc
     per, tot = db.digests(ctx, stream)
-    kinds = {"wave": db.n_wave, "reg": db.n_reg, "reg2": db.n_reg2}
+    kinds = {"wave": db.n_wave, "reg": db.n_reg, "reg2": db.n_reg2, "reg0": db.n_reg0}
     del db
     torch.cuda.empty_cache()
     return per, tot, kinds

@@ -224,10 +224,10 @@ def test_wave_slices_plan_and_pack():
     assert all((int(x) & 0xFF) == 0xFF for x in tf[n:])
 
 
-def test_lane_friendly_entries_stay_in_lane_slices():
-    """CDR_CAP_LANE (small working sets, moderate length) and the register-table caps keep
-    a divergent history in a lane slice under CDR_PLAN_WAVE; PLAN_WAVE_ALL sends it to a
-    wave slice."""
+def test_register_table_entries_stay_in_lane_slices():
+    """The register-table caps (CDR_CAP_REG / REG2) keep a divergent history in a lane
+    slice under CDR_PLAN_WAVE (other CDR_CAP_WAVE entries get wave slices: the general lane
+    kernel is only the fallback for what fits neither); PLAN_WAVE_ALL sends them to waves."""
     b = engine.synth_batch(3, 300, seed=12)
     pl = engine.plan(b)
     lane_ok = [w for w in range(b.n_wfs) if pl.caps[w].flags & abi.CAP_LANE]
@@ -237,25 +237,29 @@ def test_lane_friendly_entries_stay_in_lane_slices():
         assert c.act_live <= 6 and c.timer_live <= 10 and b.wfs[w].ev_len <= 512
     n_all = engine.slice_kinds(b, pl, abi.PLAN_WAVE | abi.PLAN_WAVE_ALL)[1]
     n_def = engine.slice_kinds(b, pl, abi.PLAN_WAVE)[1]
-    # register-table entries (CDR_CAP_REG / REG2) also stay in lane slices
     keep = [w for w in range(b.n_wfs) if (pl.caps[w].flags & abi.CAP_WAVE) and
-            (pl.caps[w].flags & (abi.CAP_LANE | abi.CAP_REG | abi.CAP_REG2))]
-    assert n_def == n_all - len(keep)
+            (pl.caps[w].flags & (abi.CAP_REG | abi.CAP_REG2))]
+    assert keep and n_def == n_all - len(keep)
+    # the small-table corner carries CDR_CAP_REG too
+    assert all(pl.caps[w].flags & abi.CAP_REG for w in range(b.n_wfs) if pl.caps[w].flags & abi.CAP_REG0)
 
 
 def test_long_histories_get_wave_slices():
-    """CDR_PLAN_WAVE's long-history rule (cdr.h CDR_PLAN_NO_LONG): a lane-capable history
-    longer than max(CDR_LONG_MIN, CDR_LONG_FACTOR x lane events per resident slot) gets a
-    wave slice of its own; CDR_PLAN_NO_LONG keeps it in a lane slice."""
+    """CDR_PLAN_WAVE's long-history rule (cdr.h CDR_PLAN_NO_LONG): a register-table history
+    longer than T = max(CDR_LONG_MIN, CDR_LONG_FACTOR x lane events per resident slot) — T /
+    CDR_LONG_REG2_DIV for CDR_CAP_REG2 — gets a wave slice of its own; CDR_PLAN_NO_LONG
+    keeps it in a lane slice."""
     b = engine.synth_batch(4, 3000, seed=13)
     pl = engine.plan(b)
-    lanecap = abi.CAP_LANE | abi.CAP_REG | abi.CAP_REG2
+    regcap = abi.CAP_REG | abi.CAP_REG2
     flags = [pl.caps[w].flags for w in range(b.n_wfs)]
     lens = [int(b.wfs[w].ev_len) for w in range(b.n_wfs)]
-    lane_ev = sum(n for f, n in zip(flags, lens) if not (f & abi.CAP_WAVE) or (f & lanecap))
+    lane_ev = sum(n for f, n in zip(flags, lens) if not (f & abi.CAP_WAVE) or (f & regcap))
     thr = max(1024, 2 * (lane_ev // (64 * 2048)))
-    divergent = sum(1 for f in flags if (f & abi.CAP_WAVE) and not (f & lanecap))
-    long_ = sum(1 for f, n in zip(flags, lens) if (f & abi.CAP_WAVE) and (f & lanecap) and n > thr)
+    thr2 = max(512, thr // 2)
+    divergent = sum(1 for f in flags if (f & abi.CAP_WAVE) and not (f & regcap))
+    long_ = sum(1 for f, n in zip(flags, lens) if (f & abi.CAP_WAVE) and (f & regcap) and
+                n > (thr if f & abi.CAP_REG else thr2))
     assert long_ > 0
     assert engine.slice_kinds(b, pl, abi.PLAN_WAVE)[1] == divergent + long_
     assert engine.slice_kinds(b, pl, abi.PLAN_WAVE | abi.PLAN_NO_LONG)[1] == divergent
