@@ -280,7 +280,7 @@ CdrDevBatch = _S("cdr_dev_batch", [
     ("ev", CdrSlices), ("scratch", C.c_void_p), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
     ("n_wfs", u32), ("empty_uuid", u32), ("max_act_slots", u32), ("max_tim_slots", u32),
     ("n_fast_slices", u32), ("n_wave_slices", u32), ("n_reg_slices", u32), ("n_reg2_slices", u32),
-    ("n_reg0_slices", u32), ("_pad_reg0", u32),
+    ("n_reg0_slices", u32), ("_pad_reg0", u32), ("class_lo", u32 * 6), ("class_hi", u32 * 6),
     ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64), ("carry", C.c_void_p)])
 
 # ------------------------------------------------------------------ synth
@@ -341,6 +341,7 @@ EXPORTS = {
     "cdr_encode_blobs_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut),
                                      C.POINTER(CdrStrtab), C.c_void_p, C.c_void_p, u64, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),
+    "cdr_plan_class_ranges": (i32, [C.c_void_p, u32, C.c_void_p, C.c_void_p]),
     "cdr_compact_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
                                 C.c_void_p, C.c_void_p]),
     "cdr_checksum_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p, C.c_void_p]),

@@ -305,6 +305,7 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
     db.n_reg2_slices += (sflags[i] & CDR_SLICE_REG2) ? 1u : 0u;
     db.n_reg0_slices += (sflags[i] & CDR_SLICE_REG0) ? 1u : 0u;
   }
+  cdr_plan_class_ranges(sflags.data(), ns, db.class_lo, db.class_hi);
   db.ev.slice_scratch_off = (const uint64_t*)up(WS_SC_OFF, sc_off.data(), ns * 8ull);
   db.ev.slice_act_slots = (const uint32_t*)up(WS_SC_ACT, sc_act.data(), ns * 4ull);
   db.ev.slice_tim_slots = (const uint32_t*)up(WS_SC_TIM, sc_tim.data(), ns * 4ull);

@@ -480,6 +480,23 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
                             nullptr);
 }
 
+int cdr_plan_class_ranges(const uint32_t* slice_flags, uint32_t n_slices, uint32_t* lo, uint32_t* hi) {
+  if (!lo || !hi || (!slice_flags && n_slices)) return CDR_API_EINVAL;
+  for (int c = 0; c < 6; c++) lo[c] = hi[c] = 0;
+  for (uint32_t s = 0; s < n_slices; s++) {
+    const uint32_t f = slice_flags[s];
+    const int c = (f & CDR_SLICE_WAVE)   ? CDR_CLASS_WAVE
+                  : (f & CDR_SLICE_FAST) ? CDR_CLASS_FAST
+                  : (f & CDR_SLICE_REG0) ? CDR_CLASS_REG0
+                  : (f & CDR_SLICE_REG)  ? CDR_CLASS_REG
+                  : (f & CDR_SLICE_REG2) ? CDR_CLASS_REG2
+                                         : CDR_CLASS_GENERAL;
+    if (hi[c] == 0) lo[c] = s;
+    hi[c] = s + 1;
+  }
+  return CDR_API_OK;
+}
+
 int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n_slices, uint64_t* scratch_off,
                      uint32_t* act_slots, uint32_t* tim_slots, uint32_t* slice_flags, uint64_t* total_words,
                      uint32_t* n_fast) {

@@ -1319,6 +1319,7 @@ extern "C" int cdr_ingest_plan(cdr_ctx* ctx, const cdr_ingest_out* dec, const cd
     b.n_reg2_slices += (sflags[i] & CDR_SLICE_REG2) ? 1u : 0u;
     b.n_reg0_slices += (sflags[i] & CDR_SLICE_REG0) ? 1u : 0u;
   }
+  cdr_plan_class_ranges(sflags.data(), ns, b.class_lo, b.class_hi);
   b.n_fast_slices = n_fast;
   b.n_wave_slices = n_wave;
   b.cluster = meta->cluster;

@@ -494,6 +494,7 @@ struct cdr_launch {
   uint32_t la, lt;  // activity / user-timer working slots per lane held in LDS
   uint32_t fast;    // CDR_SLICE_FAST slices go to k_replay_fast (else every slice here)
   uint32_t reg;     // CDR_SLICE_REG slices go to k_replay_reg (else here)
+  uint32_t s0;      // slice of block 0 (the launch covers its kernel class's slice range)
 };
 #define AS4 __attribute__((address_space(4)))
 __device__ __forceinline__ const AS4 cdr_launch* KA() {
@@ -521,7 +522,7 @@ template <bool LDS, bool TASKS>
 __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu(CDR_WPE, 8))) void k_replay(
     cdr_launch L) {
   (void)L;  // read through KA()
-  const uint32_t s = blockIdx.x;
+  const uint32_t s = blockIdx.x + KA()->s0;
   const uint32_t lane = threadIdx.x;
   if (s >= KA()->B.ev.n_slices) return;
   // slice scalars (readfirstlane makes their uniformity visible, so the descriptor
@@ -1883,17 +1884,34 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
                        in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
-  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u};
+  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u, 0u};
+  // each kernel over its class's slice range (cdr_plan_class_ranges), or every slice
+  bool ranged = false;
+  for (int c = 0; c < 6; c++) ranged |= in->class_hi[c] > 0;
+  auto grid_of = [&](int cls, cdr_launch& Lc) {
+    Lc = L;
+    if (!ranged) return dim3(blocks);
+    const uint32_t lo = in->class_lo[cls], hi = in->class_hi[cls] < blocks ? in->class_hi[cls] : blocks;
+    Lc.s0 = lo < hi ? lo : 0u;
+    return dim3(lo < hi ? hi - lo : 0u);
+  };
+  cdr_launch Lw, Lr2, Lg, Lr0, Lf, Lr1;
+  const dim3 gw = grid_of(CDR_CLASS_WAVE, Lw), gr2 = grid_of(CDR_CLASS_REG2, Lr2), gg = grid_of(CDR_CLASS_GENERAL, Lg),
+             gr0 = grid_of(CDR_CLASS_REG0, Lr0), gf = grid_of(CDR_CLASS_FAST, Lf), gr1 = grid_of(CDR_CLASS_REG, Lr1);
   // kernel streams: each replay kernel class present gets a side stream of its own
   // (all forked from the caller's stream, so none is dispatched ahead of the others but
   // by priority), launched longest-first: the wave kernel (the batch's longest histories, one wave each, scalar-unit-
   // bound), the 12-activity register kernel (one wave per SIMD), the general kernel (the
   // few histories no specialised kernel takes), the small-table register kernel, the
   // fast kernel — so that no class's slices wait for another's kernel to finish
-  const bool reg1 = blocks && reg && in->n_reg_slices;
-  const bool reg0 = blocks && reg && in->n_reg0_slices;
-  const bool reg2 = blocks && reg && in->n_reg2_slices;
-  const bool wv = blocks && wave, gen = blocks && general, fst = blocks && fast;
+  const bool reg1 = blocks && reg && in->n_reg_slices && gr1.x;
+  const bool reg0 = blocks && reg && in->n_reg0_slices && gr0.x;
+  const bool reg2 = blocks && reg && in->n_reg2_slices && gr2.x;
+  const bool wv = blocks && wave && gw.x, fst = blocks && fast && gf.x;
+  // the general kernel also takes the fast / register slices whose kernels are off
+  const dim3 gg_all = (ranged && (!fast || !reg)) ? dim3(blocks) : gg;
+  if (ranged && (!fast || !reg)) Lg.s0 = 0;
+  const bool gen = blocks && general && gg_all.x;
   const bool on[cdr_ctx::N_SIDE] = {wv, reg2, gen, reg0, fst, reg1};
   int kinds = 0;
   for (bool o : on) kinds += o ? 1 : 0;
@@ -1904,40 +1922,40 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   for (int i = 0; i < cdr_ctx::N_SIDE; i++)
     if (fk[i]) HIPCHK(hipStreamWaitEvent(c->side[i], c->fork, 0));
   auto sx = [&](int i) { return fk[i] ? c->side[i] : st; };
-  if (wv) hipLaunchKernelGGL(k_replay_wave, dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, sx(0), L);
+  if (wv) hipLaunchKernelGGL(k_replay_wave, gw, dim3(CDR_SLICE_WIDTH), 0, sx(0), Lw);
   HIPCHK(hipGetLastError());
   if (reg2) {
     typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
-    hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), dim3(blocks),
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), L);
+    hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), gr2,
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), Lr2);
   }
   HIPCHK(hipGetLastError());
   if (gen) {
     if (tasks)
-      hipLaunchKernelGGL((k_replay<true, true>), dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, sx(2), L);
+      hipLaunchKernelGGL((k_replay<true, true>), gg_all, dim3(CDR_SLICE_WIDTH), lds, sx(2), Lg);
     else
-      hipLaunchKernelGGL((k_replay<true, false>), dim3(blocks), dim3(CDR_SLICE_WIDTH), lds, sx(2), L);
+      hipLaunchKernelGGL((k_replay<true, false>), gg_all, dim3(CDR_SLICE_WIDTH), lds, sx(2), Lg);
   }
   HIPCHK(hipGetLastError());
   if (gen && spill) {
     if (tasks)
-      hipLaunchKernelGGL((k_replay<false, true>), dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, sx(2), L);
+      hipLaunchKernelGGL((k_replay<false, true>), gg_all, dim3(CDR_SLICE_WIDTH), 0, sx(2), Lg);
     else
-      hipLaunchKernelGGL((k_replay<false, false>), dim3(blocks), dim3(CDR_SLICE_WIDTH), 0, sx(2), L);
+      hipLaunchKernelGGL((k_replay<false, false>), gg_all, dim3(CDR_SLICE_WIDTH), 0, sx(2), Lg);
   }
   HIPCHK(hipGetLastError());
   if (reg0) {  // the small-table variant, at 3 waves per SIMD
     typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
-    hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), dim3(blocks),
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), L);
+    hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), gr0,
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), Lr0);
   }
   HIPCHK(hipGetLastError());
-  if (fst) hipLaunchKernelGGL(k_replay_fast, dim3(blocks), dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), L);
+  if (fst) hipLaunchKernelGGL(k_replay_fast, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), Lf);
   HIPCHK(hipGetLastError());
   if (reg1) {
     typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
-    hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), dim3(blocks),
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), L);
+    hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), gr1,
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), Lr1);
   }
   HIPCHK(hipGetLastError());
   for (int i = 0; i < cdr_ctx::N_SIDE; i++)

@@ -115,6 +115,7 @@ class DeviceBatch:
         db.n_reg2_slices = self.n_reg2
         self.n_reg0 = int(((self.h_sflags & abi.SLICE_REG0) != 0).sum())
         db.n_reg0_slices = self.n_reg0
+        L.cdr_plan_class_ranges(self.h_sflags.ctypes.data, len(self.h_sflags), db.class_lo, db.class_hi)
         db.empty_uuid = meta.empty_uuid
         db.cluster = meta.cluster
         db.now_ns = meta.now_ns

@@ -223,6 +223,10 @@ typedef struct cdr_dev_batch {
   uint32_t n_reg2_slices; /* slices with CDR_SLICE_REG2 (cdr_plan_scratch) */
   uint32_t n_reg0_slices; /* slices with CDR_SLICE_REG0 (cdr_plan_scratch) */
   uint32_t _pad_reg0;
+  /* slice index range [class_lo[c], class_hi[c]) holding every slice of kernel class c
+   * (CDR_CLASS_*, cdr_plan_class_ranges): each replay kernel is launched over its range
+   * only; all zero = unknown, every kernel is launched over every slice */
+  uint32_t class_lo[6], class_hi[6];
   cdr_cluster_meta cluster;
   int64_t now_ns;
   uint64_t uuid_seed;
@@ -273,6 +277,15 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
  * cdr_plan_slices_ex, is kept and such slices get no scratch); returns the total words via
  * *total_words and the number of CDR_SLICE_FAST slices via *n_fast (nullable).
  * Outputs sized [n_slices]; pass NULL outputs to query the totals only. */
+/* Kernel classes of the slices (by their CDR_SLICE_* flags) and the index range each
+ * class's slices span: lo[c] = first, hi[c] = last + 1 (0, 0 for an absent class).  The
+ * planner above puts a class's slices next to each other, so a range holds only its
+ * class's slices; the kernels check the flags, so any order stays correct. */
+enum cdr_kernel_class {
+  CDR_CLASS_FAST = 0, CDR_CLASS_REG0 = 1, CDR_CLASS_REG = 2, CDR_CLASS_REG2 = 3, CDR_CLASS_WAVE = 4,
+  CDR_CLASS_GENERAL = 5
+};
+int cdr_plan_class_ranges(const uint32_t* slice_flags, uint32_t n_slices, uint32_t* lo, uint32_t* hi);
 int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n_slices, uint64_t* scratch_off,
                      uint32_t* act_slots, uint32_t* tim_slots, uint32_t* slice_flags, uint64_t* total_words,
                      uint32_t* n_fast);
