@@ -1806,10 +1806,23 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
   bool sides_ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
-  for (int i = 0; i < cdr_ctx::N_SIDE; i++)
-    sides_ok = sides_ok &&
-               hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, i < 3 ? prio_hi : prio_lo) == hipSuccess &&
-               hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming) == hipSuccess;
+  // experiment (CDR_WAVE_CUS=k): the wave class on every k-th CU alone, the others elsewhere
+  int wave_cus = 0;
+  if (const char* e = std::getenv("CDR_WAVE_CUS")) wave_cus = std::atoi(e);
+  hipDeviceProp_t prop{};
+  const int n_cu = (wave_cus > 1 && hipGetDeviceProperties(&prop, device) == hipSuccess) ? prop.multiProcessorCount : 0;
+  for (int i = 0; i < cdr_ctx::N_SIDE; i++) {
+    if (n_cu > 0) {
+      std::vector<uint32_t> m((n_cu + 31) / 32, 0u);
+      for (int cu = 0; cu < n_cu; cu++)
+        if ((cu % wave_cus == 0) == (i == 0)) m[cu / 32] |= 1u << (cu % 32);
+      sides_ok = sides_ok && hipExtStreamCreateWithCUMask(&c->side[i], (uint32_t)m.size(), m.data()) == hipSuccess;
+    } else {
+      sides_ok = sides_ok &&
+                 hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, i < 3 ? prio_hi : prio_lo) == hipSuccess;
+    }
+    sides_ok = sides_ok && hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming) == hipSuccess;
+  }
   if (!sides_ok)
     c->concurrent = 0;
   if (const char* e = std::getenv("CDR_SERIAL_KERNELS")) c->concurrent = c->concurrent && e[0] == '0';
