@@ -302,6 +302,8 @@ def main():
     ap.add_argument("--wave-all", action="store_true", help="every divergent history on a wave slice")
     ap.add_argument("--no-refresh", action="store_true", help="skip the refreshTasks / row-encoder side measurements")
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size GPU == oracle digest check")
+    ap.add_argument("--no-cls", action="store_true",
+                    help="register-table slices on k_replay_reg alone (no class-sorted blocks, k_replay_cls off)")
     args = ap.parse_args()
 
     import torch
@@ -323,7 +325,11 @@ def main():
     total = args.wfs * world
     mine, load = assign_shards(total, world, rank, workflow_weights(args.config, total, args.seed))
     log(f"[rank {rank}] {len(mine)} of {total} workflows (shard->GPU greedy over {NUM_SHARDS} shards)")
-    db = DeviceBatch(torch, args.config, mine, args.seed, plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0))
+    db = DeviceBatch(torch, args.config, mine, args.seed,
+                     plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0),
+                     ctx_for_cls=None if args.no_cls else ctx)
+    if args.no_cls:
+        L.cdr_set_cls_path(ctx, 0)
     log(f"[rank {rank}] {db.n_fast} of {db.info.n_slices} slices on the fast-path kernel, {db.n_wave} wave slices")
     log(f"[rank {rank}] packed {db.n_events:,} events in {db.pack_s:.2f}s (host SoA), H2D {db.h2d_s:.2f}s "
         f"({db.in_bytes / 1e9:.2f} GB in, {db.out_bytes / 1e9:.2f} GB out buffers)")
@@ -415,7 +421,9 @@ def main():
         "refresh": refresh,
         "encode": encode,
         "host": {"soa_pack_s": db.pack_s, "h2d_s": db.h2d_s,
-                 "h2d_gbs": db.in_bytes / max(db.h2d_s, 1e-9) / 1e9},
+                 "h2d_gbs": db.in_bytes / max(db.h2d_s, 1e-9) / 1e9,
+                 # class-sorted blocks of the register-table slices (device packing step, once per batch)
+                 "cls_build_s": db.cls_s, "cls_rows": db.cls_rows},
         "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_workflows": tot_ok,
         "parity_checked": bool(parity) and parity["mismatched_entries_all_ranks"] == 0,
         "parity": parity,

@@ -281,7 +281,8 @@ CdrDevBatch = _S("cdr_dev_batch", [
     ("n_wfs", u32), ("empty_uuid", u32), ("max_act_slots", u32), ("max_tim_slots", u32),
     ("n_fast_slices", u32), ("n_wave_slices", u32), ("n_reg_slices", u32), ("n_reg2_slices", u32),
     ("n_reg0_slices", u32), ("_pad_reg0", u32), ("class_lo", u32 * 6), ("class_hi", u32 * 6),
-    ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64), ("carry", C.c_void_p)])
+    ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64), ("carry", C.c_void_p),
+    ("cls_slab", C.c_void_p), ("cls_row0", C.c_void_p), ("cls_rows", C.c_void_p)])
 
 # ------------------------------------------------------------------ synth
 CdrSynthParams = _S("cdr_synth_params", [
@@ -296,6 +297,8 @@ CdrSynthSizes = _S("cdr_synth_sizes", [("n_events", u64), ("n_entries", u32), ("
 CdrSynthPlanInfo = _S("cdr_synth_plan_info", [
     ("n_events", u64), ("n_entries", u32), ("n_slices", u32), ("n_rows", u64), ("arena_words", u64),
     ("n_kvs", u64), ("n_rps", u64), ("totals", CdrTotals)])
+
+CLS_RETRY = 0x7FFF  # k_replay_cls's hand-on code (cdr_set_cls_path mode 2 only)
 
 MIRRORS = {
     "cdr_event": CdrEvent, "cdr_wf_desc": CdrWfDesc, "cdr_cluster_meta": CdrClusterMeta, "cdr_batch": CdrBatch,
@@ -322,6 +325,9 @@ EXPORTS = {
                                C.POINTER(u64), C.c_void_p]),
     "cdr_set_fast_path": (i32, [C.c_void_p, i32]),
     "cdr_set_reg_path": (i32, [C.c_void_p, i32]),
+    "cdr_set_cls_path": (i32, [C.c_void_p, i32]),
+    "cdr_cls_plan_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cdr_cls_pack_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.c_void_p]),
     "cdr_set_plan_mode": (i32, [C.c_void_p, u32]),
     "cdr_pack_slices": (i32, [C.POINTER(CdrBatch), C.POINTER(CdrSlices), i32]),
     "cdr_create": (C.c_void_p, [i32, C.c_void_p]),

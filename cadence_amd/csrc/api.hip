@@ -370,6 +370,36 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
     (void)hipStreamSynchronize(st);  // no copy may still read the host vectors
     return oom ? CDR_API_ENOMEM : CDR_API_EDEVICE;
   }
+  // class-sorted blocks of the register-table slices (k_replay_cls): size pass, the
+  // total rows back to the host, write pass
+  if (ctx->cls && ctx->reg && ctx->fast && !tasks && db.n_reg_slices + db.n_reg2_slices + db.n_reg0_slices > 0 &&
+      b->cluster.n_clusters <= (int)CDR_REG_NCL) {
+    uint32_t* crows = (uint32_t*)cdr_ws_get(ctx, WS_CLS_ROWS, ns * 16ull);
+    uint64_t* crow0 = (uint64_t*)cdr_ws_get(ctx, WS_CLS_ROW0, (ns + 1) * 8ull);
+    if (!crows || !crow0) {
+      (void)hipStreamSynchronize(st);
+      return CDR_API_ENOMEM;
+    }
+    uint64_t total = 0;
+    rc = cdr_cls_plan_async(ctx, &db, crows, crow0, st);
+    if (rc == CDR_API_OK && (hipMemcpyAsync(&total, crow0 + ns, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                             hipStreamSynchronize(st) != hipSuccess))
+      rc = CDR_API_EDEVICE;
+    if (rc != CDR_API_OK) {
+      (void)hipStreamSynchronize(st);
+      return rc;
+    }
+    uint8_t* cslab = (uint8_t*)cdr_ws_get(ctx, WS_CLS_SLAB, total ? total * CDR_ROW_BYTES : 8);
+    if (!cslab) return CDR_API_ENOMEM;
+    db.cls_slab = cslab;
+    db.cls_row0 = crow0;
+    db.cls_rows = crows;
+    rc = cdr_cls_pack_async(ctx, &db, st);
+    if (rc != CDR_API_OK) {
+      (void)hipStreamSynchronize(st);
+      return rc;
+    }
+  }
   if (refresh) {  // the replay itself emits no stateBuilder tasks
     cdr_out rout = dout;
     rout.transfer = rout.timer_tasks = nullptr;

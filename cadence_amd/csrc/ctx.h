@@ -23,6 +23,7 @@ enum cdr_ws_slot {
   WS_CY_CANCEL, WS_CY_SIGNAL, WS_CY_RP, WS_CY_SA, WS_CY_DESC,
   WS_O_RESULT, WS_O_EXEC, WS_O_REPL, WS_O_VH, WS_O_ACT, WS_O_TIMER, WS_O_CHILD, WS_O_CANCEL, WS_O_SIGNAL,
   WS_O_RP, WS_O_SA, WS_O_XFER, WS_O_TTASK, WS_O_NTASKS, WS_O_LD,
+  WS_CLS_ROWS, WS_CLS_ROW0, WS_CLS_SLAB,  // class-sorted blocks (cdr_cls_plan_async / cdr_cls_pack_async)
   // cdr_ingest_decode (ingest.hip)
   WS_IN_COUNTS, WS_IN_BASES, WS_IN_STATUS, WS_IN_ESTATUS, WS_IN_EVOFF, WS_IN_TKEY, WS_IN_TVAL, WS_IN_TREF,
   WS_IN_TLEN, WS_IN_SKEY, WS_IN_SIDX, WS_IN_SKEY2, WS_IN_SIDX2, WS_IN_TMP, WS_IN_DOM, WS_IN_EVENTS, WS_IN_KVS,
@@ -57,6 +58,7 @@ struct cdr_ctx {
   int device;
   int fast = 1;                        // cdr_set_fast_path
   int reg = 1;                         // cdr_set_reg_path
+  int cls = 1;                         // cdr_set_cls_path
   uint32_t plan_mode = CDR_PLAN_WAVE;  // cdr_set_plan_mode
   hipEvent_t ev[4];
   bool timed;

@@ -495,7 +495,10 @@ struct cdr_launch {
   uint32_t fast;    // CDR_SLICE_FAST slices go to k_replay_fast (else every slice here)
   uint32_t reg;     // CDR_SLICE_REG slices go to k_replay_reg (else here)
   uint32_t s0;      // slice of block 0 (the launch covers its kernel class's slice range)
+  uint32_t retry;   // k_replay_reg: only the entries k_replay_cls left CLS_RETRY
 };
+// result code k_replay_cls leaves on an entry it hands to k_replay_reg (never returned)
+#define CLS_RETRY 0x7FFF
 #define AS4 __attribute__((address_space(4)))
 __device__ __forceinline__ const AS4 cdr_launch* KA() {
   const AS4 cdr_launch* p = (const AS4 cdr_launch*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1683,6 +1686,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
 #include "replay_fast.inc"
 #include "replay_wave.inc"
 #include "replay_reg.inc"
+#include "replay_cls.inc"
 
 // Per-workflow table epilogue: move live rows to the front in key order (the
 // canonical order of the Go maps' keys), sort the SearchAttributes map by key, and
@@ -1841,6 +1845,35 @@ int cdr_set_fast_path(cdr_ctx* c, int enable) {
   return old;
 }
 
+int cdr_set_cls_path(cdr_ctx* c, int enable) {
+  if (!c) return CDR_API_EINVAL;
+  const int old = c->cls;
+  c->cls = enable == 2 ? 2 : (enable ? 1 : 0);
+  return old;
+}
+
+int cdr_cls_plan_async(cdr_ctx* c, const cdr_dev_batch* in, uint32_t* cls_rows, uint64_t* cls_row0, void* stream) {
+  if (!c || !in || !cls_rows || !cls_row0) return CDR_API_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(c->device));
+  const uint32_t ns = in->ev.n_slices;
+  if (ns) hipLaunchKernelGGL(k_cls_count, dim3(ns), dim3(CDR_SLICE_WIDTH), 0, st, *in, cls_rows, cls_row0);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_cls_scan, dim3(1), dim3(1024), 0, st, cls_row0, ns);
+  HIPCHK(hipGetLastError());
+  return CDR_API_OK;
+}
+
+int cdr_cls_pack_async(cdr_ctx* c, const cdr_dev_batch* in, void* stream) {
+  if (!c || !in || !in->cls_slab || !in->cls_row0 || !in->cls_rows) return CDR_API_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(c->device));
+  if (in->ev.n_slices)
+    hipLaunchKernelGGL(k_cls_fill, dim3(in->ev.n_slices), dim3(CDR_SLICE_WIDTH), 0, st, *in);
+  HIPCHK(hipGetLastError());
+  return CDR_API_OK;
+}
+
 int cdr_set_reg_path(cdr_ctx* c, int enable) {
   if (!c) return CDR_API_EINVAL;
   const int old = c->reg;
@@ -1890,6 +1923,13 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   // register-table kernel: LastReplicationInfo kept for clusters < CDR_REG_NCL only
   const bool reg = c->fast && c->reg && in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices > 0 && !tasks &&
                    in->cluster.n_clusters <= (int)CDR_REG_NCL;
+  // class-decomposed replay of the register-table slices (their class-sorted blocks)
+  const bool cls = reg && c->cls && in->cls_slab && in->cls_row0 && in->cls_rows;
+  const bool cls_fb = c->cls != 2;  // 2 (tests): no k_replay_reg pass for the CLS_RETRY entries
+  auto retry_of = [](cdr_launch x) {
+    x.retry = 1u;
+    return x;
+  };
   const bool wave = in->n_wave_slices > 0;
   const bool general = (fast ? in->n_fast_slices : 0u) +
                            (reg ? in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices : 0u) +
@@ -1939,8 +1979,14 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   HIPCHK(hipGetLastError());
   if (reg2) {
     typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
-    hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), gr2,
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), Lr2);
+    if (cls) {
+      typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LC;
+      hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_CLS2>), gr2,
+                         dim3(CDR_SLICE_WIDTH), LC::bytes, sx(1), Lr2);
+    }
+    if (!cls || cls_fb)
+      hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), gr2,
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), cls ? retry_of(Lr2) : Lr2);
   }
   HIPCHK(hipGetLastError());
   if (gen) {
@@ -1959,16 +2005,28 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   HIPCHK(hipGetLastError());
   if (reg0) {  // the small-table variant, at 3 waves per SIMD
     typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
-    hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), gr0,
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), Lr0);
+    if (cls) {
+      typedef ClsLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LC;
+      hipLaunchKernelGGL((k_replay_cls<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_CLS0>), gr0,
+                         dim3(CDR_SLICE_WIDTH), LC::bytes, sx(3), Lr0);
+    }
+    if (!cls || cls_fb)
+      hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), gr0,
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), cls ? retry_of(Lr0) : Lr0);
   }
   HIPCHK(hipGetLastError());
   if (fst) hipLaunchKernelGGL(k_replay_fast, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), Lf);
   HIPCHK(hipGetLastError());
   if (reg1) {
     typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
-    hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), gr1,
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), Lr1);
+    if (cls) {
+      typedef ClsLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LC;
+      hipLaunchKernelGGL((k_replay_cls<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_CLS>), gr1,
+                         dim3(CDR_SLICE_WIDTH), LC::bytes, sx(5), Lr1);
+    }
+    if (!cls || cls_fb)
+      hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), gr1,
+                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), cls ? retry_of(Lr1) : Lr1);
   }
   HIPCHK(hipGetLastError());
   for (int i = 0; i < cdr_ctx::N_SIDE; i++)

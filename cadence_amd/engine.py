@@ -345,6 +345,13 @@ class Engine:
         """CDR_PLAN_* bits of cdr_replay_batch's slicing; returns the previous mode."""
         return int(abi.lib().cdr_set_plan_mode(self.ctx, mode))
 
+    def set_cls(self, enable) -> int:
+        """Replay register-table slices with the class-decomposed kernel (k_replay_cls,
+        default; cdr_replay_batch builds their class-sorted blocks) or with k_replay_reg
+        alone; 2 (tests): k_replay_cls without the k_replay_reg pass for the entries it
+        hands on (result code CLS_RETRY).  Returns the previous setting."""
+        return int(abi.lib().cdr_set_cls_path(self.ctx, 2 if enable == 2 else (1 if enable else 0)))
+
     def set_fast_path(self, enable: bool) -> bool:
         """Route sequential-activity slices to the fast-path kernel (default) or replay
         everything with the general kernel; returns the previous setting."""

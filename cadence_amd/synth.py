@@ -34,7 +34,8 @@ RESULT_DTYPE = np.dtype([("code", "<i4"), ("flags", "<u4"), ("fid", "<i8"), ("fi
 class DeviceBatch:
     """Synthetic batch generated straight into the sliced layout, uploaded to HBM."""
 
-    def __init__(self, torch, config, index_map, seed, target_len=0, plan_mode=abi.PLAN_WAVE):
+    def __init__(self, torch, config, index_map, seed, target_len=0, plan_mode=abi.PLAN_WAVE, ctx_for_cls=None,
+                 cls=True):
         L = abi.lib()
         self.torch = torch
         self.index_map = index_map
@@ -121,6 +122,10 @@ class DeviceBatch:
         db.now_ns = meta.now_ns
         db.uuid_seed = meta.uuid_seed
         self.db = db
+        self.cls_s = 0.0
+        self.cls_rows = 0
+        if cls and ctx_for_cls and self.n_reg + self.n_reg2 + self.n_reg0 > 0:
+            self.build_cls(ctx_for_cls)
         tot = info.totals
         out = abi.CdrOut()
         sizes = {"result": info.n_entries * C.sizeof(abi.CdrWfResult),
@@ -144,6 +149,32 @@ class DeviceBatch:
         types = abi.slab_columns(self.h_slab, self.h_row0, self.h_slen, ("type_flags",))["type_flags"] & 0xFF
         self.type_counts = np.bincount(types, minlength=256)
         self.n_events = int(self.type_counts[:abi.EV["UpsertWorkflowSearchAttributes"] + 1].sum())
+
+    def build_cls(self, ctx):
+        """Class-sorted blocks of the register-table slices (cdr_cls_plan_async +
+        cdr_cls_pack_async, replay_cls.inc): a packing step, done once per batch and timed
+        apart from the replay (cls_s)."""
+        torch, L, db = self.torch, abi.lib(), self.db
+        ns = self.info.n_slices
+        stream = torch.cuda.current_stream().cuda_stream
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rows_t = torch.zeros(max(1, ns * 4) * 4, dtype=torch.uint8, device="cuda")
+        row0_t = torch.zeros((ns + 1) * 8, dtype=torch.uint8, device="cuda")
+        rc = L.cdr_cls_plan_async(ctx, C.byref(db), C.c_void_p(rows_t.data_ptr()), C.c_void_p(row0_t.data_ptr()),
+                                  C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"cdr_cls_plan_async rc={rc}")
+        total = int(row0_t.view(torch.int64)[ns].item())
+        slab_t = torch.empty(max(8, total * 64 * abi.EL_BYTES), dtype=torch.uint8, device="cuda")
+        db.cls_slab, db.cls_row0, db.cls_rows = slab_t.data_ptr(), row0_t.data_ptr(), rows_t.data_ptr()
+        rc = L.cdr_cls_pack_async(ctx, C.byref(db), C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"cdr_cls_pack_async rc={rc}")
+        torch.cuda.synchronize()
+        self.cls_s = time.perf_counter() - t0
+        self.cls_rows = total
+        self.keep += [rows_t, row0_t, slab_t]
 
     def builders(self) -> np.ndarray:
         """cdr_wf_desc.builder of every entry."""

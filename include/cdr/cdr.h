@@ -233,7 +233,36 @@ typedef struct cdr_dev_batch {
   /* device copy of the batch's cdr_carry (pointers into device memory), or NULL; its
    * entries replay with the general kernel (cdr_plan_caps clears CDR_CAP_FAST/WAVE) */
   const cdr_carry* carry;
+  /* class-sorted copy of the register-table slices (cdr_cls_plan_async +
+   * cdr_cls_pack_async), or NULL: slice s's block starts at row cls_row0[s] of cls_slab
+   * (standard CDR_ROW_BYTES rows) and holds its lanes' W, activity, timer and external
+   * events in four regions of cls_rows[4 s + 0..3] rows (CDR_CLS_*) */
+  const uint8_t* cls_slab;
+  const uint64_t* cls_row0; /* [n_slices + 1], exclusive scan of the blocks' rows */
+  const uint32_t* cls_rows; /* [n_slices * 4] */
 } cdr_dev_batch;
+
+/* Class-sorted blocks (replay_cls.inc).  Every register-table slice (CDR_SLICE_REG /
+ * REG2 / REG0) can carry a second copy of its events, permuted per lane into four
+ * class regions aligned across the slice's 64 lanes: W (decision and workflow events),
+ * activity events, user-timer events, external (child / request-cancel / signal)
+ * events, each region in history order; MarkerRecorded, CancelTimerFailed and
+ * RequestCancelActivityTaskFailed (no state of their own) are left out, and a lane with
+ * fewer events of a class than the slice's maximum gets CDR_EV_PAD rows there.  Columns
+ * are the standard ones except: the task_id column holds the annotation
+ * CDR_CLS_ANN(k, k - k0, d) — k the event's index in its history, k0 the index of its
+ * call's first event, d = event_id - NextEventID at its call (0xFFFFFFFF when that does
+ * not fit) — and type_flags' bits 21 / 22 mean "event_id not needed" / "version not
+ * needed or equal to the previous W event's".  The replay reads them instead of the
+ * original rows for the entity FSMs (one class per step), and the original rows for the
+ * call structure and the version bookkeeping. */
+#define CDR_CLS_W 0
+#define CDR_CLS_A 1
+#define CDR_CLS_T 2
+#define CDR_CLS_X 3
+#define CDR_SEF_CLS_NO_ID (1u << 21)
+#define CDR_SEF_CLS_VER_SAME (1u << 22)
+#define CDR_CLS_ANN(k, dk, d) ((uint64_t)(k) | ((uint64_t)(dk) << 20) | ((uint64_t)(d) << 32))
 
 /* ------------------------------------------------------------ host planning */
 
@@ -323,6 +352,24 @@ int cdr_set_fast_path(cdr_ctx* ctx, int enable);
 /* Route CDR_SLICE_REG slices to k_replay_reg (default 1) or to the general kernel (0);
  * returns the old value. */
 int cdr_set_reg_path(cdr_ctx* ctx, int enable);
+/* Replay register-table slices that carry a class-sorted block (cdr_dev_batch.cls_slab)
+ * with the class-decomposed kernel k_replay_cls (default 1; entries it leaves
+ * CLS_RETRY go through k_replay_reg) or with k_replay_reg alone (0); 2 (tests only):
+ * k_replay_cls with no k_replay_reg pass, so an entry it hands on keeps the internal
+ * result code 0x7FFF.  The host-buffer calls build the blocks when this is on.  Returns
+ * the old value. */
+int cdr_set_cls_path(cdr_ctx* ctx, int enable);
+
+/* Size pass of the class-sorted blocks (see cdr_dev_batch.cls_slab): cls_rows[4 s + c]
+ * (device, n_slices * 4) = the rows of each class region of every register-table slice
+ * (0 for the others) and cls_row0[0..n_slices] (device, n_slices + 1) their exclusive
+ * scan; the caller reads the total, cls_row0[n_slices], and allocates cls_slab at
+ * total * CDR_ROW_BYTES bytes.  Asynchronous. */
+int cdr_cls_plan_async(cdr_ctx* ctx, const cdr_dev_batch* in, uint32_t* cls_rows, uint64_t* cls_row0,
+                       void* stream);
+/* Write pass: the class-sorted blocks into in->cls_slab at in->cls_row0 / cls_rows (from
+ * cdr_cls_plan_async on the same batch).  Asynchronous. */
+int cdr_cls_pack_async(cdr_ctx* ctx, const cdr_dev_batch* in, void* stream);
 
 /* Slicing mode of cdr_replay_batch's planning (CDR_PLAN_*; default CDR_PLAN_WAVE).
  * Returns the previous mode. */

@@ -1,0 +1,93 @@
+"""Class-decomposed register-table replay (k_replay_cls, replay_cls.inc) vs the oracle.
+
+k_replay_cls replays each register-table slice from its class-sorted block and hands
+every entry it does not replay itself (errors, panics, a second Started, ...) to
+k_replay_reg.  The default path (both kernels) is covered by every parity test; here
+the class kernel runs ALONE (cdr_set_cls_path mode 2: entries it hands on keep the
+internal code CLS_RETRY), so that an entry it did replay cannot hide behind the
+fallback: every entry it did not hand on must equal the oracle field by field, and on
+clean batches it must hand on none.
+"""
+import re
+
+import pytest
+
+from cadence_amd import abi, engine
+
+pytestmark = pytest.mark.gpu
+
+
+def _cls_alone(eng, batch):
+    old = eng.set_cls(2)
+    try:
+        return eng.replay(batch)
+    finally:
+        eng.set_cls(old)
+
+
+def _split(batch, got, ref):
+    retried = {w for w in range(batch.n_wfs) if got.result[w].code == abi.CLS_RETRY}
+    # a handed-on entry's continue-as-new run is left CDR_NOT_APPLIED by k_finalize
+    retried |= {w for w in range(batch.n_wfs) if batch.wfs[w].parent in retried}
+    bad = engine.compare(batch, got, ref, limit=10 ** 9)
+    wrong = [b for b in bad if int(re.match(r"wf (\d+):", b).group(1)) not in retried]
+    return retried, wrong
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 5, 0])
+def test_cls_alone_clean(engine_gpu, cfg):
+    import oracle
+    b = engine.synth_batch(cfg, 1500, seed=0x5EED0200 + cfg)
+    ref = oracle.replay(b)
+    got = _cls_alone(engine_gpu, b)
+    retried, wrong = _split(b, got, ref)
+    assert not wrong, "\n".join(wrong[:10])
+    assert not retried, sorted(retried)[:10]  # clean: nothing handed on
+
+
+@pytest.mark.parametrize("cfg", [0, 3, 4, 5])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_cls_alone_faults(engine_gpu, cfg, seed):
+    """Injected faults: the class kernel hands the failing entries on; the rest match."""
+    import oracle
+    b = engine.synth_batch(cfg, 800, seed=seed * 7000 + cfg, error_rate=0.3)
+    ref = oracle.replay(b)
+    got = _cls_alone(engine_gpu, b)
+    retried, wrong = _split(b, got, ref)
+    assert not wrong, "\n".join(wrong[:10])
+    if cfg in (3, 4, 5):  # the class kernel ran (and handed its failing entries on)
+        assert retried, "no entry handed on: k_replay_cls did not run"
+    # and with k_replay_reg behind it, everything matches
+    bad = engine.compare(b, engine_gpu.replay(b), ref)
+    assert not bad, "\n".join(bad[:10])
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 5])
+def test_cls_on_off_equal(engine_gpu, cfg):
+    """The same batch with the class kernel on and off: identical outputs."""
+    b = engine.synth_batch(cfg, 1000, seed=0x5EED0300 + cfg, error_rate=0.05)
+    on = engine_gpu.replay(b)
+    old = engine_gpu.set_cls(False)
+    try:
+        off = engine_gpu.replay(b)
+    finally:
+        engine_gpu.set_cls(old)
+    bad = engine.compare(b, on, off)
+    assert not bad, "\n".join(bad[:10])
+
+
+def test_cls_long_and_2dc(engine_gpu):
+    """Register-table entries with long histories (NO_LONG keeps them in lane slices) and
+    every builder."""
+    import oracle
+    for builder in (abi.BUILDER_LOCAL, abi.BUILDER_2DC, abi.BUILDER_NDC):
+        b = engine.synth_batch(3, 300, seed=4242 + builder, builder=builder, target_len=900)
+        ref = oracle.replay(b)
+        old = engine_gpu.set_plan_mode(abi.PLAN_WAVE | abi.PLAN_NO_LONG)
+        try:
+            got = _cls_alone(engine_gpu, b)
+        finally:
+            engine_gpu.set_plan_mode(old)
+        retried, wrong = _split(b, got, ref)
+        assert not wrong, f"builder {builder}: " + "\n".join(wrong[:10])
+        assert not retried - {w for w in range(b.n_wfs) if ref.result[w].code != abi.OK}

@@ -21,6 +21,13 @@ def _check(batch, eng, both_paths=False, lanes=True):
     got = eng.replay(batch)
     bad = engine.compare(batch, got, ref)
     assert not bad, "default routing: " + "\n".join(bad[:10])
+    old = eng.set_cls(False)  # register-table slices on k_replay_reg alone
+    try:
+        got = eng.replay(batch)
+    finally:
+        eng.set_cls(old)
+    bad = engine.compare(batch, got, ref)
+    assert not bad, "no class-sorted blocks: " + "\n".join(bad[:10])
     old = eng.set_plan_mode(abi.PLAN_WAVE | abi.PLAN_WAVE_ALL)  # every divergent history on a wave
     try:
         got = eng.replay(batch)

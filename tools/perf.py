@@ -26,16 +26,26 @@ def main():
     ap.add_argument("--no-wave", action="store_true", help="plan divergent histories into lane slices")
     ap.add_argument("--wave-all", action="store_true", help="every divergent history on a wave slice")
     ap.add_argument("--no-reg", action="store_true", help="register-table slices on the general kernel")
+    ap.add_argument("--ab-cls", action="store_true",
+                    help="each lib twice: class-decomposed register slices (k_replay_cls) on, then off")
     args = ap.parse_args()
     import torch
     from cadence_amd.synth import DeviceBatch
     torch.cuda.set_device(0)
     idx = np.arange(args.wfs, dtype=np.uint32)
+    bctx = abi.lib().cdr_create(0, None)
     db = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config,
-                           plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0))
+                     plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0),
+                     ctx_for_cls=bctx)
+    print(json.dumps({"cls_build_s": round(db.cls_s, 4), "cls_rows": db.cls_rows, "rows": db.info.n_rows}), flush=True)
     stream = torch.cuda.current_stream().cuda_stream
     libs = [(p, abi.load(p)) for p in args.libs]
+    if args.ab_cls:
+        libs = [(p + tag, L) for p, L in libs for tag in ("", "#nocls")]
     ctxs = [L.cdr_create(0, None) for _, L in libs]
+    for (p, L), c in zip(libs, ctxs):
+        if p.endswith("#nocls"):
+            L.cdr_set_cls_path(c, 0)
     if args.no_reg:
         for (_, L), c in zip(libs, ctxs):
             L.cdr_set_reg_path(c, 0)
