@@ -499,6 +499,9 @@ struct cdr_launch {
 };
 // result code k_replay_cls leaves on an entry it hands to k_replay_reg (never returned)
 #define CLS_RETRY 0x7FFF
+// result flag k_replay_cls sets when its pending rows are already dense and in key
+// order (k_tables skips their sort and clears it; never returned)
+#define RF_ROWS_SORTED 0x80000000u
 #define AS4 __attribute__((address_space(4)))
 __device__ __forceinline__ const AS4 cdr_launch* KA() {
   const AS4 cdr_launch* p = (const AS4 cdr_launch*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1697,11 +1700,15 @@ __global__ __launch_bounds__(256) void k_tables(cdr_dev_batch B, cdr_out O) {
   cdr_wf_result& r = O.result[w];
   if (r.code != CDR_OK) return;
   const cdr_wf_caps& cp = B.caps[w];
-  r.n_activity = compact_sorted(O.act + cp.act_off, r.n_activity, ActKey{});
-  r.n_timer = compact_sorted(O.timer + cp.timer_off, r.n_timer, TimerKey{});
-  r.n_child = compact_sorted(O.child + cp.child_off, r.n_child, ChildKey{});
-  r.n_cancel = compact_sorted(O.cancel + cp.cancel_off, r.n_cancel, CancelKey{});
-  r.n_signal = compact_sorted(O.signal + cp.signal_off, r.n_signal, SignalKey{});
+  if (r.flags & RF_ROWS_SORTED) {  // k_replay_cls wrote its rows dense and in key order
+    r.flags &= ~RF_ROWS_SORTED;
+  } else {
+    r.n_activity = compact_sorted(O.act + cp.act_off, r.n_activity, ActKey{});
+    r.n_timer = compact_sorted(O.timer + cp.timer_off, r.n_timer, TimerKey{});
+    r.n_child = compact_sorted(O.child + cp.child_off, r.n_child, ChildKey{});
+    r.n_cancel = compact_sorted(O.cancel + cp.cancel_off, r.n_cancel, CancelKey{});
+    r.n_signal = compact_sorted(O.signal + cp.signal_off, r.n_signal, SignalKey{});
+  }
   cdr_kv* sa = O.sa + cp.sa_off;
   const uint32_t n = r.n_search_attr;
   for (uint32_t a = 1; a < n; a++) {
