@@ -234,11 +234,13 @@ SLICE_FAST = 0x1
 SLICE_WAVE = 0x2
 SLICE_REG = 0x4
 SLICE_REG2 = 0x8
+SLICE_PAR = 0x20
 SLICE_REG0 = 0x10
 CAP_FAST = 0x1
 CAP_WAVE = 0x2
 PLAN_WAVE = 0x1
 PLAN_WAVE_ALL = 0x2  # with PLAN_WAVE: lane-friendly (CAP_LANE) entries on the wave kernel too
+PLAN_PAR = 0x8  # with PLAN_WAVE: long register-table histories to CDR_SLICE_PAR lane slices (CDR_PLAN_PAR)
 PLAN_NO_LONG = 0x4  # with PLAN_WAVE: keep long lane-capable histories in lane slices (CDR_PLAN_NO_LONG)
 CAP_LANE = 0x4
 CAP_REG = 0x8
@@ -280,7 +282,7 @@ CdrDevBatch = _S("cdr_dev_batch", [
     ("ev", CdrSlices), ("scratch", C.c_void_p), ("wfs", C.c_void_p), ("caps", C.c_void_p), ("kvs", C.c_void_p), ("rps", C.c_void_p),
     ("n_wfs", u32), ("empty_uuid", u32), ("max_act_slots", u32), ("max_tim_slots", u32),
     ("n_fast_slices", u32), ("n_wave_slices", u32), ("n_reg_slices", u32), ("n_reg2_slices", u32),
-    ("n_reg0_slices", u32), ("_pad_reg0", u32), ("class_lo", u32 * 6), ("class_hi", u32 * 6),
+    ("n_reg0_slices", u32), ("n_par_slices", u32), ("class_lo", u32 * 6), ("class_hi", u32 * 6),
     ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64), ("carry", C.c_void_p),
     ("cls_slab", C.c_void_p), ("cls_row0", C.c_void_p), ("cls_rows", C.c_void_p)])
 

@@ -304,6 +304,7 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
     db.n_reg_slices += (sflags[i] & CDR_SLICE_REG) ? 1u : 0u;
     db.n_reg2_slices += (sflags[i] & CDR_SLICE_REG2) ? 1u : 0u;
     db.n_reg0_slices += (sflags[i] & CDR_SLICE_REG0) ? 1u : 0u;
+    db.n_par_slices += (sflags[i] & CDR_SLICE_PAR) ? 1u : 0u;
   }
   cdr_plan_class_ranges(sflags.data(), ns, db.class_lo, db.class_hi);
   db.ev.slice_scratch_off = (const uint64_t*)up(WS_SC_OFF, sc_off.data(), ns * 8ull);
@@ -372,7 +373,8 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   }
   // class-sorted blocks of the register-table slices (k_replay_cls): size pass, the
   // total rows back to the host, write pass
-  if (ctx->cls && ctx->reg && ctx->fast && !tasks && db.n_reg_slices + db.n_reg2_slices + db.n_reg0_slices > 0 &&
+  if (ctx->cls && ctx->reg && ctx->fast && !tasks &&
+      db.n_reg_slices + db.n_reg2_slices + db.n_reg0_slices + db.n_par_slices > 0 &&
       b->cluster.n_clusters <= (int)CDR_REG_NCL) {
     uint32_t* crows = (uint32_t*)cdr_ws_get(ctx, WS_CLS_ROWS, ns * 16ull);
     uint64_t* crow0 = (uint64_t*)cdr_ws_get(ctx, WS_CLS_ROW0, (ns + 1) * 8ull);

@@ -70,7 +70,7 @@ struct cdr_ctx {
   // of one kernel after another (fork/join by events on the caller's stream).
   // Concurrency beyond the HIP runtime's hardware queues (GPU_MAX_HW_QUEUES, default 4)
   // serialises on a shared queue.
-  static constexpr int N_SIDE = 6;
+  static constexpr int N_SIDE = 7;  // + the PAR slices' stream
   hipStream_t side[N_SIDE] = {};
   hipEvent_t fork = nullptr, join[N_SIDE] = {};
   int concurrent = 1;

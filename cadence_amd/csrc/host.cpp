@@ -362,7 +362,7 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
                        uint32_t* n_slices, uint64_t* n_rows, uint32_t* n_wave) {
   if (!wfs && n_wfs) return CDR_API_EINVAL;
   if ((mode & CDR_PLAN_WAVE) && !caps && n_wfs) return CDR_API_EINVAL;
-  std::vector<uint32_t> lanes, waves;
+  std::vector<uint32_t> lanes, waves, pars;
   lanes.reserve(n_wfs);
   // long histories: a lane slice advances one event per step, so a history much longer
   // than the batch's lane work per resident wave (its steps / CDR_LANE_RESIDENT) sets
@@ -387,9 +387,15 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   }
   // wave slices: every CDR_CAP_WAVE entry no register-table kernel takes (the general
   // lane kernel is the slow fallback for what fits neither), and the long ones
+  // (CDR_PLAN_PAR: the long register-table ones to PAR lane slices instead)
   for (uint32_t w = 0; w < n_wfs; w++) {
     const uint32_t f = caps ? caps[w].flags : 0u;
     const uint64_t thr = (f & CDR_CAP_REG) ? long_thr : long_thr2;
+    if ((mode & CDR_PLAN_WAVE) && (mode & CDR_PLAN_PAR) && !(mode & CDR_PLAN_WAVE_ALL) &&
+        (f & (CDR_CAP_REG | CDR_CAP_REG2)) && (uint64_t)wfs[w].ev_len > thr) {
+      pars.push_back(w);
+      continue;
+    }
     ((mode & CDR_PLAN_WAVE) && (f & CDR_CAP_WAVE) &&
              ((mode & CDR_PLAN_WAVE_ALL) || !(f & (CDR_CAP_REG | CDR_CAP_REG2)) || (uint64_t)wfs[w].ev_len > thr)
          ? waves
@@ -426,6 +432,7 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   };
   std::stable_sort(lanes.begin(), lanes.end(), lane_order);
   std::stable_sort(waves.begin(), waves.end(), longer);
+  std::stable_sort(pars.begin(), pars.end(), longer);
   // each kernel group starts a slice of its own (a mixed slice would replay on the
   // general kernel at the length of the next group's longest histories)
   {
@@ -438,23 +445,27 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     }
     lanes.swap(padded);
   }
-  const uint32_t nl = (uint32_t)((lanes.size() + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
+  // PAR slices first (slices 0 .. np - 1), then the lane slices, then the wave slices
+  const uint32_t np = (uint32_t)((pars.size() + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
+  const uint32_t nl = np + (uint32_t)((lanes.size() + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
   const uint32_t nw = (uint32_t)waves.size();
   uint64_t rows = 0;
   for (uint32_t s = 0; s < nl; s++) {
+    const std::vector<uint32_t>& src = s < np ? pars : lanes;
+    const uint32_t s0 = s < np ? s : s - np;
     uint32_t len = 0;  // the slice's longest lane
-    for (uint32_t l = 0; l < CDR_SLICE_WIDTH && (size_t)s * CDR_SLICE_WIDTH + l < lanes.size(); l++) {
-      const uint32_t w = lanes[(size_t)s * CDR_SLICE_WIDTH + l];
+    for (uint32_t l = 0; l < CDR_SLICE_WIDTH && (size_t)s0 * CDR_SLICE_WIDTH + l < src.size(); l++) {
+      const uint32_t w = src[(size_t)s0 * CDR_SLICE_WIDTH + l];
       if (w != UINT32_MAX) len = std::max(len, (uint32_t)wfs[w].ev_len);
     }
     if (slice_len) slice_len[s] = len;
     if (slice_row0) slice_row0[s] = rows;
-    if (slice_flags) slice_flags[s] = 0;
+    if (slice_flags) slice_flags[s] = s < np ? CDR_SLICE_PAR : 0u;
     rows += len;
     if (lane_wf)
       for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
-        const size_t i = (size_t)s * CDR_SLICE_WIDTH + l;
-        lane_wf[i] = (i < lanes.size() && lanes[i] != UINT32_MAX) ? (int32_t)lanes[i] : -1;
+        const size_t i = (size_t)s0 * CDR_SLICE_WIDTH + l;
+        lane_wf[(size_t)s * CDR_SLICE_WIDTH + l] = (i < src.size() && src[i] != UINT32_MAX) ? (int32_t)src[i] : -1;
       }
   }
   for (uint32_t q = 0; q < nw; q++) {
@@ -485,6 +496,7 @@ int cdr_plan_class_ranges(const uint32_t* slice_flags, uint32_t n_slices, uint32
   for (int c = 0; c < 6; c++) lo[c] = hi[c] = 0;
   for (uint32_t s = 0; s < n_slices; s++) {
     const uint32_t f = slice_flags[s];
+    if (f & CDR_SLICE_PAR) continue;  // slices 0 .. n_par_slices - 1, launched on their own
     const int c = (f & CDR_SLICE_WAVE)   ? CDR_CLASS_WAVE
                   : (f & CDR_SLICE_FAST) ? CDR_CLASS_FAST
                   : (f & CDR_SLICE_REG0) ? CDR_CLASS_REG0
@@ -532,7 +544,9 @@ int cdr_plan_scratch(const cdr_wf_caps* caps, const int32_t* lane_wf, uint32_t n
     if (scratch_off) scratch_off[s] = off;
     if (act_slots) act_slots[s] = a;
     if (tim_slots) tim_slots[s] = t;
-    if (slice_flags)
+    if (slice_flags && (slice_flags[s] & CDR_SLICE_PAR))  // register-table lanes, any class
+      slice_flags[s] = (reg0 || reg || reg2) ? CDR_SLICE_PAR : 0u;
+    else if (slice_flags)
       slice_flags[s] = fast ? CDR_SLICE_FAST : reg0 ? CDR_SLICE_REG0 : reg ? CDR_SLICE_REG : reg2 ? CDR_SLICE_REG2 : 0u;
     off += ((uint64_t)a * CDR_ACT_PLANES + (uint64_t)t * CDR_TIM_PLANES) * CDR_SLICE_WIDTH;
   }

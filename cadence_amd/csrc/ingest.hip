@@ -1318,6 +1318,7 @@ extern "C" int cdr_ingest_plan(cdr_ctx* ctx, const cdr_ingest_out* dec, const cd
     b.n_reg_slices += (sflags[i] & CDR_SLICE_REG) ? 1u : 0u;
     b.n_reg2_slices += (sflags[i] & CDR_SLICE_REG2) ? 1u : 0u;
     b.n_reg0_slices += (sflags[i] & CDR_SLICE_REG0) ? 1u : 0u;
+    b.n_par_slices += (sflags[i] & CDR_SLICE_PAR) ? 1u : 0u;
   }
   cdr_plan_class_ranges(sflags.data(), ns, b.class_lo, b.class_hi);
   b.n_fast_slices = n_fast;
@@ -1326,6 +1327,24 @@ extern "C" int cdr_ingest_plan(cdr_ctx* ctx, const cdr_ingest_out* dec, const cd
   b.now_ns = meta->now_ns;
   b.uuid_seed = meta->uuid_seed;
   b.carry = nullptr;
+  // class-sorted blocks of the register-table slices (k_replay_cls), as cdr_replay_batch
+  if (ctx->cls && b.n_reg_slices + b.n_reg2_slices + b.n_reg0_slices + b.n_par_slices > 0) {
+    uint32_t* crows = (uint32_t*)cdr_ws_get(ctx, WS_CLS_ROWS, ns * 16ull);
+    uint64_t* crow0 = (uint64_t*)cdr_ws_get(ctx, WS_CLS_ROW0, (ns + 1) * 8ull);
+    if (!crows || !crow0) return CDR_API_ENOMEM;
+    int rc = cdr_cls_plan_async(ctx, &b, crows, crow0, st);
+    if (rc != CDR_API_OK) return rc;
+    uint64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, crow0 + ns, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    uint8_t* cslab = (uint8_t*)cdr_ws_get(ctx, WS_CLS_SLAB, total ? total * CDR_ROW_BYTES : 8);
+    if (!cslab) return CDR_API_ENOMEM;
+    b.cls_slab = cslab;
+    b.cls_row0 = crow0;
+    b.cls_rows = crows;
+    rc = cdr_cls_pack_async(ctx, &b, st);
+    if (rc != CDR_API_OK) return rc;
+  }
   *db = b;
   HIPCHK(hipStreamSynchronize(st));
   return CDR_API_OK;

@@ -541,7 +541,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     const uint32_t sf = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_flags[s]);
     if (sf & CDR_SLICE_WAVE) return;  // k_replay_wave
     if (KA()->fast && (sf & CDR_SLICE_FAST)) return;
-    if (KA()->reg && (sf & (CDR_SLICE_REG | CDR_SLICE_REG2 | CDR_SLICE_REG0))) return;  // k_replay_reg
+    if (KA()->reg && (sf & (CDR_SLICE_REG | CDR_SLICE_REG2 | CDR_SLICE_REG0 | CDR_SLICE_PAR))) return;  // k_replay_reg / cls
   }
   const uint64_t row0_ = KA()->B.ev.slice_row0[s];
   const uint64_t row0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(row0_ >> 32)) << 32) |
@@ -1796,7 +1796,7 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
   cdr_opts o;
   cdr_opts_default(&o);
   if (opts) o = *opts;
-  if (o.plan_mode & ~(uint32_t)(CDR_PLAN_WAVE | CDR_PLAN_WAVE_ALL | CDR_PLAN_NO_LONG)) return nullptr;
+  if (o.plan_mode & ~(uint32_t)(CDR_PLAN_WAVE | CDR_PLAN_WAVE_ALL | CDR_PLAN_NO_LONG | CDR_PLAN_PAR)) return nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return nullptr;
   if (hipSetDevice(device) != hipSuccess) return nullptr;
@@ -1830,7 +1830,8 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
       sides_ok = sides_ok && hipExtStreamCreateWithCUMask(&c->side[i], (uint32_t)m.size(), m.data()) == hipSuccess;
     } else {
       sides_ok = sides_ok &&
-                 hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, i < 3 ? prio_hi : prio_lo) == hipSuccess;
+                 hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, (i < 3 || i == 6) ? prio_hi : prio_lo) ==
+                     hipSuccess;
     }
     sides_ok = sides_ok && hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming) == hipSuccess;
   }
@@ -1889,7 +1890,7 @@ int cdr_set_reg_path(cdr_ctx* c, int enable) {
 }
 
 int cdr_set_plan_mode(cdr_ctx* c, uint32_t mode) {
-  if (!c || (mode & ~(uint32_t)(CDR_PLAN_WAVE | CDR_PLAN_WAVE_ALL | CDR_PLAN_NO_LONG))) return CDR_API_EINVAL;
+  if (!c || (mode & ~(uint32_t)(CDR_PLAN_WAVE | CDR_PLAN_WAVE_ALL | CDR_PLAN_NO_LONG | CDR_PLAN_PAR))) return CDR_API_EINVAL;
   const uint32_t old = c->plan_mode;
   c->plan_mode = mode;
   return (int)old;
@@ -1928,7 +1929,8 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   if (tasks && (in->n_wave_slices > 0 || !out->timer_tasks || !out->n_tasks)) return CDR_API_EINVAL;
   const bool fast = c->fast && in->n_fast_slices > 0 && !tasks;
   // register-table kernel: LastReplicationInfo kept for clusters < CDR_REG_NCL only
-  const bool reg = c->fast && c->reg && in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices > 0 && !tasks &&
+  const bool reg = c->fast && c->reg &&
+                   in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices + in->n_par_slices > 0 && !tasks &&
                    in->cluster.n_clusters <= (int)CDR_REG_NCL;
   // class-decomposed replay of the register-table slices (their class-sorted blocks)
   const bool cls = reg && c->cls && in->cls_slab && in->cls_row0 && in->cls_rows;
@@ -1939,7 +1941,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   };
   const bool wave = in->n_wave_slices > 0;
   const bool general = (fast ? in->n_fast_slices : 0u) +
-                           (reg ? in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices : 0u) +
+                           (reg ? in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices + in->n_par_slices : 0u) +
                            in->n_wave_slices <
                        in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
@@ -1968,11 +1970,14 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const bool reg0 = blocks && reg && in->n_reg0_slices && gr0.x;
   const bool reg2 = blocks && reg && in->n_reg2_slices && gr2.x;
   const bool wv = blocks && wave && gw.x, fst = blocks && fast && gf.x;
+  // the PAR slices (the batch's long register-table histories): slices 0 .. n_par_slices - 1
+  const uint32_t npar = in->n_par_slices < blocks ? in->n_par_slices : blocks;
+  const bool par = blocks && reg && npar > 0;
   // the general kernel also takes the fast / register slices whose kernels are off
   const dim3 gg_all = (ranged && (!fast || !reg)) ? dim3(blocks) : gg;
   if (ranged && (!fast || !reg)) Lg.s0 = 0;
   const bool gen = blocks && general && gg_all.x;
-  const bool on[cdr_ctx::N_SIDE] = {wv, reg2, gen, reg0, fst, reg1};
+  const bool on[cdr_ctx::N_SIDE] = {wv, reg2, gen, reg0, fst, reg1, par};
   int kinds = 0;
   for (bool o : on) kinds += o ? 1 : 0;
   bool fk[cdr_ctx::N_SIDE];
@@ -1982,6 +1987,20 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   for (int i = 0; i < cdr_ctx::N_SIDE; i++)
     if (fk[i]) HIPCHK(hipStreamWaitEvent(c->side[i], c->fork, 0));
   auto sx = [&](int i) { return fk[i] ? c->side[i] : st; };
+  if (par) {  // first: the longest critical paths of the batch
+    cdr_launch Lp = L;
+    Lp.s0 = 0;
+    typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
+    if (cls) {
+      typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, true> LC;
+      hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_CLS2, true>),
+                         dim3(npar), dim3(4 * CDR_SLICE_WIDTH), LC::bytes, sx(6), Lp);
+    }
+    if (!cls || cls_fb)
+      hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR>), dim3(npar),
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6), cls ? retry_of(Lp) : Lp);
+  }
+  HIPCHK(hipGetLastError());
   if (wv) hipLaunchKernelGGL(k_replay_wave, gw, dim3(CDR_SLICE_WIDTH), 0, sx(0), Lw);
   HIPCHK(hipGetLastError());
   if (reg2) {

@@ -116,6 +116,8 @@ class DeviceBatch:
         db.n_reg2_slices = self.n_reg2
         self.n_reg0 = int(((self.h_sflags & abi.SLICE_REG0) != 0).sum())
         db.n_reg0_slices = self.n_reg0
+        self.n_par = int(((self.h_sflags & abi.SLICE_PAR) != 0).sum())
+        db.n_par_slices = self.n_par
         L.cdr_plan_class_ranges(self.h_sflags.ctypes.data, len(self.h_sflags), db.class_lo, db.class_hi)
         db.empty_uuid = meta.empty_uuid
         db.cluster = meta.cluster
@@ -124,7 +126,7 @@ class DeviceBatch:
         self.db = db
         self.cls_s = 0.0
         self.cls_rows = 0
-        if cls and ctx_for_cls and self.n_reg + self.n_reg2 + self.n_reg0 > 0:
+        if cls and ctx_for_cls and self.n_reg + self.n_reg2 + self.n_reg0 + self.n_par > 0:
             self.build_cls(ctx_for_cls)
         tot = info.totals
         out = abi.CdrOut()

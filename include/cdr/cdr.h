@@ -135,6 +135,10 @@ typedef struct cdr_slices {
 /* every lane's history has CDR_CAP_REG0: the register-table variant with the small tables
  * (CDR_REG0_*) at 3 waves per SIMD */
 #define CDR_SLICE_REG0 0x10u
+/* a lane slice of the batch's long register-table histories (cdr_plan_slices_ex with
+ * CDR_PLAN_PAR; the first n_par_slices slices): replayed by k_replay_cls's four-wave
+ * variant, its loops at once (replay_cls.inc), or by k_replay_reg <CDR_REG2_NA, ...> */
+#define CDR_SLICE_PAR 0x20u
 /* event types the fast-path kernel replays (bit = cdr_event_type) */
 #define CDR_FAST_TYPES                                                                                       \
   (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_WF_COMPLETED) | CDR_TB(CDR_EV_WF_FAILED) |                      \
@@ -222,7 +226,7 @@ typedef struct cdr_dev_batch {
   uint32_t n_reg_slices;  /* slices with CDR_SLICE_REG (cdr_plan_scratch) */
   uint32_t n_reg2_slices; /* slices with CDR_SLICE_REG2 (cdr_plan_scratch) */
   uint32_t n_reg0_slices; /* slices with CDR_SLICE_REG0 (cdr_plan_scratch) */
-  uint32_t _pad_reg0;
+  uint32_t n_par_slices;  /* slices with CDR_SLICE_PAR: slices 0 .. n_par_slices - 1 (cdr_plan_slices_ex) */
   /* slice index range [class_lo[c], class_hi[c]) holding every slice of kernel class c
    * (CDR_CLASS_*, cdr_plan_class_ranges): each replay kernel is launched over its range
    * only; all zero = unknown, every kernel is launched over every slice */
@@ -293,6 +297,11 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
  * CDR_LONG_REG2_DIV (at least CDR_LONG_MIN / 2) for CDR_CAP_REG2 entries: such a history
  * alone would set the lane kernels' critical path.  This bit turns that rule off. */
 #define CDR_PLAN_NO_LONG 0x4u
+/* with CDR_PLAN_WAVE: the long register-table histories the rule above would give wave
+ * slices go instead to CDR_SLICE_PAR lane slices (longest first, 64 to a slice, the first
+ * slices of the plan), where the class-decomposed kernel runs their loops on four waves at
+ * once */
+#define CDR_PLAN_PAR 0x8u
 #define CDR_LONG_MIN 1024u
 #define CDR_LONG_FACTOR 2u
 #define CDR_LONG_REG2_DIV 2u

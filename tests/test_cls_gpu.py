@@ -91,3 +91,50 @@ def test_cls_long_and_2dc(engine_gpu):
         retried, wrong = _split(b, got, ref)
         assert not wrong, f"builder {builder}: " + "\n".join(wrong[:10])
         assert not retried - {w for w in range(b.n_wfs) if ref.result[w].code != abi.OK}
+
+
+def _n_par(batch, mode):
+    import ctypes as C
+    import numpy as np
+    pl = engine.plan(batch)
+    L = abi.lib()
+    ns, rows, nw = C.c_uint32(), C.c_uint64(), C.c_uint32()
+    L.cdr_plan_slices_ex(batch.wfs, pl.caps, batch.n_wfs, mode, None, None, None, None, C.byref(ns), C.byref(rows),
+                         C.byref(nw))
+    lane = np.zeros(ns.value * 64, np.int32)
+    flags = np.zeros(ns.value, np.uint32)
+    L.cdr_plan_slices_ex(batch.wfs, pl.caps, batch.n_wfs, mode, lane.ctypes.data, None, None, flags.ctypes.data,
+                         C.byref(ns), C.byref(rows), C.byref(nw))
+    return int(((flags & abi.SLICE_PAR) != 0).sum())
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 5])
+@pytest.mark.parametrize("err", [0.0, 0.2])
+def test_par_long_histories(engine_gpu, cfg, err):
+    """Long register-table histories in CDR_SLICE_PAR slices: the class kernel's four-wave
+    variant (its loops at once, the X wave waiting on the W wave's progress) alone, then
+    with k_replay_reg behind it, against the oracle."""
+    import oracle
+    b = engine.synth_batch(cfg, 160, seed=0x5EED0400 + cfg + int(err * 10), target_len=1500, max_len=6000,
+                           error_rate=err)
+    mode = abi.PLAN_WAVE | abi.PLAN_PAR
+    assert _n_par(b, mode) > 0
+    ref = oracle.replay(b)
+    old = engine_gpu.set_plan_mode(mode)
+    try:
+        got = _cls_alone(engine_gpu, b)
+        retried, wrong = _split(b, got, ref)
+        assert not wrong, "\n".join(wrong[:10])
+        if err == 0.0:
+            assert not retried, sorted(retried)[:10]
+        full = engine_gpu.replay(b)
+        bad = engine.compare(b, full, ref)
+        assert not bad, "\n".join(bad[:10])
+        oldc = engine_gpu.set_cls(False)  # PAR slices on k_replay_reg <12, 10, 4>
+        try:
+            bad = engine.compare(b, engine_gpu.replay(b), ref)
+        finally:
+            engine_gpu.set_cls(oldc)
+        assert not bad, "\n".join(bad[:10])
+    finally:
+        engine_gpu.set_plan_mode(old)
