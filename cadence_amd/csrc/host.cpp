@@ -445,17 +445,23 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     }
     lanes.swap(padded);
   }
-  // PAR slices first (slices 0 .. np - 1), then the lane slices, then the wave slices
-  const uint32_t np = (uint32_t)((pars.size() + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
+  // PAR slices first (slices 0 .. np - 1, CDR_PAR_LANES histories each: their P loop runs
+  // one history at a time), then the lane slices, then the wave slices
+  const uint32_t np = (uint32_t)((pars.size() + CDR_PAR_LANES - 1) / CDR_PAR_LANES);
   const uint32_t nl = np + (uint32_t)((lanes.size() + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
   const uint32_t nw = (uint32_t)waves.size();
   uint64_t rows = 0;
   for (uint32_t s = 0; s < nl; s++) {
     const std::vector<uint32_t>& src = s < np ? pars : lanes;
     const uint32_t s0 = s < np ? s : s - np;
+    const uint32_t width = s < np ? CDR_PAR_LANES : CDR_SLICE_WIDTH;  // lanes taken from src
+    auto at = [&](uint32_t l) -> uint32_t {  // workflow of lane l, UINT32_MAX = empty
+      const size_t i = (size_t)s0 * width + l;
+      return (l < width && i < src.size()) ? src[i] : UINT32_MAX;
+    };
     uint32_t len = 0;  // the slice's longest lane
-    for (uint32_t l = 0; l < CDR_SLICE_WIDTH && (size_t)s0 * CDR_SLICE_WIDTH + l < src.size(); l++) {
-      const uint32_t w = src[(size_t)s0 * CDR_SLICE_WIDTH + l];
+    for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
+      const uint32_t w = at(l);
       if (w != UINT32_MAX) len = std::max(len, (uint32_t)wfs[w].ev_len);
     }
     if (slice_len) slice_len[s] = len;
@@ -464,8 +470,8 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     rows += len;
     if (lane_wf)
       for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
-        const size_t i = (size_t)s0 * CDR_SLICE_WIDTH + l;
-        lane_wf[(size_t)s * CDR_SLICE_WIDTH + l] = (i < src.size() && src[i] != UINT32_MAX) ? (int32_t)src[i] : -1;
+        const uint32_t w = at(l);
+        lane_wf[(size_t)s * CDR_SLICE_WIDTH + l] = w != UINT32_MAX ? (int32_t)w : -1;
       }
   }
   for (uint32_t q = 0; q < nw; q++) {
