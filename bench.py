@@ -302,8 +302,8 @@ def main():
     ap.add_argument("--wave-all", action="store_true", help="every divergent history on a wave slice")
     ap.add_argument("--no-refresh", action="store_true", help="skip the refreshTasks / row-encoder side measurements")
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size GPU == oracle digest check")
-    ap.add_argument("--par", action="store_true",
-                    help="long register-table histories in CDR_SLICE_PAR slices (four-wave class kernel) instead of wave slices")
+    ap.add_argument("--no-par", action="store_true",
+                    help="long register-table histories on wave slices instead of CDR_SLICE_PAR slices")
     ap.add_argument("--no-cls", action="store_true",
                     help="register-table slices on k_replay_reg alone (no class-sorted blocks, k_replay_cls off)")
     args = ap.parse_args()
@@ -329,7 +329,7 @@ def main():
     log(f"[rank {rank}] {len(mine)} of {total} workflows (shard->GPU greedy over {NUM_SHARDS} shards)")
     db = DeviceBatch(torch, args.config, mine, args.seed,
                      plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0)
-                     | (abi.PLAN_PAR if args.par else 0),
+                     | (0 if args.no_par else abi.PLAN_PAR),
                      ctx_for_cls=None if args.no_cls else ctx)
     if args.no_cls:
         L.cdr_set_cls_path(ctx, 0)

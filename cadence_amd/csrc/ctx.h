@@ -59,7 +59,7 @@ struct cdr_ctx {
   int fast = 1;                        // cdr_set_fast_path
   int reg = 1;                         // cdr_set_reg_path
   int cls = 1;                         // cdr_set_cls_path
-  uint32_t plan_mode = CDR_PLAN_WAVE;  // cdr_set_plan_mode
+  uint32_t plan_mode = CDR_PLAN_WAVE | CDR_PLAN_PAR;  // cdr_set_plan_mode
   hipEvent_t ev[4];
   bool timed;
   // optional per-launch timing ring (bench): event pairs around every replay kernel

@@ -1786,7 +1786,7 @@ extern "C" {
 void cdr_opts_default(cdr_opts* o) {
   if (!o) return;
   *o = cdr_opts{};
-  o->plan_mode = CDR_PLAN_WAVE;
+  o->plan_mode = CDR_PLAN_WAVE | CDR_PLAN_PAR;
   o->fast_path = 1;
   o->reg_path = 1;
   o->concurrent = 1;

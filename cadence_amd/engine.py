@@ -330,7 +330,7 @@ class Engine:
         opts = abi.CdrOpts()
         L.cdr_opts_default(C.byref(opts))
         opts.fast_path = 1 if fast_path else 0
-        opts.plan_mode = abi.PLAN_WAVE if wave else 0
+        opts.plan_mode = (abi.PLAN_WAVE | abi.PLAN_PAR) if wave else 0
         self.ctx = L.cdr_create(device, C.byref(opts))
         if not self.ctx:
             raise RuntimeError("cdr_create failed: no usable HIP device (the engine has no CPU fallback)")
@@ -339,7 +339,7 @@ class Engine:
         """Plan divergent histories into wave slices (one wavefront per workflow,
         replay_wave.inc; default) or into lane slices of the general kernel; returns
         the previous setting."""
-        return bool(abi.lib().cdr_set_plan_mode(self.ctx, abi.PLAN_WAVE if enable else 0))
+        return bool(abi.lib().cdr_set_plan_mode(self.ctx, (abi.PLAN_WAVE | abi.PLAN_PAR) if enable else 0))
 
     def set_plan_mode(self, mode: int) -> int:
         """CDR_PLAN_* bits of cdr_replay_batch's slicing; returns the previous mode."""

@@ -34,7 +34,7 @@ RESULT_DTYPE = np.dtype([("code", "<i4"), ("flags", "<u4"), ("fid", "<i8"), ("fi
 class DeviceBatch:
     """Synthetic batch generated straight into the sliced layout, uploaded to HBM."""
 
-    def __init__(self, torch, config, index_map, seed, target_len=0, plan_mode=abi.PLAN_WAVE, ctx_for_cls=None,
+    def __init__(self, torch, config, index_map, seed, target_len=0, plan_mode=abi.PLAN_WAVE | abi.PLAN_PAR, ctx_for_cls=None,
                  cls=True):
         L = abi.lib()
         self.torch = torch

@@ -297,10 +297,10 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
  * CDR_LONG_REG2_DIV (at least CDR_LONG_MIN / 2) for CDR_CAP_REG2 entries: such a history
  * alone would set the lane kernels' critical path.  This bit turns that rule off. */
 #define CDR_PLAN_NO_LONG 0x4u
-/* with CDR_PLAN_WAVE: the long register-table histories the rule above would give wave
- * slices go instead to CDR_SLICE_PAR lane slices (longest first, 64 to a slice, the first
- * slices of the plan), where the class-decomposed kernel runs their loops on four waves at
- * once */
+/* with CDR_PLAN_WAVE (default on): the long register-table histories the rule above would
+ * give wave slices go instead to CDR_SLICE_PAR lane slices (longest first, CDR_PAR_LANES to
+ * a slice, the first slices of the plan), where the class-decomposed kernel runs their
+ * loops on four waves at once */
 #define CDR_PLAN_PAR 0x8u
 #define CDR_PAR_LANES 16u /* histories per CDR_SLICE_PAR slice (lanes 0 .. 15; the rest empty) */
 #define CDR_LONG_MIN 1024u

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--wave-all", action="store_true", help="every divergent history on a wave slice")
     ap.add_argument("--no-reg", action="store_true", help="register-table slices on the general kernel")
     ap.add_argument("--no-long", action="store_true", help="long lane-capable histories stay in lane slices")
-    ap.add_argument("--par", action="store_true", help="long register-table histories to PAR slices (CDR_PLAN_PAR)")
+    ap.add_argument("--no-par", action="store_true", help="long register-table histories on wave slices, not PAR slices")
     ap.add_argument("--ab-cls", action="store_true",
                     help="each lib twice: class-decomposed register slices (k_replay_cls) on, then off")
     args = ap.parse_args()
@@ -38,7 +38,7 @@ def main():
     bctx = abi.lib().cdr_create(0, None)
     db = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config,
                      plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0)
-                     | (abi.PLAN_NO_LONG if args.no_long else 0) | (abi.PLAN_PAR if args.par else 0),
+                     | (abi.PLAN_NO_LONG if args.no_long else 0) | (0 if args.no_par else abi.PLAN_PAR),
                      ctx_for_cls=bctx)
     print(json.dumps({"cls_build_s": round(db.cls_s, 4), "cls_rows": db.cls_rows, "rows": db.info.n_rows}), flush=True)
     stream = torch.cuda.current_stream().cuda_stream
