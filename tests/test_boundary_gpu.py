@@ -14,7 +14,7 @@ def test_create_with_opts_and_reserved_workspace():
     L = abi.lib()
     o = abi.CdrOpts()
     L.cdr_opts_default(C.byref(o))
-    assert (o.plan_mode, o.fast_path, o.reg_path, o.concurrent) == (abi.PLAN_WAVE, 1, 1, 1)
+    assert (o.plan_mode, o.fast_path, o.reg_path, o.concurrent) == (abi.PLAN_WAVE | abi.PLAN_PAR, 1, 1, 1)
     o.fast_path, o.concurrent, o.workspace_bytes = 0, 0, 64 << 20
     ctx = L.cdr_create(0, C.byref(o))
     assert ctx

@@ -40,7 +40,8 @@ def _gpu_digests(ctx, cfg, index_map, seed, plan_mode, reg, cls=True):
         L.cdr_set_reg_path(ctx, 1)
     assert rc == 0, rc
     per, tot = db.digests(ctx, stream)
-    kinds = {"wave": db.n_wave, "reg": db.n_reg, "reg2": db.n_reg2, "reg0": db.n_reg0, "cls_rows": db.cls_rows}
+    kinds = {"wave": db.n_wave, "reg": db.n_reg, "reg2": db.n_reg2, "reg0": db.n_reg0, "cls_rows": db.cls_rows,
+             "par": db.n_par}
     del db
     torch.cuda.empty_cache()
     return per, tot, kinds
@@ -52,8 +53,10 @@ def _gpu_digests(ctx, cfg, index_map, seed, plan_mode, reg, cls=True):
     (3, abi.PLAN_WAVE, "nocls"),  # register-table slices on k_replay_reg alone (no class-sorted blocks)
     (3, abi.PLAN_WAVE | abi.PLAN_WAVE_ALL, True),
     (4, abi.PLAN_WAVE, True),
+    (4, abi.PLAN_WAVE | abi.PLAN_PAR, True),  # the long histories on four-wave PAR slices (the default)
     (4, abi.PLAN_WAVE | abi.PLAN_NO_LONG, True),  # long histories kept in register-table lane slices
     (5, abi.PLAN_WAVE, True),
+    (5, abi.PLAN_WAVE | abi.PLAN_PAR, True),
     (5, abi.PLAN_WAVE, False),  # register-table slices on the general kernel
 ])
 def test_fullsize_entry_digests(engine_gpu, cfg, plan_mode, reg):
@@ -76,5 +79,7 @@ def test_fullsize_entry_digests(engine_gpu, cfg, plan_mode, reg):
         assert (kinds["cls_rows"] > 0) == cls, kinds  # the class-sorted blocks were built (or not)
     if cfg in (4, 5) and not plan_mode & abi.PLAN_WAVE_ALL:
         assert kinds["reg2"] > 0, kinds
+    if cfg in (4, 5) and plan_mode & abi.PLAN_PAR:  # the long register-table histories on PAR slices
+        assert kinds["par"] > 0, kinds
     if cfg in (4, 5) and plan_mode == abi.PLAN_WAVE:  # the long-history rule (cdr.h CDR_PLAN_NO_LONG)
         assert kinds["wave"] > 0, kinds
