@@ -1811,9 +1811,8 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
       return nullptr;
     }
   c->timed = false;
-  // the classes whose slices are few and long (wave, 12-activity register, general) get
-  // high-priority streams: their workgroups are dispatched before the bulk classes fill
-  // the CUs (a 256-VGPR wave finds no room beside two 238-VGPR ones)
+  // the PAR slices' stream gets high priority: their workgroups are dispatched before the
+  // bulk classes fill the CUs (CDR_STREAM_PRIO overrides, a bit mask of side streams)
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
   bool sides_ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
@@ -1822,6 +1821,12 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
   if (const char* e = std::getenv("CDR_WAVE_CUS")) wave_cus = std::atoi(e);
   hipDeviceProp_t prop{};
   const int n_cu = (wave_cus > 1 && hipGetDeviceProperties(&prop, device) == hipSuccess) ? prop.multiProcessorCount : 0;
+  // side streams at high priority (bit i: stream i): the PAR slices only — their long
+  // histories set the critical path; every other mask measured was slower on C4/C5
+  // (tools/gpu_prio_streams.sh: C5 7.7 ms vs 9.0 with wave / 12-activity / general / PAR
+  // high, 10.3-10.7 with PAR plus any one other class high)
+  uint32_t hi_mask = 0x40u;
+  if (const char* e = std::getenv("CDR_STREAM_PRIO")) hi_mask = (uint32_t)std::strtoul(e, nullptr, 0);
   for (int i = 0; i < cdr_ctx::N_SIDE; i++) {
     if (n_cu > 0) {
       std::vector<uint32_t> m((n_cu + 31) / 32, 0u);
@@ -1830,7 +1835,7 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
       sides_ok = sides_ok && hipExtStreamCreateWithCUMask(&c->side[i], (uint32_t)m.size(), m.data()) == hipSuccess;
     } else {
       sides_ok = sides_ok &&
-                 hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, (i < 3 || i == 6) ? prio_hi : prio_lo) ==
+                 hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, ((hi_mask >> i) & 1u) ? prio_hi : prio_lo) ==
                      hipSuccess;
     }
     sides_ok = sides_ok && hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming) == hipSuccess;
