@@ -1992,74 +1992,99 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   for (int i = 0; i < cdr_ctx::N_SIDE; i++)
     if (fk[i]) HIPCHK(hipStreamWaitEvent(c->side[i], c->fork, 0));
   auto sx = [&](int i) { return fk[i] ? c->side[i] : st; };
-  if (par) {  // first: the longest critical paths of the batch
-    cdr_launch Lp = L;
-    Lp.s0 = 0;
-    typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
-    if (cls) {
-      typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, true> LC;
-      hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_CLS2, true>),
-                         dim3(npar), dim3(4 * CDR_SLICE_WIDTH), LC::bytes, sx(6), Lp);
+  // each class's launches (its stream sx(i)); the order they are issued in decides which
+  // class's workgroups take the CUs first (CDR_LAUNCH_ORDER overrides: a digit string of
+  // side-stream indices, default \"6012345\": PAR, wave, 12-activity, general, small-table,
+  // fast, 6-activity)
+  auto launch_class = [&](int i) {
+    switch (i) {
+      case 6:
+    if (par) {  // first: the longest critical paths of the batch
+      cdr_launch Lp = L;
+      Lp.s0 = 0;
+      typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
+      if (cls) {
+        typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, true> LC;
+        hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_CLS2, true>),
+                           dim3(npar), dim3(4 * CDR_SLICE_WIDTH), LC::bytes, sx(6), Lp);
+      }
+      if (!cls || cls_fb)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR>), dim3(npar),
+                           dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6), cls ? retry_of(Lp) : Lp);
     }
-    if (!cls || cls_fb)
-      hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR>), dim3(npar),
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6), cls ? retry_of(Lp) : Lp);
-  }
-  HIPCHK(hipGetLastError());
-  if (wv) hipLaunchKernelGGL(k_replay_wave, gw, dim3(CDR_SLICE_WIDTH), 0, sx(0), Lw);
-  HIPCHK(hipGetLastError());
-  if (reg2) {
-    typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
-    if (cls) {
-      typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LC;
-      hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_CLS2>), gr2,
-                         dim3(CDR_SLICE_WIDTH), LC::bytes, sx(1), Lr2);
+        break;
+      case 0:
+    if (wv) hipLaunchKernelGGL(k_replay_wave, gw, dim3(CDR_SLICE_WIDTH), 0, sx(0), Lw);
+        break;
+      case 1:
+    if (reg2) {
+      typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
+      if (cls) {
+        typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LC;
+        hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_CLS2>), gr2,
+                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(1), Lr2);
+      }
+      if (!cls || cls_fb)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), gr2,
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), cls ? retry_of(Lr2) : Lr2);
     }
-    if (!cls || cls_fb)
-      hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), gr2,
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), cls ? retry_of(Lr2) : Lr2);
-  }
-  HIPCHK(hipGetLastError());
-  if (gen) {
-    if (tasks)
-      hipLaunchKernelGGL((k_replay<true, true>), gg_all, dim3(CDR_SLICE_WIDTH), lds, sx(2), Lg);
-    else
-      hipLaunchKernelGGL((k_replay<true, false>), gg_all, dim3(CDR_SLICE_WIDTH), lds, sx(2), Lg);
-  }
-  HIPCHK(hipGetLastError());
-  if (gen && spill) {
-    if (tasks)
-      hipLaunchKernelGGL((k_replay<false, true>), gg_all, dim3(CDR_SLICE_WIDTH), 0, sx(2), Lg);
-    else
-      hipLaunchKernelGGL((k_replay<false, false>), gg_all, dim3(CDR_SLICE_WIDTH), 0, sx(2), Lg);
-  }
-  HIPCHK(hipGetLastError());
-  if (reg0) {  // the small-table variant, at 3 waves per SIMD
-    typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
-    if (cls) {
-      typedef ClsLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LC;
-      hipLaunchKernelGGL((k_replay_cls<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_CLS0>), gr0,
-                         dim3(CDR_SLICE_WIDTH), LC::bytes, sx(3), Lr0);
+        break;
+      case 2:
+    if (gen) {
+      if (tasks)
+        hipLaunchKernelGGL((k_replay<true, true>), gg_all, dim3(CDR_SLICE_WIDTH), lds, sx(2), Lg);
+      else
+        hipLaunchKernelGGL((k_replay<true, false>), gg_all, dim3(CDR_SLICE_WIDTH), lds, sx(2), Lg);
     }
-    if (!cls || cls_fb)
-      hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), gr0,
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), cls ? retry_of(Lr0) : Lr0);
-  }
-  HIPCHK(hipGetLastError());
-  if (fst) hipLaunchKernelGGL(k_replay_fast, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), Lf);
-  HIPCHK(hipGetLastError());
-  if (reg1) {
-    typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
-    if (cls) {
-      typedef ClsLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LC;
-      hipLaunchKernelGGL((k_replay_cls<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_CLS>), gr1,
-                         dim3(CDR_SLICE_WIDTH), LC::bytes, sx(5), Lr1);
+    if (gen && spill) {
+      if (tasks)
+        hipLaunchKernelGGL((k_replay<false, true>), gg_all, dim3(CDR_SLICE_WIDTH), 0, sx(2), Lg);
+      else
+        hipLaunchKernelGGL((k_replay<false, false>), gg_all, dim3(CDR_SLICE_WIDTH), 0, sx(2), Lg);
     }
-    if (!cls || cls_fb)
-      hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), gr1,
-                       dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), cls ? retry_of(Lr1) : Lr1);
+        break;
+      case 3:
+    if (reg0) {  // the small-table variant, at 3 waves per SIMD
+      typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
+      if (cls) {
+        typedef ClsLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LC;
+        hipLaunchKernelGGL((k_replay_cls<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_CLS0>), gr0,
+                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(3), Lr0);
+      }
+      if (!cls || cls_fb)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), gr0,
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), cls ? retry_of(Lr0) : Lr0);
+    }
+        break;
+      case 4:
+    if (fst) hipLaunchKernelGGL(k_replay_fast, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), Lf);
+        break;
+      case 5:
+    if (reg1) {
+      typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
+      if (cls) {
+        typedef ClsLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LC;
+        hipLaunchKernelGGL((k_replay_cls<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_CLS>), gr1,
+                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(5), Lr1);
+      }
+      if (!cls || cls_fb)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), gr1,
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), cls ? retry_of(Lr1) : Lr1);
+    }
+        break;
+    }
+  };
+  static const char* order = [] {
+    const char* e = std::getenv("CDR_LAUNCH_ORDER");
+    uint32_t seen = 0;  // a permutation of the side-stream indices, or the default
+    for (size_t j = 0; e && j < std::strlen(e); j++)
+      if (e[j] >= '0' && e[j] < '0' + cdr_ctx::N_SIDE) seen |= 1u << (e[j] - '0');
+    return (e && std::strlen(e) == (size_t)cdr_ctx::N_SIDE && seen == (1u << cdr_ctx::N_SIDE) - 1u) ? e : "6012345";
+  }();
+  for (int j = 0; j < cdr_ctx::N_SIDE; j++) {
+    launch_class(order[j] - '0');
+    HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipGetLastError());
   for (int i = 0; i < cdr_ctx::N_SIDE; i++)
     if (fk[i]) {
       HIPCHK(hipEventRecord(c->join[i], c->side[i]));
