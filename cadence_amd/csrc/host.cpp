@@ -458,16 +458,24 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   }
   // PAR slices first (slices 0 .. np - 1, CDR_PAR_LANES histories each: their P loop runs
   // one history at a time), then the lane slices, then the wave slices
-  const uint32_t np = (uint32_t)((pars.size() + CDR_PAR_LANES - 1) / CDR_PAR_LANES);
+  // (the CDR_PAR_SOLO longest get a slice each: a W step over one lane runs one handler group)
+  static const uint32_t solo_max = [] {
+    const char* e = std::getenv("CDR_PAR_SOLO");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 0) : (uint32_t)CDR_PAR_SOLO;
+  }();
+  const uint32_t solo = std::min<uint32_t>(solo_max, (uint32_t)pars.size());
+  // PAR slice s takes pars[par_at(s) ...] (solo slices first, then CDR_PAR_LANES per slice)
+  auto par_at = [&](uint32_t s) -> size_t { return s < solo ? s : solo + (size_t)(s - solo) * CDR_PAR_LANES; };
+  const uint32_t np = solo + (uint32_t)((pars.size() - solo + CDR_PAR_LANES - 1) / CDR_PAR_LANES);
   const uint32_t nl = np + (uint32_t)((lanes.size() + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
   const uint32_t nw = (uint32_t)waves.size();
   uint64_t rows = 0;
   for (uint32_t s = 0; s < nl; s++) {
     const std::vector<uint32_t>& src = s < np ? pars : lanes;
-    const uint32_t s0 = s < np ? s : s - np;
-    const uint32_t width = s < np ? CDR_PAR_LANES : CDR_SLICE_WIDTH;  // lanes taken from src
+    const uint32_t width = s < solo ? 1u : s < np ? CDR_PAR_LANES : CDR_SLICE_WIDTH;  // lanes taken from src
+    const size_t first = s < np ? par_at(s) : (size_t)(s - np) * CDR_SLICE_WIDTH;
     auto at = [&](uint32_t l) -> uint32_t {  // workflow of lane l, UINT32_MAX = empty
-      const size_t i = (size_t)s0 * width + l;
+      const size_t i = first + l;
       return (l < width && i < src.size()) ? src[i] : UINT32_MAX;
     };
     uint32_t len = 0;  // the slice's longest lane

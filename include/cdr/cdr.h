@@ -303,6 +303,7 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
  * loops on four waves at once */
 #define CDR_PLAN_PAR 0x8u
 #define CDR_PAR_LANES 16u /* histories per CDR_SLICE_PAR slice (lanes 0 .. 15; the rest empty) */
+#define CDR_PAR_SOLO 0u   /* ... except the longest CDR_PAR_SOLO, one per slice */
 #define CDR_LONG_MIN 1024u
 #define CDR_LONG_FACTOR 2u
 #define CDR_LONG_REG2_DIV 2u
