@@ -263,3 +263,69 @@ def test_long_histories_get_wave_slices():
     assert long_ > 0
     assert engine.slice_kinds(b, pl, abi.PLAN_WAVE)[1] == divergent + long_
     assert engine.slice_kinds(b, pl, abi.PLAN_WAVE | abi.PLAN_NO_LONG)[1] == divergent
+
+
+def _plan(b, pl, mode):
+    L = abi.lib()
+    ns, rows, nw = C.c_uint32(), C.c_uint64(), C.c_uint32()
+    L.cdr_plan_slices_ex(b.wfs, pl.caps, b.n_wfs, mode, None, None, None, None, C.byref(ns), C.byref(rows),
+                         C.byref(nw))
+    lane = np.zeros(ns.value * 64, np.int32)
+    slen = np.zeros(ns.value, np.uint32)
+    row0 = np.zeros(ns.value, np.uint64)
+    flags = np.zeros(ns.value, np.uint32)
+    L.cdr_plan_slices_ex(b.wfs, pl.caps, b.n_wfs, mode, lane.ctypes.data, slen.ctypes.data, row0.ctypes.data,
+                         flags.ctypes.data, C.byref(ns), C.byref(rows), C.byref(nw))
+    return lane.reshape(-1, 64), slen, row0, flags
+
+
+def test_par_slices_plan():
+    """CDR_PLAN_PAR: the long register-table histories the long-history rule would give wave
+    slices become the FIRST slices, CDR_PAR_LANES (16) to a slice, longest first, flagged
+    CDR_SLICE_PAR; the scratch planner keeps the flag (register-table lanes); the class
+    ranges leave them out (they are launched as slices 0 .. n_par - 1)."""
+    b = engine.synth_batch(4, 3000, seed=13)
+    pl = engine.plan(b)
+    L = abi.lib()
+    lw, _, _, fw = _plan(b, pl, abi.PLAN_WAVE)
+    lp, slen, row0, fp = _plan(b, pl, abi.PLAN_WAVE | abi.PLAN_PAR)
+    n_long = int(((fw & abi.SLICE_WAVE) != 0).sum()) - int(((fp & abi.SLICE_WAVE) != 0).sum())
+    par = np.nonzero(fp & abi.SLICE_PAR)[0]
+    assert n_long > 0 and len(par) == (n_long + 15) // 16
+    assert (par == np.arange(len(par))).all()  # the first slices
+    ws = [int(x) for s in par for x in lp[s] if x >= 0]
+    assert len(ws) == n_long and all((lp[s][16:] == -1).all() for s in par)
+    lens = [int(b.wfs[w].ev_len) for w in ws]
+    assert lens == sorted(lens, reverse=True)
+    assert all(pl.caps[w].flags & (abi.CAP_REG | abi.CAP_REG2) for w in ws)
+    assert all(int(slen[s]) == max(int(b.wfs[w].ev_len) for w in lp[s] if w >= 0) for s in par)
+    assert sorted(int(x) for x in lp.ravel() if x >= 0) == list(range(b.n_wfs))  # every entry once
+    words, nf = C.c_uint64(), C.c_uint32()
+    L.cdr_plan_scratch(pl.caps, lp.ctypes.data, len(fp), None, None, None, fp.ctypes.data, C.byref(words),
+                       C.byref(nf))
+    assert (fp[par] == abi.SLICE_PAR).all()
+    lo, hi = (C.c_uint32 * 6)(), (C.c_uint32 * 6)()
+    L.cdr_plan_class_ranges(fp.ctypes.data, len(fp), lo, hi)
+    assert min(lo[c] for c in range(6) if hi[c]) >= len(par)
+
+
+def test_register_lanes_ordered_by_entity_counts():
+    """Within a length class, register-table lanes follow their entity counts (scheduled
+    activities, then started timers, then initiated externals, descending), so that the
+    class-sorted blocks' aligned regions carry little padding."""
+    b = engine.synth_batch(3, 2000, seed=17)
+    pl = engine.plan(b)
+    lp, _, _, _ = _plan(b, pl, abi.PLAN_WAVE)
+    order = [int(x) for x in lp.ravel() if x >= 0]
+    reg = [w for w in order if (pl.caps[w].flags & (abi.CAP_REG | abi.CAP_REG2 | abi.CAP_REG0)) and
+           not (pl.caps[w].flags & abi.CAP_FAST)]
+    lcl = lambda w: int(np.log2(float(b.wfs[w].ev_len) + 1.0) * 16.0)  # noqa: E731
+    key = lambda w: (pl.caps[w].act_cap, pl.caps[w].timer_cap,  # noqa: E731
+                     pl.caps[w].child_cap + pl.caps[w].cancel_cap + pl.caps[w].signal_cap)
+    pairs = 0
+    for a, c in zip(reg, reg[1:]):
+        grp = lambda w: (pl.caps[w].flags & abi.CAP_REG0, pl.caps[w].flags & abi.CAP_REG)  # noqa: E731
+        if grp(a) == grp(c) and lcl(a) == lcl(c):
+            assert key(a) >= key(c), (a, c, key(a), key(c))
+            pairs += 1
+    assert pairs > 100
