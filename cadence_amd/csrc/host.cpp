@@ -369,12 +369,14 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   // the lane kernels' critical path alone; on a wave of its own it replays ~10x faster
   // per event and co-runs with the lane slices (replay.hip, side stream).  The
   // 12-activity register kernel runs one wave per SIMD, so its threshold is lower.
-  uint64_t long_thr = UINT64_MAX, long_thr2 = UINT64_MAX;
+  // PAR slices replay a long history ~4x faster than a lane slice, so their threshold is
+  // lower (CDR_PAR_FACTOR), within the CDR_PAR_MAX_SLICES cap below
+  uint64_t long_thr = UINT64_MAX, long_thr2 = UINT64_MAX, par_thr = UINT64_MAX, par_thr2 = UINT64_MAX;
   if ((mode & CDR_PLAN_WAVE) && !(mode & CDR_PLAN_NO_LONG)) {
     static const uint32_t* lp = [] {
-      static uint32_t v[3] = {CDR_LONG_MIN, CDR_LONG_FACTOR, CDR_LONG_REG2_DIV};
-      if (const char* e = std::getenv("CDR_LONG"))  // tuning override "min,factor,reg2 divisor"
-        std::sscanf(e, "%u,%u,%u", &v[0], &v[1], &v[2]);
+      static uint32_t v[4] = {CDR_LONG_MIN, CDR_LONG_FACTOR, CDR_LONG_REG2_DIV, CDR_PAR_FACTOR};
+      if (const char* e = std::getenv("CDR_LONG"))  // tuning override "min,factor,reg2 divisor[,PAR factor]"
+        std::sscanf(e, "%u,%u,%u,%u", &v[0], &v[1], &v[2], &v[3]);
       return v;
     }();
     uint64_t lane_ev = 0;
@@ -384,6 +386,8 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     const uint64_t per_slot = lane_ev / ((uint64_t)CDR_SLICE_WIDTH * CDR_LANE_RESIDENT);
     long_thr = std::max<uint64_t>(lp[0], (uint64_t)lp[1] * per_slot);
     long_thr2 = std::max<uint64_t>(lp[0] / 2, long_thr / std::max(1u, lp[2]));
+    par_thr = std::max<uint64_t>(lp[0], (uint64_t)lp[3] * per_slot);
+    par_thr2 = std::max<uint64_t>(lp[0] / 2, par_thr / std::max(1u, lp[2]));
   }
   // wave slices: every CDR_CAP_WAVE entry no register-table kernel takes (the general
   // lane kernel is the slow fallback for what fits neither), and the long ones
@@ -392,7 +396,7 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     const uint32_t f = caps ? caps[w].flags : 0u;
     const uint64_t thr = (f & CDR_CAP_REG) ? long_thr : long_thr2;
     if ((mode & CDR_PLAN_WAVE) && (mode & CDR_PLAN_PAR) && !(mode & CDR_PLAN_WAVE_ALL) &&
-        (f & (CDR_CAP_REG | CDR_CAP_REG2)) && (uint64_t)wfs[w].ev_len > thr) {
+        (f & (CDR_CAP_REG | CDR_CAP_REG2)) && (uint64_t)wfs[w].ev_len > ((f & CDR_CAP_REG) ? par_thr : par_thr2)) {
       pars.push_back(w);
       continue;
     }
@@ -441,9 +445,22 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     if (sa != sc) return sa > sc;
     return wfs[a].ev_len > wfs[c].ev_len;
   };
+  // a PAR slice holds a whole CU (four 256-VGPR waves), so beyond about one round of them the
+  // PAR kernel queues behind itself: the longest CDR_PAR_MAX_SLICES slices' worth stay PAR,
+  // the rest go back to the register-table lanes
+  std::stable_sort(pars.begin(), pars.end(), longer);
+  {
+    static const uint64_t par_max = [] {
+      const char* e = std::getenv("CDR_PAR_MAX");  // tuning override (slices)
+      return (uint64_t)(e ? std::strtoul(e, nullptr, 0) : CDR_PAR_MAX_SLICES) * CDR_PAR_LANES;
+    }();
+    if (pars.size() > par_max) {
+      lanes.insert(lanes.end(), pars.begin() + par_max, pars.end());
+      pars.resize(par_max);
+    }
+  }
   std::stable_sort(lanes.begin(), lanes.end(), lane_order);
   std::stable_sort(waves.begin(), waves.end(), longer);
-  std::stable_sort(pars.begin(), pars.end(), longer);
   // each kernel group starts a slice of its own (a mixed slice would replay on the
   // general kernel at the length of the next group's longest histories)
   {

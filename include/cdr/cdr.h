@@ -304,9 +304,11 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
 #define CDR_PLAN_PAR 0x8u
 #define CDR_PAR_LANES 16u /* histories per CDR_SLICE_PAR slice (lanes 0 .. 15; the rest empty) */
 #define CDR_PAR_SOLO 0u   /* ... except the longest CDR_PAR_SOLO, one per slice */
+#define CDR_PAR_MAX_SLICES 128u /* at most this many PAR slices (the longest histories); the rest stay lane slices */
 #define CDR_LONG_MIN 1024u
 #define CDR_LONG_FACTOR 2u
 #define CDR_LONG_REG2_DIV 2u
+#define CDR_PAR_FACTOR 1u /* CDR_PLAN_PAR: the long threshold's factor for PAR slices */
 #define CDR_LANE_RESIDENT 2048u
 int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
                        int32_t* lane_wf, uint32_t* slice_len, uint64_t* slice_row0, uint32_t* slice_flags,

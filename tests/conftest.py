@@ -15,6 +15,12 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def engine_gpu():
     from cadence_amd import engine
+    # torch (device memory for the tests) ships its own HIP/HSA runtime beside the one
+    # libcdr.so links (/opt/rocm): both load into the process, and torch's finds no GPU
+    # when libcdr's initialised the device first, so torch goes first whatever test runs first
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     e = engine.Engine(0)
     yield e
     e.close()

@@ -4,6 +4,8 @@ packer are correct (no GPU compute is called here)."""
 import ctypes as C
 import os
 import re
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -307,6 +309,34 @@ def test_par_slices_plan():
     lo, hi = (C.c_uint32 * 6)(), (C.c_uint32 * 6)()
     L.cdr_plan_class_ranges(fp.ctypes.data, len(fp), lo, hi)
     assert min(lo[c] for c in range(6) if hi[c]) >= len(par)
+
+
+def test_par_slices_capped():
+    """At most CDR_PAR_MAX_SLICES PAR slices (env CDR_PAR_MAX here, read once per process, so
+    in a child process): the longest histories keep them, the rest return to the register-table
+    lane slices, and every entry is still planned once."""
+    code = r"""
+import numpy as np
+from cadence_amd import abi, engine
+import importlib.util, sys
+spec = importlib.util.spec_from_file_location("th", "tests/test_host.py")
+th = importlib.util.module_from_spec(spec); spec.loader.exec_module(th)
+b = engine.synth_batch(4, 3000, seed=13)
+pl = engine.plan(b)
+lp, _, _, fp = th._plan(b, pl, abi.PLAN_WAVE | abi.PLAN_PAR)
+par = np.nonzero(fp & abi.SLICE_PAR)[0]
+assert len(par) == 2, len(par)
+ws = [int(x) for s in par for x in lp[s] if x >= 0]
+rest = [int(x) for s in range(len(par), len(fp)) for x in lp[s]
+        if x >= 0 and pl.caps[x].flags & (abi.CAP_REG | abi.CAP_REG2)]
+assert len(ws) == 32 and min(b.wfs[w].ev_len for w in ws) >= max(b.wfs[w].ev_len for w in rest)
+assert sorted(int(x) for x in lp.ravel() if x >= 0) == list(range(b.n_wfs))
+print("ok")
+"""
+    env = dict(os.environ, CDR_PAR_MAX="2")
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
 
 
 def test_register_lanes_ordered_by_entity_counts():
