@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--no-reg", action="store_true", help="register-table slices on the general kernel")
     ap.add_argument("--no-long", action="store_true", help="long lane-capable histories stay in lane slices")
     ap.add_argument("--no-par", action="store_true", help="long register-table histories on wave slices, not PAR slices")
+    ap.add_argument("--par-subset", type=int, default=0,
+                    help="replay only the histories of the full batch's first N PAR slices (PAR kernel alone)")
     ap.add_argument("--ab-cls", action="store_true",
                     help="each lib twice: class-decomposed register slices (k_replay_cls) on, then off")
     args = ap.parse_args()
@@ -36,6 +38,13 @@ def main():
     torch.cuda.set_device(0)
     idx = np.arange(args.wfs, dtype=np.uint32)
     bctx = abi.lib().cdr_create(0, None)
+    if args.par_subset:
+        full = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config, cls=False)
+        par = np.nonzero(full.h_sflags & abi.SLICE_PAR)[0][:args.par_subset]
+        lanes = full.h_lane.reshape(-1, 64)[par].ravel()
+        idx = np.sort(idx[lanes[(lanes >= 0) & (lanes < len(idx))]])
+        del full
+        torch.cuda.empty_cache()
     db = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config,
                      plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0)
                      | (abi.PLAN_NO_LONG if args.no_long else 0) | (0 if args.no_par else abi.PLAN_PAR),
