@@ -310,7 +310,11 @@ def _hip():
     """The HIP runtime (device buffers for small host-driven calls; no torch)."""
     global _hip_lib
     if _hip_lib is None:
-        L = C.CDLL("libamdhip64.so")
+        # the runtime libcdr.so is bound to: by soname, after libcdr.so is loaded (with torch
+        # loaded first that is torch's copy, whose soname is the same; a plain
+        # "libamdhip64.so" would load a second runtime beside it)
+        abi.lib()
+        L = C.CDLL("libamdhip64.so.7")
         L.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
         L.hipFree.argtypes = [C.c_void_p]
         L.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]

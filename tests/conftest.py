@@ -3,6 +3,16 @@ import sys
 
 import pytest
 
+# torch (device memory for the GPU tests) ships its own HIP runtime whose soname is the
+# one libcdr.so links (libamdhip64.so.7): loaded first, it is the one runtime of the
+# process and libcdr.so binds to it; loaded after libcdr.so it is a second runtime that
+# finds no GPU once libcdr.so's has opened the device.  So torch is imported before any
+# test module loads libcdr.so.
+try:
+    import torch  # noqa: F401
+except ImportError:  # the CPU suite does not need it
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
@@ -15,12 +25,6 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def engine_gpu():
     from cadence_amd import engine
-    # torch (device memory for the tests) ships its own HIP/HSA runtime beside the one
-    # libcdr.so links (/opt/rocm): both load into the process, and torch's finds no GPU
-    # when libcdr's initialised the device first, so torch goes first whatever test runs first
-    import torch
-    if torch.cuda.is_available():
-        torch.cuda.init()
     e = engine.Engine(0)
     yield e
     e.close()
