@@ -198,6 +198,35 @@ def stream_peak_gbs(torch, nbytes=4 << 30, reps=5):
     return 2 * nbytes / dt / 1e9
 
 
+def host_cores() -> tuple:
+    """(cores this process may run on, how that was found): the CPU affinity mask,
+    bounded by the cgroup's CPU quota (cgroup v2 cpu.max, v1 cfs_quota_us / period) when
+    one is set; CDR_CPU_THREADS overrides."""
+    if os.environ.get("CDR_CPU_THREADS"):
+        return max(1, int(os.environ["CDR_CPU_THREADS"])), "CDR_CPU_THREADS"
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    how = f"sched_getaffinity={n}"
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        how += f", cgroup quota {quota:g} CPUs"
+        n = max(1, min(n, int(quota)))
+    else:
+        how += ", no cgroup quota"
+    return n, how
+
+
 def cpu_baseline(config, n_wfs, seed, min_seconds=10.0):
     """CPU restatement (oracle/) on the box's host cores, one task per workflow (the
     analogue of the reference's goroutine-per-workflow), over a bounded sample."""
@@ -206,7 +235,7 @@ def cpu_baseline(config, n_wfs, seed, min_seconds=10.0):
     b = engine.synth_batch(config, n_wfs, seed)
     pl = engine.plan(b)
     n_ev = len(b.events)
-    threads = max(1, min(os.cpu_count() or 1, int(os.environ.get("CDR_CPU_THREADS", "16"))))
+    threads, cores_how = host_cores()
     res = {}
     for th in (threads, 1):
         reps, t0 = 0, time.perf_counter()
@@ -228,7 +257,7 @@ def cpu_baseline(config, n_wfs, seed, min_seconds=10.0):
         if time.perf_counter() - t0 >= min_seconds / 4 or reps >= 1000:
             break
     refresh_eps = b.n_wfs * reps / (time.perf_counter() - t0)
-    return {"value": res[threads], "unit": "events/s", "cores": threads, "kind": "port",
+    return {"value": res[threads], "unit": "events/s", "cores": threads, "cores_source": cores_how, "kind": "port",
             "refresh_entries_per_s_1thread": refresh_eps,
             "sample": f"config {config}: {n_wfs} workflows x {n_ev // max(1, n_wfs)} events, replayed "
                       f"{'repeatedly'} for >= {min_seconds:.0f} s; single-thread {res[1]:.4g} events/s; "
@@ -277,7 +306,7 @@ def parity_check(db, ctx, stream, config, mine, seed):
     import oracle
     t0 = time.perf_counter()
     got, got_sum = db.digests(ctx, stream)
-    threads = max(1, min(os.cpu_count() or 1, int(os.environ.get("CDR_CPU_THREADS", "16"))))
+    threads = host_cores()[0]
     want, want_sum, hist = oracle.synth_digests(config, mine, seed, threads=threads)
     bad = np.nonzero(got != want)[0] if len(got) == len(want) else np.arange(max(len(got), len(want)))
     return {"checked": True, "entries": int(len(want)), "mismatched_entries": int(len(bad)),
@@ -306,6 +335,9 @@ def main():
                     help="long register-table histories on wave slices instead of CDR_SLICE_PAR slices")
     ap.add_argument("--no-cls", action="store_true",
                     help="register-table slices on k_replay_reg alone (no class-sorted blocks, k_replay_cls off)")
+    ap.add_argument("--cls-in-step", action="store_true",
+                    help="class-sorted blocks built on the device (k_cls_count / k_cls_fill) INSIDE every timed step, "
+                         "instead of emitted by the host packer")
     args = ap.parse_args()
 
     import torch
@@ -327,18 +359,30 @@ def main():
     total = args.wfs * world
     mine, load = assign_shards(total, world, rank, workflow_weights(args.config, total, args.seed))
     log(f"[rank {rank}] {len(mine)} of {total} workflows (shard->GPU greedy over {NUM_SHARDS} shards)")
+    # the register-table slices' class-sorted blocks: emitted by the host packer beside the
+    # slab (default; host packing time cls_pack_s), built on the device in every step
+    # (--cls-in-step), or none (--no-cls)
+    cls_src = None if args.no_cls else "device" if args.cls_in_step else "host"
     db = DeviceBatch(torch, args.config, mine, args.seed,
                      plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0)
                      | (0 if args.no_par else abi.PLAN_PAR),
-                     ctx_for_cls=None if args.no_cls else ctx)
+                     ctx_for_cls=ctx, cls=cls_src)
     if args.no_cls:
-        L.cdr_set_cls_path(ctx, 0)
+        L.cdr_set_cls_path(ctx, abi.CLS_OFF)
     log(f"[rank {rank}] {db.n_fast} of {db.info.n_slices} slices on the fast-path kernel, {db.n_wave} wave slices")
-    log(f"[rank {rank}] packed {db.n_events:,} events in {db.pack_s:.2f}s (host SoA), H2D {db.h2d_s:.2f}s "
+    log(f"[rank {rank}] packed {db.n_events:,} events in {db.pack_s:.2f}s (host SoA) + {db.cls_pack_s:.2f}s "
+        f"(class blocks, {db.cls_where}), H2D {db.h2d_s:.2f}s "
         f"({db.in_bytes / 1e9:.2f} GB in, {db.out_bytes / 1e9:.2f} GB out buffers)")
     stream = torch.cuda.current_stream().cuda_stream
 
     def step():
+        if db.cls_where == "device" and args.cls_in_step:  # the class sort inside the step
+            rows_t, row0_t, _ = db.cls_dev
+            rc = L.cdr_cls_plan_async(ctx, C.byref(db.db), C.c_void_p(rows_t.data_ptr()),
+                                      C.c_void_p(row0_t.data_ptr()), C.c_void_p(stream))
+            rc = rc or L.cdr_cls_pack_async(ctx, C.byref(db.db), C.c_void_p(stream))
+            if rc:
+                raise RuntimeError(f"class block build rc={rc}")
         rc = L.cdr_replay_sliced_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(stream))
         if rc:
             raise RuntimeError(f"cdr_replay_sliced_async rc={rc}")
@@ -425,8 +469,16 @@ def main():
         "encode": encode,
         "host": {"soa_pack_s": db.pack_s, "h2d_s": db.h2d_s,
                  "h2d_gbs": db.in_bytes / max(db.h2d_s, 1e-9) / 1e9,
-                 # class-sorted blocks of the register-table slices (device packing step, once per batch)
-                 "cls_build_s": db.cls_s, "cls_rows": db.cls_rows},
+                 # class-sorted blocks of the register-table slices: where they came from, the
+                 # host packer's time for them (part of the SoA packing), a device build
+                 # outside the step (0 unless cls_where == "device" without --cls-in-step)
+                 "cls_where": db.cls_where, "cls_in_step": bool(args.cls_in_step and db.cls_where == "device"),
+                 "cls_pack_s": db.cls_pack_s, "cls_rows": db.cls_rows,
+                 "cls_build_s": 0.0 if args.cls_in_step else db.cls_s,
+                 # one batch end to end on this rank: host packing (slab + class blocks) + H2D +
+                 # one replay step
+                 "per_batch_s": db.pack_s + db.cls_pack_s + db.h2d_s + ms_per_step / 1e3,
+                 "per_batch_events_per_s": db.n_events / (db.pack_s + db.cls_pack_s + db.h2d_s + ms_per_step / 1e3)},
         "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_workflows": tot_ok,
         "parity_checked": bool(parity) and parity["mismatched_entries_all_ranks"] == 0,
         "parity": parity,

@@ -100,7 +100,9 @@ AttrDT = _S("cdr_attr_dt", [("scheduled_event_id", i64), ("started_event_id", i6
 AttrATSched = _S("cdr_attr_at_scheduled", [
     ("activity_id", u32), ("task_list", u32), ("s2s_s", i32), ("s2c_s", i32), ("stc_s", i32), ("hb_s", i32),
     ("flags", u32), ("nonretriable", u32), ("retry_initial_s", i32), ("retry_max_interval_s", i32),
-    ("retry_max_attempts", i32), ("retry_expiration_s", i32), ("backoff_coefficient", f64)])
+    ("retry_max_attempts", i32), ("retry_expiration_s", i32), ("backoff_coefficient", f64),
+    ("domain", u32), ("target_domain_id", u32)])
+AF_HAS_RETRY, AF_DOMAIN_MISSING = 0x1, 0x2
 AttrAT = _S("cdr_attr_at", [("scheduled_event_id", i64), ("started_event_id", i64), ("request_id", u32),
                             ("activity_id", u32), ("timeout_type", i32), ("attempt", i32)])
 AttrTimer = _S("cdr_attr_timer", [("timer_id", u32), ("_pad", u32), ("start_to_fire_s", i64),
@@ -300,7 +302,9 @@ CdrSynthPlanInfo = _S("cdr_synth_plan_info", [
     ("n_events", u64), ("n_entries", u32), ("n_slices", u32), ("n_rows", u64), ("arena_words", u64),
     ("n_kvs", u64), ("n_rps", u64), ("totals", CdrTotals)])
 
-CLS_RETRY = 0x7FFF  # k_replay_cls's hand-on code (cdr_set_cls_path mode 2 only)
+CLS_RETRY = 0x7FFF  # k_replay_cls's hand-on code (cdr_set_cls_path CLS_ALONE only)
+CLS_OFF, CLS_ON, CLS_ALONE, CLS_BUILD = range(4)  # cdr_set_cls_path modes (cdr.h CDR_CLS_*)
+CLS_SLICES = 0x4 | 0x8 | 0x10 | 0x20  # CDR_CLS_SLICES: slices that carry a class-sorted block
 
 MIRRORS = {
     "cdr_event": CdrEvent, "cdr_wf_desc": CdrWfDesc, "cdr_cluster_meta": CdrClusterMeta, "cdr_batch": CdrBatch,
@@ -330,6 +334,8 @@ EXPORTS = {
     "cdr_set_cls_path": (i32, [C.c_void_p, i32]),
     "cdr_cls_plan_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.c_void_p, C.c_void_p, C.c_void_p]),
     "cdr_cls_pack_async": (i32, [C.c_void_p, C.POINTER(CdrDevBatch), C.c_void_p]),
+    "cdr_plan_cls": (i32, [C.POINTER(CdrSlices), C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cdr_pack_cls": (i32, [C.POINTER(CdrSlices), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, i32]),
     "cdr_set_plan_mode": (i32, [C.c_void_p, u32]),
     "cdr_pack_slices": (i32, [C.POINTER(CdrBatch), C.POINTER(CdrSlices), i32]),
     "cdr_create": (C.c_void_p, [i32, C.c_void_p]),

@@ -371,35 +371,33 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
     (void)hipStreamSynchronize(st);  // no copy may still read the host vectors
     return oom ? CDR_API_ENOMEM : CDR_API_EDEVICE;
   }
-  // class-sorted blocks of the register-table slices (k_replay_cls): size pass, the
-  // total rows back to the host, write pass
-  if (ctx->cls && ctx->reg && ctx->fast && !tasks &&
+  // class-sorted blocks of the register-table slices (k_replay_cls), packed on the host
+  // beside the slab when the context asks for them (CDR_CLS_BUILD / CDR_CLS_ALONE): by
+  // default a batch replayed once goes to k_replay_reg, since the block's packing and
+  // H2D cost more than the class kernel saves
+  if (ctx->cls >= CDR_CLS_ALONE && ctx->reg && ctx->fast && !tasks &&
       db.n_reg_slices + db.n_reg2_slices + db.n_reg0_slices + db.n_par_slices > 0 &&
       b->cluster.n_clusters <= (int)CDR_REG_NCL) {
-    uint32_t* crows = (uint32_t*)cdr_ws_get(ctx, WS_CLS_ROWS, ns * 16ull);
-    uint64_t* crow0 = (uint64_t*)cdr_ws_get(ctx, WS_CLS_ROW0, (ns + 1) * 8ull);
-    if (!crows || !crow0) {
-      (void)hipStreamSynchronize(st);
-      return CDR_API_ENOMEM;
+    // the uploads above read host memory this call owns: pack the blocks meanwhile
+    std::vector<uint32_t> crows(ns * 4ull);
+    std::vector<uint64_t> crow0(ns + 1ull);
+    const cdr_wf_desc* wfs_h = b->wfs;
+    rc = cdr_plan_cls(&hs, wfs_h, crows.data(), crow0.data());
+    std::vector<uint8_t> cslab;
+    if (rc == CDR_API_OK) {
+      cslab.resize(crow0[ns] ? crow0[ns] * CDR_ROW_BYTES : 8);
+      rc = cdr_pack_cls(&hs, wfs_h, crows.data(), crow0.data(), cslab.data(), 0);
     }
-    uint64_t total = 0;
-    rc = cdr_cls_plan_async(ctx, &db, crows, crow0, st);
-    if (rc == CDR_API_OK && (hipMemcpyAsync(&total, crow0 + ns, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                             hipStreamSynchronize(st) != hipSuccess))
-      rc = CDR_API_EDEVICE;
-    if (rc != CDR_API_OK) {
-      (void)hipStreamSynchronize(st);
-      return rc;
+    if (rc == CDR_API_OK) {
+      db.cls_rows = (const uint32_t*)up(WS_CLS_ROWS, crows.data(), crows.size() * 4);
+      db.cls_row0 = (const uint64_t*)up(WS_CLS_ROW0, crow0.data(), crow0.size() * 8);
+      db.cls_slab = (const uint8_t*)up(WS_CLS_SLAB, cslab.data(), cslab.size());
+      // the host vectors die with this scope: the copies must land first
+      if (hipStreamSynchronize(st) != hipSuccess) dev_err = true;
     }
-    uint8_t* cslab = (uint8_t*)cdr_ws_get(ctx, WS_CLS_SLAB, total ? total * CDR_ROW_BYTES : 8);
-    if (!cslab) return CDR_API_ENOMEM;
-    db.cls_slab = cslab;
-    db.cls_row0 = crow0;
-    db.cls_rows = crows;
-    rc = cdr_cls_pack_async(ctx, &db, st);
-    if (rc != CDR_API_OK) {
+    if (rc != CDR_API_OK || oom || dev_err) {
       (void)hipStreamSynchronize(st);
-      return rc;
+      return rc != CDR_API_OK ? rc : oom ? CDR_API_ENOMEM : CDR_API_EDEVICE;
     }
   }
   if (refresh) {  // the replay itself emits no stateBuilder tasks

@@ -31,6 +31,7 @@ enum cdr_ws_slot {
   // cdr_ingest_plan (ingest.hip)
   WS_PL_CAPS, WS_PL_AWORDS, WS_PL_ABASE, WS_PL_WFS, WS_PL_LANE, WS_PL_SLEN, WS_PL_ROW0, WS_PL_SFLAGS, WS_PL_SCOFF,
   WS_PL_SCACT, WS_PL_SCTIM, WS_PL_SCRATCH, WS_PL_SLAB, WS_PL_ARENA,
+  WS_PL_CLS_ROWS, WS_PL_CLS_ROW0, WS_PL_CLS_SLAB,  // the ingested batch's own class-sorted blocks
   // cdr_encode_blobs_async (encode_var.hip)
   WS_ENC_SIZES, WS_ENC_TMP,
   WS_NUM
@@ -58,7 +59,7 @@ struct cdr_ctx {
   int device;
   int fast = 1;                        // cdr_set_fast_path
   int reg = 1;                         // cdr_set_reg_path
-  int cls = 1;                         // cdr_set_cls_path
+  int cls = CDR_CLS_ON;                // cdr_set_cls_path (CDR_CLS_*)
   uint32_t plan_mode = CDR_PLAN_WAVE | CDR_PLAN_PAR;  // cdr_set_plan_mode
   hipEvent_t ev[4];
   bool timed;
@@ -73,6 +74,12 @@ struct cdr_ctx {
   static constexpr int N_SIDE = 7;  // + the PAR slices' stream
   hipStream_t side[N_SIDE] = {};
   hipEvent_t fork = nullptr, join[N_SIDE] = {};
+  // class i launches on side[side_of[i]]: every class on its own stream when the runtime
+  // has the hardware queues for it (GPU_MAX_HW_QUEUES >= 8), else three streams — the PAR
+  // slices; the few-and-long classes (wave, 12-activity, general); the bulk classes
+  // (small-table, fast, 6-activity) — so that with HIP's default 4 queues the caller's
+  // stream and the three sides each get a queue of their own
+  int side_of[N_SIDE] = {0, 1, 2, 3, 4, 5, 6};
   int concurrent = 1;
   // grow-only device workspace of the host-buffer calls
   void* ws[WS_NUM] = {};

@@ -30,9 +30,9 @@ int hw_threads(int threads) {
 }
 
 template <class F>
-void parallel_for(uint64_t n, int threads, F&& f) {
+void parallel_for(uint64_t n, int threads, F&& f, uint64_t grain = 256, uint64_t serial_below = 4096) {
   threads = hw_threads(threads);
-  if (threads <= 1 || n < 4096) {
+  if (threads <= 1 || n < serial_below) {
     for (uint64_t i = 0; i < n; i++) f(i);
     return;
   }
@@ -40,9 +40,9 @@ void parallel_for(uint64_t n, int threads, F&& f) {
   std::vector<std::thread> pool;
   auto work = [&] {
     for (;;) {
-      uint64_t i0 = next.fetch_add(256);
+      uint64_t i0 = next.fetch_add(grain);
       if (i0 >= n) break;
-      uint64_t i1 = std::min(n, i0 + 256);
+      uint64_t i1 = std::min(n, i0 + grain);
       for (uint64_t i = i0; i < i1; i++) f(i);
     }
   };
@@ -640,6 +640,145 @@ int cdr_pack_slices(const cdr_batch* b, cdr_slices* o, int threads) {
         cdr_internal::pack_lane(nullptr, 0, row0, len, l, 0, o);
     }
   });
+  return bad ? CDR_API_EINVAL : CDR_API_OK;
+}
+
+// ---- class-sorted blocks on the host (cdr.h; the device twins are k_cls_count /
+// k_cls_fill in replay_cls.inc): the packer regroups each register-table lane's events
+// by entity class, so the class-decomposed replay reads one class per step (the
+// per-event type switch of stateBuilder.go:157-600, regrouped)
+static uint32_t cls_lane_len(const cdr_slices* s, const cdr_wf_desc* wfs, uint64_t sl, uint32_t lane) {
+  const int32_t w = s->lane_wf[sl * CDR_SLICE_WIDTH + lane];
+  return w >= 0 ? (uint32_t)wfs[w].ev_len : 0u;
+}
+static inline uint32_t slab_u32(const uint8_t* rows, uint64_t k, int c, uint32_t lane) {
+  uint32_t v;
+  std::memcpy(&v, rows + k * CDR_ROW_BYTES + cdr_col_off(c) + lane * 4u, 4);
+  return v;
+}
+static inline int64_t slab_i64(const uint8_t* rows, uint64_t k, int c, uint32_t lane) {
+  int64_t v;
+  std::memcpy(&v, rows + k * CDR_ROW_BYTES + cdr_col_off(c) + lane * 8u, 8);
+  return v;
+}
+
+int cdr_plan_cls(const cdr_slices* s, const cdr_wf_desc* wfs, uint32_t* cls_rows, uint64_t* cls_row0) {
+  if (!s || !wfs || !cls_rows || !cls_row0 || !s->slice_flags) return CDR_API_EINVAL;
+  uint64_t acc = 0;
+  for (uint64_t sl = 0; sl < s->n_slices; sl++) {
+    uint32_t m[4] = {0, 0, 0, 0};
+    if (s->slice_flags[sl] & CDR_CLS_SLICES) {
+      const uint8_t* rows = s->slab + s->slice_row0[sl] * CDR_ROW_BYTES;
+      for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
+        const uint32_t len = cls_lane_len(s, wfs, sl, l);
+        if (len > s->slice_len[sl]) return CDR_API_EINVAL;
+        uint32_t n[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < len; k++) {
+          const uint32_t c = cdr_cls_of(slab_u32(rows, k, CDR_COL_TYPE_FLAGS, l) & 0xFFu);
+          if (c < 4) n[c]++;
+        }
+        for (int j = 0; j < 4; j++) m[j] = std::max(m[j], n[j]);
+      }
+    }
+    cls_row0[sl] = acc;
+    for (int j = 0; j < 4; j++) {
+      cls_rows[4 * sl + j] = m[j];
+      acc += m[j];
+    }
+  }
+  cls_row0[s->n_slices] = acc;
+  return CDR_API_OK;
+}
+
+int cdr_pack_cls(const cdr_slices* s, const cdr_wf_desc* wfs, const uint32_t* cls_rows, const uint64_t* cls_row0,
+                 uint8_t* cls_slab, int threads) {
+  if (!s || !wfs || !cls_rows || !cls_row0 || !cls_slab || !s->slice_flags) return CDR_API_EINVAL;
+  std::atomic<int> bad{0};
+  parallel_for(
+      s->n_slices, threads,
+      [&](uint64_t sl) {
+        if (!(s->slice_flags[sl] & CDR_CLS_SLICES)) return;
+        const uint8_t* src = s->slab + s->slice_row0[sl] * CDR_ROW_BYTES;
+        uint8_t* dst = cls_slab + cls_row0[sl] * CDR_ROW_BYTES;
+        uint32_t M[4], off[4], acc = 0;
+        for (int j = 0; j < 4; j++) {
+          M[j] = cls_rows[4 * sl + j];
+          off[j] = acc;
+          acc += M[j];
+        }
+        if (cls_row0[sl + 1] - cls_row0[sl] != acc) {
+          bad = 1;
+          return;
+        }
+        std::memset(dst, 0, (size_t)acc * CDR_ROW_BYTES);
+        auto put = [&](uint64_t row, int c, uint32_t lane, const void* v) {
+          std::memcpy(dst + row * CDR_ROW_BYTES + cdr_col_off(c) + lane * cdr_col_size(c), v, cdr_col_size(c));
+        };
+        // per lane state, walked row by row (each source row read once, contiguously)
+        uint32_t len[CDR_SLICE_WIDTH], pos[CDR_SLICE_WIDTH][4], k0[CDR_SLICE_WIDTH];
+        int64_t prev_id[CDR_SLICE_WIDTH], x_next[CDR_SLICE_WIDTH], wver[CDR_SLICE_WIDTH];
+        bool any_w[CDR_SLICE_WIDTH];
+        uint32_t maxlen = 0;
+        for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
+          len[l] = cls_lane_len(s, wfs, sl, l);
+          if (len[l] > s->slice_len[sl]) bad = 1;
+          maxlen = std::max(maxlen, len[l]);
+          pos[l][0] = pos[l][1] = pos[l][2] = pos[l][3] = 0;
+          k0[l] = 0;
+          prev_id[l] = 0;
+          x_next[l] = CDR_FIRST_EVENT_ID;
+          wver[l] = 0;
+          any_w[l] = false;
+        }
+        if (bad) return;
+        for (uint32_t k = 0; k < maxlen; k++) {
+          for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
+            if (k >= len[l]) continue;
+            const uint32_t tf = slab_u32(src, k, CDR_COL_TYPE_FLAGS, l);
+            const int64_t id = slab_i64(src, k, CDR_COL_EVENT_ID, l), ver = slab_i64(src, k, CDR_COL_VERSION, l);
+            const bool bf = (tf & CDR_SEF_BATCH_FIRST) || k == 0;
+            if (bf && k > 0) x_next[l] = prev_id[l] + 1;  // NextEventID after the previous call (stateBuilder.go:603-604)
+            if (bf) k0[l] = k;
+            prev_id[l] = id;
+            const uint32_t type = tf & 0xFFu;
+            const uint32_t c = cdr_cls_of(type);
+            if (c == CDR_CLS_DROP) continue;
+            if (pos[l][c] >= M[c]) {  // the plan does not belong to this slab
+              bad = 1;
+              return;
+            }
+            const uint64_t row = off[c] + pos[l][c]++;
+            const bool need_id = type < 64 && ((1ull << type) & CDR_CLS_NEED_ID);
+            const bool same_v = c != CDR_CLS_W || (any_w[l] && ver == wver[l]);
+            if (c == CDR_CLS_W) {
+              wver[l] = ver;
+              any_w[l] = true;
+            }
+            const uint32_t tf2 = (tf & ~(CDR_SEF_ID_NEXT | CDR_SEF_VER_SAME)) | (need_id ? 0u : CDR_SEF_CLS_NO_ID) |
+                                 (same_v ? CDR_SEF_CLS_VER_SAME : 0u);
+            const uint64_t d = (uint64_t)id - (uint64_t)x_next[l];
+            const uint32_t xd = (id >= x_next[l] && d < 0xFFFFFFFFull) ? (uint32_t)d : 0xFFFFFFFFu;
+            const uint64_t ann = CDR_CLS_ANN(k, (k - k0[l]) & 0xFFFu, xd);
+            const int64_t ts = slab_i64(src, k, CDR_COL_TIMESTAMP, l), key = slab_i64(src, k, CDR_COL_KEY, l),
+                          aux = slab_i64(src, k, CDR_COL_AUX, l);
+            const uint32_t h = slab_u32(src, k, CDR_COL_H, l), nn = slab_u32(src, k, CDR_COL_N, l);
+            put(row, CDR_COL_TYPE_FLAGS, l, &tf2);
+            put(row, CDR_COL_EVENT_ID, l, &id);
+            put(row, CDR_COL_VERSION, l, &ver);
+            put(row, CDR_COL_TIMESTAMP, l, &ts);
+            put(row, CDR_COL_TASK_ID, l, &ann);
+            put(row, CDR_COL_KEY, l, &key);
+            put(row, CDR_COL_AUX, l, &aux);
+            put(row, CDR_COL_H, l, &h);
+            put(row, CDR_COL_N, l, &nn);
+          }
+        }
+        const uint32_t pad = CDR_EV_PAD | CDR_SEF_CLS_NO_ID | CDR_SEF_CLS_VER_SAME;
+        for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++)
+          for (int j = 0; j < 4; j++)
+            for (uint32_t p = pos[l][j]; p < M[j]; p++) put(off[j] + p, CDR_COL_TYPE_FLAGS, l, &pad);
+      },
+      1, 2);
   return bad ? CDR_API_EINVAL : CDR_API_OK;
 }
 

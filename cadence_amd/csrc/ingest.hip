@@ -578,6 +578,7 @@ struct Blob {
         cdr_attr_at_scheduled& a = e.a.at_sched;
         fields([&](uint32_t t, uint32_t id) {
           if (id == 10 && t == T_STRING) a.activity_id = str();
+          else if (id == 25 && t == T_STRING) a.domain = str();
           else if (id == 30) a.task_list = name_of(t);
           else if (id == 45 && t == T_I32) a.s2c_s = (int32_t)r.be32();
           else if (id == 50 && t == T_I32) a.s2s_s = (int32_t)r.be32();
@@ -588,6 +589,11 @@ struct Blob {
             retry(a);
           } else skip(r, t);
         });
+        if (a.domain) {  // the target domain's ID (refreshTasks, getTargetDomainID)
+          bool miss;
+          a.target_domain_id = domain_id(a.domain, &miss);
+          a.flags |= miss ? CDR_AF_DOMAIN_MISSING : 0u;
+        }
         return;
       }
       case 180: case 190: case 230: case 240: {
@@ -1327,17 +1333,23 @@ extern "C" int cdr_ingest_plan(cdr_ctx* ctx, const cdr_ingest_out* dec, const cd
   b.now_ns = meta->now_ns;
   b.uuid_seed = meta->uuid_seed;
   b.carry = nullptr;
-  // class-sorted blocks of the register-table slices (k_replay_cls), as cdr_replay_batch
-  if (ctx->cls && b.n_reg_slices + b.n_reg2_slices + b.n_reg0_slices + b.n_par_slices > 0) {
-    uint32_t* crows = (uint32_t*)cdr_ws_get(ctx, WS_CLS_ROWS, ns * 16ull);
-    uint64_t* crow0 = (uint64_t*)cdr_ws_get(ctx, WS_CLS_ROW0, (ns + 1) * 8ull);
+  // class-sorted blocks of the register-table slices (k_replay_cls), in the plan's own
+  // workspace slots (a later host-buffer call on the context must not overwrite them);
+  // built when the context asks the packers for them (CDR_CLS_BUILD / CDR_CLS_ALONE, as
+  // cdr_replay_batch)
+  b.cls_slab = nullptr;
+  b.cls_row0 = nullptr;
+  b.cls_rows = nullptr;
+  if (ctx->cls >= CDR_CLS_ALONE && b.n_reg_slices + b.n_reg2_slices + b.n_reg0_slices + b.n_par_slices > 0) {
+    uint32_t* crows = (uint32_t*)cdr_ws_get(ctx, WS_PL_CLS_ROWS, ns * 16ull);
+    uint64_t* crow0 = (uint64_t*)cdr_ws_get(ctx, WS_PL_CLS_ROW0, (ns + 1) * 8ull);
     if (!crows || !crow0) return CDR_API_ENOMEM;
     int rc = cdr_cls_plan_async(ctx, &b, crows, crow0, st);
     if (rc != CDR_API_OK) return rc;
     uint64_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, crow0 + ns, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    uint8_t* cslab = (uint8_t*)cdr_ws_get(ctx, WS_CLS_SLAB, total ? total * CDR_ROW_BYTES : 8);
+    uint8_t* cslab = (uint8_t*)cdr_ws_get(ctx, WS_PL_CLS_SLAB, total ? total * CDR_ROW_BYTES : 8);
     if (!cslab) return CDR_API_ENOMEM;
     b.cls_slab = cslab;
     b.cls_row0 = crow0;

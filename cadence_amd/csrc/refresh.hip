@@ -13,7 +13,8 @@
 //
 // Same conventions as the oracle (oracle/refresh_ref.cpp): pending rows in ascending
 // key order (the output tables are sorted), an entry whose refresh fails keeps its
-// tables and gets no tasks, an activity's target domain is the execution's domain.
+// tables and gets no tasks; an activity's target domain comes from its scheduled event's
+// attributes (cdr_attr_at_scheduled.domain / target_domain_id, getTargetDomainID).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -213,11 +214,28 @@ __global__ __launch_bounds__(256) void k_refresh(cdr_dev_batch B, cdr_out O, int
     for (uint32_t j = 0; j < r.n_activity; j++) {
       const int64_t sched = act[j].schedule_id, started = act[j].started_id;
       if (started == CDR_EMPTY_EVENT_ID) {
-        if (E.find(sched) < 0) {
+        const int64_t k = E.find(sched);
+        if (k < 0) {
           code = CDR_E_REFRESH_EVENT_NOT_FOUND;
           break;
         }
-        X(CDR_TT_ACTIVITY, sched, act[j].version, x.domain_id, act[j].task_list, 0, 0, 0);
+        // generateActivityTransferTasks (mutableStateTaskGenerator.go:302-333): the target
+        // domain is getTargetDomainID(attr.GetDomain()) (:531-545) — "" the execution's; a
+        // scheduled event of another type has nil attributes (the empty domain)
+        uint32_t dom = x.domain_id;
+        constexpr uint64_t kAtWords = (sizeof(cdr_attr_at_scheduled) + 7) / 8;
+        const uint64_t off = (uint64_t)E.i64(k, CDR_COL_AUX) & 0xFFFFFFFFull;
+        if (E.type(k) == CDR_EV_AT_SCHEDULED && off + kAtWords <= B.ev.arena_words) {
+          const cdr_attr_at_scheduled* a = (const cdr_attr_at_scheduled*)(B.ev.arena + off);
+          if (a->domain != 0) {
+            if (a->flags & CDR_AF_DOMAIN_MISSING) {
+              code = CDR_E_DOMAIN_NOT_FOUND;
+              break;
+            }
+            dom = a->target_domain_id;
+          }
+        }
+        X(CDR_TT_ACTIVITY, sched, act[j].version, dom, act[j].task_list, 0, 0, 0);
       }
       if (sched == CDR_EMPTY_EVENT_ID) continue;
       // loadActivityTimers (timerBuilder.go:249-312), first by (time, scheduleID, order)

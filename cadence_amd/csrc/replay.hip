@@ -49,9 +49,6 @@
 #ifndef CDR_WPE
 #define CDR_WPE 3 /* waves per SIMD the register allocator must leave room for */
 #endif
-#ifndef CDR_EXP
-#define CDR_EXP 0 /* cost-breakdown experiments only (tools/build_variants.sh); 0 = product */
-#endif
 #ifndef CDR_LDS_ACT_MAX
 #define CDR_LDS_ACT_MAX 1 /* activity working slots per lane kept in LDS */
 #endif
@@ -863,10 +860,6 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     prev_id = SEL(done, prev_id, e.id);
     prev_ver = SEL(done, prev_ver, e.ver);
     bool go = !done && !stop_at_call_end;  // rest of a failed call: only its last event matters (2DC)
-#if CDR_EXP == 2
-    x_signals += go ? (int32_t)(e.ts ^ e.key ^ e.aux ^ e.h ^ e.n) : 0;
-    continue;
-#endif
 
     // ---- version prelude (stateBuilder.go:134-154); 2DC: UpdateReplicationStateVersion
     // (v, true) leaves CurrentVersion = e.ver, read back from prev_ver at the end
@@ -890,10 +883,6 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
       vh_last_id = SEL(go, e.id, vh_last_id);
     }
     // LastEventTaskID (:155) is read once after the loop (last applied event)
-#if CDR_EXP == 1
-    x_signals += go ? (int32_t)(e.ts ^ e.key ^ e.aux ^ e.h ^ e.n) : 0;
-    continue;
-#endif
 
     // ---- dispatch (stateBuilder.go:157-600): one pass per distinct event type among
     // the lanes that apply an event; the type of each pass is wave-uniform, so the
@@ -1827,7 +1816,21 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
   // high, 10.3-10.7 with PAR plus any one other class high)
   uint32_t hi_mask = 0x40u;
   if (const char* e = std::getenv("CDR_STREAM_PRIO")) hi_mask = (uint32_t)std::strtoul(e, nullptr, 0);
+  // hardware queues of this process's HIP runtime (it reads GPU_MAX_HW_QUEUES once, at
+  // start; default 4): group the classes onto three side streams unless every class can
+  // have a queue (CDR_SIDE_STREAMS=3|7 overrides)
+  int hwq = 4;
+  if (const char* e = std::getenv("GPU_MAX_HW_QUEUES")) hwq = std::atoi(e) > 0 ? std::atoi(e) : 4;
+  int n_side = hwq >= cdr_ctx::N_SIDE + 1 ? cdr_ctx::N_SIDE : 3;
+  if (const char* e = std::getenv("CDR_SIDE_STREAMS")) n_side = std::atoi(e) == 3 ? 3 : cdr_ctx::N_SIDE;
+  if (n_side == 3) {
+    static const int grouped[cdr_ctx::N_SIDE] = {0, 0, 0, 5, 5, 5, 6};  // wave, reg2, general | reg0, fast, reg | PAR
+    for (int i = 0; i < cdr_ctx::N_SIDE; i++) c->side_of[i] = grouped[i];
+  }
+  bool need[cdr_ctx::N_SIDE] = {};  // only the streams some class launches on (each takes a queue)
+  for (int i = 0; i < cdr_ctx::N_SIDE; i++) need[c->side_of[i]] = true;
   for (int i = 0; i < cdr_ctx::N_SIDE; i++) {
+    if (!need[i]) continue;
     if (n_cu > 0) {
       std::vector<uint32_t> m((n_cu + 31) / 32, 0u);
       for (int cu = 0; cu < n_cu; cu++)
@@ -1858,10 +1861,10 @@ int cdr_set_fast_path(cdr_ctx* c, int enable) {
   return old;
 }
 
-int cdr_set_cls_path(cdr_ctx* c, int enable) {
-  if (!c) return CDR_API_EINVAL;
+int cdr_set_cls_path(cdr_ctx* c, int mode) {
+  if (!c || mode < CDR_CLS_OFF || mode > CDR_CLS_BUILD) return CDR_API_EINVAL;
   const int old = c->cls;
-  c->cls = enable == 2 ? 2 : (enable ? 1 : 0);
+  c->cls = mode;
   return old;
 }
 
@@ -1985,13 +1988,17 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const bool on[cdr_ctx::N_SIDE] = {wv, reg2, gen, reg0, fst, reg1, par};
   int kinds = 0;
   for (bool o : on) kinds += o ? 1 : 0;
-  bool fk[cdr_ctx::N_SIDE];
+  bool fk[cdr_ctx::N_SIDE];  // class i forks onto side[side_of[i]]
+  bool used[cdr_ctx::N_SIDE] = {};  // side stream j carries a forked class
   bool any_fork = false;
-  for (int i = 0; i < cdr_ctx::N_SIDE; i++) any_fork |= (fk[i] = c->concurrent && on[i] && kinds > 1);
+  for (int i = 0; i < cdr_ctx::N_SIDE; i++) {
+    any_fork |= (fk[i] = c->concurrent && on[i] && kinds > 1);
+    used[c->side_of[i]] |= fk[i];
+  }
   if (any_fork) HIPCHK(hipEventRecord(c->fork, st));
-  for (int i = 0; i < cdr_ctx::N_SIDE; i++)
-    if (fk[i]) HIPCHK(hipStreamWaitEvent(c->side[i], c->fork, 0));
-  auto sx = [&](int i) { return fk[i] ? c->side[i] : st; };
+  for (int j = 0; j < cdr_ctx::N_SIDE; j++)
+    if (used[j]) HIPCHK(hipStreamWaitEvent(c->side[j], c->fork, 0));
+  auto sx = [&](int i) { return fk[i] ? c->side[c->side_of[i]] : st; };
   // each class's launches (its stream sx(i)); the order they are issued in decides which
   // class's workgroups take the CUs first (CDR_LAUNCH_ORDER overrides: a digit string of
   // side-stream indices, default \"6012345\": PAR, wave, 12-activity, general, small-table,
@@ -2085,10 +2092,10 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
     launch_class(order[j] - '0');
     HIPCHK(hipGetLastError());
   }
-  for (int i = 0; i < cdr_ctx::N_SIDE; i++)
-    if (fk[i]) {
-      HIPCHK(hipEventRecord(c->join[i], c->side[i]));
-      HIPCHK(hipStreamWaitEvent(st, c->join[i], 0));
+  for (int j = 0; j < cdr_ctx::N_SIDE; j++)
+    if (used[j]) {
+      HIPCHK(hipEventRecord(c->join[j], c->side[j]));
+      HIPCHK(hipStreamWaitEvent(st, c->join[j], 0));
     }
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used + 1] : c->ev[1], st));
   if (ring) {

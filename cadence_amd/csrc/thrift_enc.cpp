@@ -239,6 +239,7 @@ struct W {
         const cdr_attr_at_scheduled& a = e.a.at_sched;
         hdr(T_STRUCT, 130);
         str(10, a.activity_id);
+        str(25, a.domain);
         named(30, a.task_list);
         i32(45, a.s2c_s);
         i32(50, a.s2s_s);

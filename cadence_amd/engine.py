@@ -349,12 +349,18 @@ class Engine:
         """CDR_PLAN_* bits of cdr_replay_batch's slicing; returns the previous mode."""
         return int(abi.lib().cdr_set_plan_mode(self.ctx, mode))
 
-    def set_cls(self, enable) -> int:
-        """Replay register-table slices with the class-decomposed kernel (k_replay_cls,
-        default; cdr_replay_batch builds their class-sorted blocks) or with k_replay_reg
-        alone; 2 (tests): k_replay_cls without the k_replay_reg pass for the entries it
-        hands on (result code CLS_RETRY).  Returns the previous setting."""
-        return int(abi.lib().cdr_set_cls_path(self.ctx, 2 if enable == 2 else (1 if enable else 0)))
+    def set_cls(self, mode) -> int:
+        """Class-decomposed replay of the register-table slices (k_replay_cls,
+        cdr_set_cls_path): True / abi.CLS_BUILD — cdr_replay_batch packs their class-sorted
+        blocks and replays them with k_replay_cls; False / abi.CLS_OFF — k_replay_reg alone;
+        abi.CLS_ON (the context default) — class blocks only for device-resident batches
+        that carry them; abi.CLS_ALONE (tests) — k_replay_cls without the k_replay_reg pass
+        for the entries it hands on (result code CLS_RETRY).  Returns the previous mode."""
+        if mode is True:
+            mode = abi.CLS_BUILD
+        elif mode is False:
+            mode = abi.CLS_OFF
+        return int(abi.lib().cdr_set_cls_path(self.ctx, int(mode)))
 
     def set_fast_path(self, enable: bool) -> bool:
         """Route sequential-activity slices to the fast-path kernel (default) or replay

@@ -190,9 +190,14 @@ class HistoryBuilder:
             s.s2c_s = int(x.get("scheduleToCloseTimeoutSeconds", 0))
             s.stc_s = int(x.get("startToCloseTimeoutSeconds", 0))
             s.hb_s = int(x.get("heartbeatTimeoutSeconds", 0))
+            dom = x.get("domain", "")  # the activity's target domain (refreshTasks, getTargetDomainID)
+            s.domain = I(dom)
+            if dom:
+                s.target_domain_id = I(self.domain_ids.get(dom, "id-of-" + dom))
+                s.flags |= abi.AF_DOMAIN_MISSING if dom in self.domains_missing else 0
             rp = x.get("retryPolicy")
             if rp is not None:
-                s.flags = abi.AF_HAS_RETRY
+                s.flags |= abi.AF_HAS_RETRY
                 s.backoff_coefficient = float(rp.get("backoffCoefficient", 0))
                 s.retry_initial_s = int(rp.get("initialIntervalInSeconds", 0))
                 s.retry_max_interval_s = int(rp.get("maximumIntervalInSeconds", 0))

@@ -82,9 +82,14 @@ def encode_batch(batch: engine.Batch, threads: int = 8) -> Encoded:
     types = ev[:, 32:36].copy().view(np.uint32)[:, 0] if len(batch.events) else np.zeros(0, np.uint32)
     ext_t = {abi.EV["StartChildWorkflowExecutionInitiated"], abi.EV["SignalExternalWorkflowExecutionInitiated"],
              abi.EV["RequestCancelExternalWorkflowExecutionInitiated"]}
-    for k in np.nonzero(np.isin(types, list(ext_t) + [abi.EV["WorkflowExecutionStarted"]]))[0]:
+    at_t = abi.EV["ActivityTaskScheduled"]
+    for k in np.nonzero(np.isin(types, list(ext_t) + [abi.EV["WorkflowExecutionStarted"], at_t]))[0]:
         e = batch.events[int(k)]
-        if e.type == abi.EV["WorkflowExecutionStarted"]:
+        if e.type == at_t:  # an activity's target domain (refreshTasks, getTargetDomainID)
+            x = e.a.at_sched
+            if x.domain and not (x.flags & abi.AF_DOMAIN_MISSING):
+                dmap[stand_in(x.domain, strings)] = stand_in(x.target_domain_id, strings)
+        elif e.type == abi.EV["WorkflowExecutionStarted"]:
             s = e.a.started
             if (s.flags & abi.SF_HAS_PARENT_DOMAIN) and not (s.flags & abi.SF_PARENT_DOMAIN_MISSING):
                 ident = stand_in(s.parent_domain_id, strings)

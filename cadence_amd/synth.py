@@ -35,7 +35,16 @@ class DeviceBatch:
     """Synthetic batch generated straight into the sliced layout, uploaded to HBM."""
 
     def __init__(self, torch, config, index_map, seed, target_len=0, plan_mode=abi.PLAN_WAVE | abi.PLAN_PAR, ctx_for_cls=None,
-                 cls=True):
+                 cls="host"):
+        """cls: where the register-table slices' class-sorted blocks (replay_cls.inc) come
+        from — "host": the packer emits them beside the slab (cdr_plan_cls / cdr_pack_cls,
+        host packing time `cls_pack_s`, uploaded with the slab); "device": built on the
+        device after the upload (cdr_cls_plan_async / cdr_cls_pack_async on ctx_for_cls,
+        `cls_s`); None: no blocks (k_replay_reg alone)."""
+        if cls not in ("host", "device", None):
+            raise ValueError(f"cls={cls!r}")
+        if cls == "device" and not ctx_for_cls:
+            raise ValueError("cls='device' needs ctx_for_cls")
         L = abi.lib()
         self.torch = torch
         self.index_map = index_map
@@ -75,6 +84,23 @@ class DeviceBatch:
         assert rc == 0, rc
         self.meta = meta
         self.pack_s = time.perf_counter() - t0
+        # ---- class-sorted blocks from the host packer (a second copy of the register-table
+        # slices' events, regrouped per lane by entity class)
+        self.cls_pack_s = 0.0
+        h_cls = None
+        n_cls_slices = int(((self.h_sflags & abi.CLS_SLICES) != 0).sum())
+        if cls == "host" and n_cls_slices:
+            t0 = time.perf_counter()
+            h_cls_rows = np.zeros(max(1, info.n_slices * 4), np.uint32)
+            h_cls_row0 = np.zeros(info.n_slices + 1, np.uint64)
+            rc = L.cdr_plan_cls(C.byref(s), C.cast(self.h_wfs, C.c_void_p), h_cls_rows.ctypes.data,
+                                h_cls_row0.ctypes.data)
+            assert rc == 0, rc
+            h_cls = np.empty(max(8, int(h_cls_row0[-1]) * abi.ROW_BYTES), np.uint8)
+            rc = L.cdr_pack_cls(C.byref(s), C.cast(self.h_wfs, C.c_void_p), h_cls_rows.ctypes.data,
+                                h_cls_row0.ctypes.data, h_cls.ctypes.data, threads)
+            assert rc == 0, rc
+            self.cls_pack_s = time.perf_counter() - t0
         # ---- upload (H2D timed separately)
         dev = torch.device("cuda", torch.cuda.current_device())
         t0 = time.perf_counter()
@@ -126,8 +152,18 @@ class DeviceBatch:
         self.db = db
         self.cls_s = 0.0
         self.cls_rows = 0
-        if cls and ctx_for_cls and self.n_reg + self.n_reg2 + self.n_reg0 + self.n_par > 0:
+        self.cls_where = None
+        self.cls_bytes = 0
+        if h_cls is not None:
+            db.cls_rows, db.cls_row0, db.cls_slab = up(h_cls_rows), up(h_cls_row0), up(h_cls)
+            self.cls_dev = tuple(self.keep[-3:])  # (rows, row0, block) device tensors
+            self.cls_rows = int(h_cls_row0[-1])
+            self.cls_where = "host"
+            self.cls_bytes = h_cls.nbytes
+            del h_cls  # the device copy is the one replayed
+        elif cls == "device" and n_cls_slices:
             self.build_cls(ctx_for_cls)
+            self.cls_where = "device"
         tot = info.totals
         out = abi.CdrOut()
         sizes = {"result": info.n_entries * C.sizeof(abi.CdrWfResult),
@@ -147,7 +183,7 @@ class DeviceBatch:
         self.out = out
         torch.cuda.synchronize()
         self.h2d_s = time.perf_counter() - t0
-        self.in_bytes = self.h_slab.nbytes + self.h_arena.nbytes
+        self.in_bytes = self.h_slab.nbytes + self.h_arena.nbytes + self.cls_bytes  # uploaded
         types = abi.slab_columns(self.h_slab, self.h_row0, self.h_slen, ("type_flags",))["type_flags"] & 0xFF
         self.type_counts = np.bincount(types, minlength=256)
         self.n_events = int(self.type_counts[:abi.EV["UpsertWorkflowSearchAttributes"] + 1].sum())
@@ -177,6 +213,7 @@ class DeviceBatch:
         self.cls_s = time.perf_counter() - t0
         self.cls_rows = total
         self.keep += [rows_t, row0_t, slab_t]
+        self.cls_dev = (rows_t, row0_t, slab_t)
 
     def builders(self) -> np.ndarray:
         """cdr_wf_desc.builder of every entry."""

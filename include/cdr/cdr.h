@@ -267,6 +267,38 @@ typedef struct cdr_dev_batch {
 #define CDR_SEF_CLS_NO_ID (1u << 21)
 #define CDR_SEF_CLS_VER_SAME (1u << 22)
 #define CDR_CLS_ANN(k, dk, d) ((uint64_t)(k) | ((uint64_t)(dk) << 20) | ((uint64_t)(d) << 32))
+#define CDR_CLS_DROP 4 /* cdr_cls_of: a type with no state of its own (only the P loop sees it) */
+#define CDR_CLS_SLICES (CDR_SLICE_REG | CDR_SLICE_REG2 | CDR_SLICE_REG0 | CDR_SLICE_PAR) /* slices with a block */
+#define CDR_CLS_A_TYPES                                                                                       \
+  (CDR_TB(CDR_EV_AT_SCHEDULED) | CDR_TB(CDR_EV_AT_STARTED) | CDR_TB(CDR_EV_AT_COMPLETED) |                    \
+   CDR_TB(CDR_EV_AT_FAILED) | CDR_TB(CDR_EV_AT_TIMED_OUT) | CDR_TB(CDR_EV_AT_CANCELED) |                      \
+   CDR_TB(CDR_EV_AT_CANCEL_REQUESTED))
+#define CDR_CLS_T_TYPES (CDR_TB(CDR_EV_TIMER_STARTED) | CDR_TB(CDR_EV_TIMER_FIRED) | CDR_TB(CDR_EV_TIMER_CANCELED))
+#define CDR_CLS_X_TYPES                                                                                         \
+  (CDR_TB(CDR_EV_CHILD_INITIATED) | CDR_TB(CDR_EV_CHILD_STARTED) | CDR_TB(CDR_EV_CHILD_START_FAILED) |         \
+   CDR_TB(CDR_EV_CHILD_COMPLETED) | CDR_TB(CDR_EV_CHILD_FAILED) | CDR_TB(CDR_EV_CHILD_CANCELED) |              \
+   CDR_TB(CDR_EV_CHILD_TIMED_OUT) | CDR_TB(CDR_EV_CHILD_TERMINATED) | CDR_TB(CDR_EV_RCE_INITIATED) |           \
+   CDR_TB(CDR_EV_RCE_FAILED) | CDR_TB(CDR_EV_EXT_CANCEL_REQUESTED) | CDR_TB(CDR_EV_SE_INITIATED) |             \
+   CDR_TB(CDR_EV_SE_FAILED) | CDR_TB(CDR_EV_EXT_SIGNALED))
+#define CDR_CLS_DROP_TYPES \
+  (CDR_TB(CDR_EV_MARKER_RECORDED) | CDR_TB(CDR_EV_CANCEL_TIMER_FAILED) | CDR_TB(CDR_EV_AT_REQ_CANCEL_FAILED))
+/* class-sorted events whose event_id a class loop reads (the others get CDR_SEF_CLS_NO_ID) */
+#define CDR_CLS_NEED_ID                                                                                          \
+  (CDR_TB(CDR_EV_WF_STARTED) | CDR_TB(CDR_EV_DT_SCHEDULED) | CDR_TB(CDR_EV_DT_STARTED) |                         \
+   CDR_TB(CDR_EV_DT_TIMED_OUT) | CDR_TB(CDR_EV_DT_FAILED) | CDR_TB(CDR_EV_AT_SCHEDULED) |                        \
+   CDR_TB(CDR_EV_TIMER_STARTED) | CDR_TB(CDR_EV_CHILD_INITIATED) | CDR_TB(CDR_EV_RCE_INITIATED) |                 \
+   CDR_TB(CDR_EV_SE_INITIATED))
+/* class region of an event type (CDR_CLS_W / A / T / X, or CDR_CLS_DROP); unknown types
+ * go to W, whose loop reports them */
+CDR_HD uint32_t cdr_cls_of(uint32_t type) {
+  if (type >= 64) return CDR_CLS_W;
+  const uint64_t b = 1ull << type;
+  return (b & CDR_CLS_A_TYPES)      ? (uint32_t)CDR_CLS_A
+         : (b & CDR_CLS_T_TYPES)    ? (uint32_t)CDR_CLS_T
+         : (b & CDR_CLS_X_TYPES)    ? (uint32_t)CDR_CLS_X
+         : (b & CDR_CLS_DROP_TYPES) ? (uint32_t)CDR_CLS_DROP
+                                    : (uint32_t)CDR_CLS_W;
+}
 
 /* ------------------------------------------------------------ host planning */
 
@@ -366,12 +398,36 @@ int cdr_set_fast_path(cdr_ctx* ctx, int enable);
  * returns the old value. */
 int cdr_set_reg_path(cdr_ctx* ctx, int enable);
 /* Replay register-table slices that carry a class-sorted block (cdr_dev_batch.cls_slab)
- * with the class-decomposed kernel k_replay_cls (default 1; entries it leaves
- * CLS_RETRY go through k_replay_reg) or with k_replay_reg alone (0); 2 (tests only):
- * k_replay_cls with no k_replay_reg pass, so an entry it hands on keeps the internal
- * result code 0x7FFF.  The host-buffer calls build the blocks when this is on.  Returns
- * the old value. */
-int cdr_set_cls_path(cdr_ctx* ctx, int enable);
+ * with the class-decomposed kernel k_replay_cls (entries it leaves CLS_RETRY go through
+ * k_replay_reg) or with k_replay_reg alone (CDR_CLS_OFF).  Modes:
+ *   CDR_CLS_OFF      k_replay_reg alone
+ *   CDR_CLS_ON       (default) k_replay_cls for device-resident batches that carry blocks
+ *                    (the packer emitted them: cdr_pack_cls); the host-buffer calls
+ *                    (cdr_replay_batch / cdr_rebuild_batch / cdr_replay_one) build none —
+ *                    a batch replayed once pays more for its block (packing + H2D of a
+ *                    second copy of the slab) than k_replay_cls saves over k_replay_reg
+ *   CDR_CLS_ALONE    (tests) as CDR_CLS_BUILD, with no k_replay_reg pass, so an entry it
+ *                    hands on keeps the internal result code 0x7FFF
+ *   CDR_CLS_BUILD    as CDR_CLS_ON, and the host-buffer calls pack blocks too (host packer)
+ * Returns the old mode. */
+#define CDR_CLS_OFF 0
+#define CDR_CLS_ON 1
+#define CDR_CLS_ALONE 2
+#define CDR_CLS_BUILD 3
+int cdr_set_cls_path(cdr_ctx* ctx, int mode);
+
+/* Host packer of the class-sorted blocks (the layout above), from a packed host slab
+ * (cdr_pack_slices / the synthetic generator) and the entries' descriptors (ev_len):
+ * cdr_plan_cls writes cls_rows[4 s + c] (n_slices * 4: the rows of each class region of
+ * every CDR_CLS_SLICES slice, 0 for the others) and cls_row0[0..n_slices] (their
+ * exclusive scan; cls_row0[n_slices] = total rows); cdr_pack_cls then writes the blocks
+ * into cls_slab (total * CDR_ROW_BYTES bytes; padding elements carry type_flags
+ * CDR_EV_PAD | CDR_SEF_CLS_NO_ID | CDR_SEF_CLS_VER_SAME and zero columns).  Byte for byte
+ * the blocks cdr_cls_plan_async / cdr_cls_pack_async build on the device (padding
+ * elements' other columns aside).  `threads` host threads (<= 0: hardware). */
+int cdr_plan_cls(const cdr_slices* s, const cdr_wf_desc* wfs, uint32_t* cls_rows, uint64_t* cls_row0);
+int cdr_pack_cls(const cdr_slices* s, const cdr_wf_desc* wfs, const uint32_t* cls_rows, const uint64_t* cls_row0,
+                 uint8_t* cls_slab, int threads);
 
 /* Size pass of the class-sorted blocks (see cdr_dev_batch.cls_slab): cls_rows[4 s + c]
  * (device, n_slices * 4) = the rows of each class region of every register-table slice

@@ -278,12 +278,17 @@ typedef struct cdr_attr_dt { /* DecisionTask{Started,Completed,TimedOut,Failed} 
 } cdr_attr_dt;
 
 #define CDR_AF_HAS_RETRY 0x1u
+#define CDR_AF_DOMAIN_MISSING 0x2u /* the domain cache has no entry for `domain` */
 typedef struct cdr_attr_at_scheduled { /* ActivityTaskScheduledEventAttributes */
   uint32_t activity_id, task_list;
   int32_t s2s_s, s2c_s, stc_s, hb_s;
   uint32_t flags, nonretriable;
   int32_t retry_initial_s, retry_max_interval_s, retry_max_attempts, retry_expiration_s;
   double backoff_coefficient;
+  /* the activity's target domain (attributes.Domain, 0 = ""), and the domain cache's ID
+   * for it, resolved by the caller: read only by refreshTasks' ActivityTask
+   * (getTargetDomainID, mutableStateTaskGenerator.go:309-326,531-545) */
+  uint32_t domain, target_domain_id;
 } cdr_attr_at_scheduled;
 
 typedef struct cdr_attr_at { /* ActivityTask{Started,Completed,Failed,TimedOut,Canceled,CancelRequested} */

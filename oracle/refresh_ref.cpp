@@ -28,8 +28,10 @@
 //    key order (Go ranges over a map: unspecified order);
 //  - an entry whose refresh fails keeps its replayed tables unchanged and gets no tasks
 //    (the reference returns the error and the rebuild discards the state);
-//  - ActivityTaskScheduled.Domain is not in the input schema, so an activity's target
-//    domain is the execution's domain (getTargetDomainID with an empty name).
+//  - an activity's target domain is getTargetDomainID(ActivityTaskScheduled.Domain)
+//    (mutableStateTaskGenerator.go:309-326,531-545): "" -> the execution's domain; else the
+//    domain cache's ID the caller resolved into the event's attributes (cdr_attr_at_scheduled
+//    target_domain_id), a failed lookup the domain-not-found error.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -155,9 +157,17 @@ struct Refresh {
     for (uint32_t j = 0; j < r.n_activity; j++) {
       const cdr_activity_info& a = act[j];
       if (a.started_id != CDR_EMPTY_EVENT_ID) continue;
-      if (!find(w, a.schedule_id)) return CDR_E_REFRESH_EVENT_NOT_FOUND;
-      cdr_task& t = X(CDR_TT_ACTIVITY, a.schedule_id, a.version);  // generateActivityTransferTasks :302-333
-      t.domain_id = x.domain_id;
+      const cdr_event* ev = find(w, a.schedule_id);
+      if (!ev) return CDR_E_REFRESH_EVENT_NOT_FOUND;
+      // generateActivityTransferTasks :302-333: getTargetDomainID(attr.GetDomain()); another
+      // event type's nil attributes read as the empty domain
+      uint32_t dom = x.domain_id;
+      if (ev->type == CDR_EV_AT_SCHEDULED && ev->a.at_sched.domain != 0) {
+        if (ev->a.at_sched.flags & CDR_AF_DOMAIN_MISSING) return CDR_E_DOMAIN_NOT_FOUND;
+        dom = ev->a.at_sched.target_domain_id;
+      }
+      cdr_task& t = X(CDR_TT_ACTIVITY, a.schedule_id, a.version);
+      t.domain_id = dom;
       t.task_list = a.task_list;
     }
     {  // GetActivityTimerTaskIfNeeded (timerBuilder.go:211-230) over loadActivityTimers (:249-312)

@@ -359,6 +359,10 @@ def _attrs(fid, st, e, S, kvs, rps, data, dom, collect):
     if fid == 130:
         x = a.at_sched
         x.activity_id = S(val(10, T_STRING, b""))
+        x.domain = S(val(25, T_STRING, b""))
+        if x.domain:  # ActivityTaskScheduledEventAttributes.domain (shared.thrift:615) -> getTargetDomainID
+            x.target_domain_id, miss = _domain(dom, x.domain)
+            x.flags |= abi.AF_DOMAIN_MISSING if miss else 0
         x.task_list = S(_name(g(30, T_STRUCT)) or b"")
         x.s2c_s, x.s2s_s, x.stc_s, x.hb_s = val(45, T_I32), val(50, T_I32), val(55, T_I32), val(60, T_I32)
         rp = g(110, T_STRUCT)

@@ -138,3 +138,35 @@ def test_par_long_histories(engine_gpu, cfg, err):
         assert not bad, "\n".join(bad[:10])
     finally:
         engine_gpu.set_plan_mode(old)
+
+
+@pytest.mark.parametrize("cfg,n", [(3, 20000), (4, 30000), (5, 20000)])
+def test_host_blocks_equal_device_blocks(engine_gpu, cfg, n):
+    """The host packer's class-sorted blocks (cdr_pack_cls) are the device build's
+    (k_cls_count / k_cls_fill) byte for byte — padding elements' type_flags included, their
+    other columns (unwritten by the device build) aside — and both replay to the same
+    outputs."""
+    import numpy as np
+    import torch
+    from cadence_amd.synth import DeviceBatch
+    idx = np.arange(n, dtype=np.uint32)
+    seed = 0x5EED0000 + cfg
+    h = DeviceBatch(torch, cfg, idx, seed, cls="host")
+    d = DeviceBatch(torch, cfg, idx, seed, ctx_for_cls=engine_gpu.ctx, cls="device")
+    assert h.cls_rows == d.cls_rows > 0
+    ns = h.info.n_slices
+    for a, b in zip(h.cls_dev[:2], d.cls_dev[:2]):
+        assert torch.equal(a[:b.numel()].cpu() if a.numel() >= b.numel() else a.cpu(), b[:a.numel()].cpu())
+    hb = abi.slab_columns(h.cls_dev[2][:h.cls_rows * abi.ROW_BYTES].cpu().numpy())
+    db_ = abi.slab_columns(d.cls_dev[2][:d.cls_rows * abi.ROW_BYTES].cpu().numpy())
+    pad = (hb["type_flags"] & 0xFF) == 0xFF
+    assert (hb["type_flags"] == db_["type_flags"]).all()
+    for col in ("event_id", "version", "timestamp", "task_id", "key", "aux", "h", "n"):
+        diff = np.nonzero((hb[col] != db_[col]) & ~pad)[0]
+        assert len(diff) == 0, (col, diff[:5])
+    stream = torch.cuda.current_stream().cuda_stream
+    import ctypes as C
+    for x in (h, d):
+        assert abi.lib().cdr_replay_sliced_async(engine_gpu.ctx, C.byref(x.db), C.byref(x.out), C.c_void_p(stream)) == 0
+    assert (h.digests(engine_gpu.ctx, stream)[0] == d.digests(engine_gpu.ctx, stream)[0]).all()
+    assert ns == d.info.n_slices

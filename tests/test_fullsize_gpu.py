@@ -25,12 +25,13 @@ N_WFS = int(os.environ.get("CDR_FULLSIZE_WFS", "1000000"))
 THREADS = int(os.environ.get("CDR_CPU_THREADS", "16"))
 
 
-def _gpu_digests(ctx, cfg, index_map, seed, plan_mode, reg, cls=True):
+def _gpu_digests(ctx, cfg, index_map, seed, plan_mode, reg, cls="host"):
     import torch
     from cadence_amd.synth import DeviceBatch
     import ctypes as C
-    # cls: the register-table slices get their class-sorted blocks (k_replay_cls)
-    db = DeviceBatch(torch, cfg, index_map, seed, plan_mode=plan_mode, ctx_for_cls=ctx if cls else None)
+    # cls: where the register-table slices' class-sorted blocks come from (k_replay_cls):
+    # "host" the packer (the default), "device" k_cls_fill, None no blocks
+    db = DeviceBatch(torch, cfg, index_map, seed, plan_mode=plan_mode, ctx_for_cls=ctx, cls=cls)
     stream = torch.cuda.current_stream().cuda_stream
     L = abi.lib()
     L.cdr_set_reg_path(ctx, int(reg))
@@ -40,7 +41,7 @@ def _gpu_digests(ctx, cfg, index_map, seed, plan_mode, reg, cls=True):
         L.cdr_set_reg_path(ctx, 1)
     assert rc == 0, rc
     per, tot = db.digests(ctx, stream)
-    kinds = {"wave": db.n_wave, "reg": db.n_reg, "reg2": db.n_reg2, "reg0": db.n_reg0, "cls_rows": db.cls_rows,
+    kinds = {"cls_where": db.cls_where, "wave": db.n_wave, "reg": db.n_reg, "reg2": db.n_reg2, "reg0": db.n_reg0, "cls_rows": db.cls_rows,
              "par": db.n_par}
     del db
     torch.cuda.empty_cache()
@@ -51,6 +52,7 @@ def _gpu_digests(ctx, cfg, index_map, seed, plan_mode, reg, cls=True):
     (2, abi.PLAN_WAVE, True),
     (3, abi.PLAN_WAVE, True),
     (3, abi.PLAN_WAVE, "nocls"),  # register-table slices on k_replay_reg alone (no class-sorted blocks)
+    (3, abi.PLAN_WAVE, "devcls"),  # class-sorted blocks built on the device (k_cls_fill)
     (3, abi.PLAN_WAVE | abi.PLAN_WAVE_ALL, True),
     (4, abi.PLAN_WAVE, True),
     (4, abi.PLAN_WAVE | abi.PLAN_PAR, True),  # the long histories on four-wave PAR slices (the default)
@@ -63,7 +65,7 @@ def test_fullsize_entry_digests(engine_gpu, cfg, plan_mode, reg):
     import oracle
     seed = 0x5EED0000 + cfg
     index_map = np.arange(N_WFS, dtype=np.uint32)
-    cls = reg != "nocls"
+    cls = None if reg == "nocls" else "device" if reg == "devcls" else "host"
     got, got_sum, kinds = _gpu_digests(engine_gpu.ctx, cfg, index_map, seed, plan_mode, bool(reg), cls)
     want, want_sum, hist = oracle.synth_digests(cfg, index_map, seed, threads=THREADS)
     assert len(got) == len(want)
@@ -76,7 +78,7 @@ def test_fullsize_entry_digests(engine_gpu, cfg, plan_mode, reg):
         assert kinds["wave"] > 0
     elif cfg in (3, 4, 5):
         assert kinds["reg"] > 0, kinds
-        assert (kinds["cls_rows"] > 0) == cls, kinds  # the class-sorted blocks were built (or not)
+        assert (kinds["cls_rows"] > 0) == (cls is not None), kinds  # the class-sorted blocks were built (or not)
     if cfg in (4, 5) and not plan_mode & abi.PLAN_WAVE_ALL:
         assert kinds["reg2"] > 0, kinds
     if cfg in (4, 5) and plan_mode & abi.PLAN_PAR:  # the long register-table histories on PAR slices

@@ -104,7 +104,7 @@ def test_pack_round_trip():
             if e.type == abi.EV["ActivityTaskScheduled"]:
                 a = e.a.at_sched
                 off = int(cols["aux"][j]) & 0xFFFFFFFF
-                rec = abi.AttrATSched.from_buffer_copy(arena[off:off + 7].tobytes())
+                rec = abi.AttrATSched.from_buffer_copy(arena[off:off + C.sizeof(abi.AttrATSched) // 8].tobytes())
                 assert bytes(rec) == bytes(a)
                 assert int(cols["key"][j]) & 0xFFFFFFFF == a.activity_id
                 assert (int(cols["key"][j]) >> 32) & 0xFFFFFFFF == a.stc_s & 0xFFFFFFFF

@@ -95,7 +95,8 @@ HANDLE_FIELDS = {  # union member -> handle fields (the rest compared by value)
     "started": ("workflow_type", "task_list", "cron_schedule", "parent_domain_id", "parent_workflow_id",
                 "parent_run_id", "continued_run_id", "nonretriable", "memo"),
     "dt_sched": ("task_list",), "dt": ("request_id", "binary_checksum"),
-    "at_sched": ("activity_id", "task_list", "nonretriable"), "at": ("request_id", "activity_id"),
+    "at_sched": ("activity_id", "task_list", "nonretriable", "domain", "target_domain_id"),
+    "at": ("request_id", "activity_id"),
     "timer": ("timer_id",), "ext": ("domain", "workflow_id", "run_id", "workflow_type", "signal_name", "input",
                                     "control", "target_domain_id"),
     "ref": ("run_id",), "can": ("new_execution_run_id",), "upsert": (),
@@ -195,6 +196,8 @@ def round_trip_equal(src: engine.Batch, dec, limit=10**9):
                     continue  # the cache lookup failed: no ID
                 if m == "ext" and f == "target_domain_id" and xa.flags & abi.XF_DOMAIN_MISSING:
                     continue
+                if m == "at_sched" and f == "target_domain_id" and xa.flags & abi.AF_DOMAIN_MISSING:
+                    continue
                 if f in hf:
                     R.same(va, vb, f"{m}.{f}")
                 else:
@@ -246,7 +249,43 @@ def test_fixture_histories_round_trip_oracle():
     assert S[e0.a.started.task_list] == b.strings[b.events[0].a.started.task_list].encode()
 
 
+def _cross_domain_activities(missing=False):
+    """Activities with no, an empty, a known and an unknown target domain
+    (ActivityTaskScheduledEventAttributes.domain, shared.thrift:615)."""
+    from cadence_amd.history import HistoryBuilder
+    from tests import test_refresh as TR
+    hb = HistoryBuilder()
+    if missing:
+        hb.domains_missing.add("gone-dom")
+    w = hb.workflow(workflow_id="wf", run_id="run", request_id="req", retention_days=2)
+    w.calls = TR._cross_domain_calls() + [[TR._act(8, "gone", "gone-dom")]]
+    return hb.build(now_ns=TR.NOW)
+
+
+@pytest.mark.parametrize("missing", [False, True])
+def test_activity_domain_round_trip_oracle(missing):
+    """Field 25 (domain) of ActivityTaskScheduled is encoded, decoded and resolved through
+    the caller's domain map like the external events' domains: the decoded record carries
+    the name and the cache's ID, or the domain-missing flag."""
+    b = _cross_domain_activities(missing)
+    enc = ingest.encode_batch(b)
+    dec = oracle_decode(enc)
+    assert round_trip_equal(b, dec) == len(b.events)
+    S = dec[6]
+    at = [e.a.at_sched for e in dec[0] if e.type == abi.EV["ActivityTaskScheduled"]]
+    assert [S[x.domain] for x in at] == [b"", b"", b"remote-dom", b"gone-dom"]
+    assert [bool(x.flags & abi.AF_DOMAIN_MISSING) for x in at] == [False, False, False, missing]
+    assert S[at[2].target_domain_id] == b"id-of-remote-dom"
+
+
 # ------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("missing", [False, True])
+def test_activity_domain_decode_gpu(engine_gpu, missing):
+    enc = ingest.encode_batch(_cross_domain_activities(missing))
+    assert_same_decode(ingest.decode(engine_gpu, enc), oracle_decode(enc))
+
+
 def decoded_tuple(d: ingest.Decoded):
     return (d.events, d.kvs, d.rps, d.ev_off, d.blob_status, d.entry_status, d.strings)
 

@@ -170,6 +170,47 @@ def test_external_tasks():
     assert (s.event_id, s.domain_id, s.target_run_id, s.flags) == (6, I("domain-id"), I("target-run"), 1)
 
 
+def _act(i, aid, domain=None):
+    x = {"activityId": aid, "taskList": {"name": "atl"}, "scheduleToStartTimeoutSeconds": 5,
+         "scheduleToCloseTimeoutSeconds": 60, "startToCloseTimeoutSeconds": 30}
+    if domain is not None:
+        x["domain"] = domain
+    return _ev(i, "ActivityTaskScheduled", activityTaskScheduledEventAttributes=x)
+
+
+def _cross_domain_calls():
+    return [[_started()] + _dt(2)[:1], _dt(2)[1:2],
+            _dt(2)[2:] + [_act(5, "local"), _act(6, "empty", ""), _act(7, "remote", "remote-dom")]]
+
+
+def test_activity_target_domain():
+    """generateActivityTransferTasks (mutableStateTaskGenerator.go:302-333): the ActivityTask's
+    DomainID is getTargetDomainID(attr.GetDomain()) (:531-545) — the execution's domain for a
+    nil or empty domain, the domain cache's ID for a named one."""
+    out, I = _rebuild(_cross_domain_calls())
+    assert out.result[0].code == abi.OK
+    xt = [t for t in out.task_rows(0, "xfer") if abi.TASK_TYPES[t.type] == "ActivityTask"]
+    assert [(t.event_id, t.domain_id) for t in xt] == [
+        (5, I("domain-id")), (6, I("domain-id")), (7, I("id-of-remote-dom"))]
+    assert all(t.task_list == I("atl") for t in xt)
+
+
+def test_activity_target_domain_missing():
+    """A named target domain the domain cache does not know: getTargetDomainID's error
+    (:538-541) fails the refresh (CDR_E_DOMAIN_NOT_FOUND), the entry keeps no tasks."""
+    import oracle
+    hb = HistoryBuilder()
+    hb.domains_missing.add("remote-dom")
+    w = hb.workflow(workflow_id="wf", run_id="run", request_id="req", retention_days=2)
+    w.calls = _cross_domain_calls()
+    b = hb.build(now_ns=NOW)
+    ref = oracle.replay(b)
+    assert ref.result[0].code == abi.OK  # the replay itself never reads the activity's domain
+    out = oracle.rebuild(b)
+    assert out.result[0].code == 11  # CDR_E_DOMAIN_NOT_FOUND
+    assert out.tasks["n"][0] == out.tasks["n"][1] == 0
+
+
 def test_snapshot_passive_task_versions():
     """CloseTransactionAsSnapshot(passive): setTaskInfo sets every task's Version to the
     current version (historyEngine.go:2383-2397) — timer picks included."""
@@ -274,3 +315,17 @@ def test_gpu_refresh_fixture_histories(engine_gpu):
     for calls in cases:
         _, b = _hb(calls)
         _check(engine_gpu, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("missing", [False, True])
+def test_gpu_activity_target_domain(engine_gpu, missing):
+    """GPU twin of the cross-domain activity KATs: refresh.hip reads the scheduled event's
+    target domain from the arena record, a missing one fails the entry."""
+    hb = HistoryBuilder()
+    if missing:
+        hb.domains_missing.add("remote-dom")
+    w = hb.workflow(workflow_id="wf", run_id="run", request_id="req", retention_days=2)
+    w.calls = _cross_domain_calls()
+    ref = _check(engine_gpu, hb.build(now_ns=NOW))
+    assert ref.result[0].code == (11 if missing else abi.OK)

@@ -20,8 +20,8 @@ from cadence_amd.synth import DeviceBatch  # noqa: E402
 torch.cuda.init()
 idx = np.arange(args.wfs, dtype=np.uint32)
 ctx = abi.lib().cdr_create(0, None)
-db = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config, ctx_for_cls=ctx)
-rows = db.keep[-3].view(torch.int32).cpu().numpy()[:db.info.n_slices * 4].reshape(-1, 4)
+db = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config, ctx_for_cls=ctx, cls="device")
+rows = db.cls_dev[0].view(torch.int32).cpu().numpy()[:db.info.n_slices * 4].reshape(-1, 4)
 fl, sl = db.h_sflags, db.h_slen
 out = {"config": args.config}
 for name, bit in (("par", abi.SLICE_PAR), ("reg0", abi.SLICE_REG0), ("reg", abi.SLICE_REG), ("reg2", abi.SLICE_REG2)):

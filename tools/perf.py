@@ -39,7 +39,7 @@ def main():
     idx = np.arange(args.wfs, dtype=np.uint32)
     bctx = abi.lib().cdr_create(0, None)
     if args.par_subset:
-        full = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config, cls=False)
+        full = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config, cls=None)
         par = np.nonzero(full.h_sflags & abi.SLICE_PAR)[0][:args.par_subset]
         lanes = full.h_lane.reshape(-1, 64)[par].ravel()
         idx = np.sort(idx[lanes[(lanes >= 0) & (lanes < len(idx))]])
@@ -49,7 +49,8 @@ def main():
                      plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0)
                      | (abi.PLAN_NO_LONG if args.no_long else 0) | (0 if args.no_par else abi.PLAN_PAR),
                      ctx_for_cls=bctx)
-    print(json.dumps({"cls_build_s": round(db.cls_s, 4), "cls_rows": db.cls_rows, "rows": db.info.n_rows}), flush=True)
+    print(json.dumps({"cls_pack_s": round(db.cls_pack_s, 4), "cls_rows": db.cls_rows, "rows": db.info.n_rows}),
+          flush=True)
     stream = torch.cuda.current_stream().cuda_stream
     libs = [(p, abi.load(p)) for p in args.libs]
     if args.ab_cls:
