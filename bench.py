@@ -287,10 +287,15 @@ def load_traffic(workload):
     """PMC HBM bytes per launch (tools/pmc.sh + tools/traffic.py) for this workload, used
     only when they were collected on this very build of libcdr.so (same SHA-1); else
     (None, reason)."""
-    p = os.path.join(HERE, "profiles", "traffic_latest.json")
-    try:
-        d = json.load(open(p))
-    except Exception:
+    d = None
+    for name in (f"traffic_{workload}.json", "traffic_latest.json"):
+        try:
+            d = json.load(open(os.path.join(HERE, "profiles", name)))
+        except Exception:
+            continue
+        if d.get("workload") == workload:
+            break
+    if d is None:
         return None, "no PMC summary"
     if d.get("workload") != workload:
         return None, f"PMC summary is for {d.get('workload')}"

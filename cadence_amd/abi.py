@@ -54,7 +54,7 @@ STATUS = {
     16: "E_REFRESH_CAPACITY", 17: "E_VH_NO_LCA", 18: "E_VH_LCA_NOT_CONTAINED", 19: "E_VH_FIRST_ITEM_MISMATCH",
     20: "E_NDC_RETRY_TASK", 21: "E_NDC_BRANCH_CHANGED", 22: "E_NDC_SAME_VERSION", 23: "E_REBUILD_VH_MISMATCH",
     24: "E_VHS_CAPACITY", 25: "E_VH_EMPTY", 32: "P_ACTIVITY_STARTED_NIL", 33: "P_CHILD_STARTED_NIL",
-    34: "P_VH_ITEM_INVALID", 35: "P_UNKNOWN_CLUSTER", 64: "NOT_APPLIED",
+    34: "P_VH_ITEM_INVALID", 35: "P_UNKNOWN_CLUSTER", 64: "NOT_APPLIED", 65: "NOT_RUN",
 }
 OK = 0
 E_HISTORY_EMPTY = 1
@@ -227,7 +227,7 @@ TASK_TYPES = {0: "DecisionTask", 1: "ActivityTask", 2: "CloseExecution", 3: "Can
               8: "UpsertWorkflowSearchAttributes", 16: "DecisionTimeout", 17: "ActivityTimeout", 18: "UserTimer",
               19: "WorkflowTimeout", 20: "DeleteHistoryEvent", 22: "WorkflowBackoffTimer"}
 CdrCarry = _S("cdr_carry", [("src", C.c_void_p), ("caps", C.c_void_p), ("n_src", u32), ("_pad", u32),
-                            ("totals", CdrTotals), ("state", CdrOut)])
+                            ("totals", CdrTotals), ("state", CdrOut), ("in_memory", C.c_void_p)])
 CdrSlices = _S("cdr_slices", [
     ("n_slices", u32), ("_pad", u32), ("n_rows", u64), ("arena_words", u64)] + [(n, C.c_void_p) for n in (
         "slice_row0", "slice_len", "lane_wf", "slab", "arena", "slice_scratch_off", "slice_act_slots",
@@ -286,7 +286,10 @@ CdrDevBatch = _S("cdr_dev_batch", [
     ("n_fast_slices", u32), ("n_wave_slices", u32), ("n_reg_slices", u32), ("n_reg2_slices", u32),
     ("n_reg0_slices", u32), ("n_par_slices", u32), ("class_lo", u32 * 6), ("class_hi", u32 * 6),
     ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64), ("carry", C.c_void_p),
-    ("cls_slab", C.c_void_p), ("cls_row0", C.c_void_p), ("cls_rows", C.c_void_p)])
+    ("cls_slab", C.c_void_p), ("cls_row0", C.c_void_p), ("cls_rows", C.c_void_p), ("skip", C.c_void_p)])
+CdrNdcRound = _S("cdr_ndc_round", [("tasks", C.c_void_p), ("task_items", C.c_void_p), ("rebuild", CdrDevBatch),
+                                   ("rebuild_out", CdrOut), ("apply", CdrDevBatch), ("apply_out", CdrOut),
+                                   ("dec", C.c_void_p), ("refresh_now", i64), ("refresh_flags", u32), ("_pad", u32)])
 
 # ------------------------------------------------------------------ synth
 CdrSynthParams = _S("cdr_synth_params", [
@@ -315,7 +318,7 @@ MIRRORS = {
     "cdr_wf_result": CdrWfResult, "cdr_wf_caps": CdrWfCaps, "cdr_totals": CdrTotals, "cdr_out": CdrOut,
     "cdr_slices": CdrSlices, "cdr_dev_batch": CdrDevBatch, "cdr_carry": CdrCarry,
     "cdr_task": CdrTask, "cdr_vh_token": CdrVHToken, "cdr_vh_branch": CdrVHBranch, "cdr_vhs": CdrVHS,
-    "cdr_ndc_task": CdrNdcTask, "cdr_ndc_decision": CdrNdcDecision, "cdr_last_decision": CdrLastDecision,
+    "cdr_ndc_task": CdrNdcTask, "cdr_ndc_decision": CdrNdcDecision, "cdr_ndc_round": CdrNdcRound, "cdr_last_decision": CdrLastDecision,
     "cdr_opts": CdrOpts, "cdr_ingest_in": CdrIngestIn, "cdr_ingest_out": CdrIngestOut,
 }
 
@@ -367,6 +370,9 @@ EXPORTS = {
                                            C.POINTER(CdrOut), C.c_void_p]),
     "cdr_vhs_sync_async": (i32, [C.c_void_p, u32, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(CdrOut),
                                  C.c_void_p]),
+    "cdr_ndc_replicate_async": (i32, [C.c_void_p, u32, C.POINTER(CdrNdcRound), C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.POINTER(CdrOut), C.c_void_p]),
+    "cdr_plan_ndc_apply": (i32, [C.POINTER(CdrBatch), C.c_void_p, C.c_void_p, C.POINTER(CdrTotals)]),
     "cdr_fingerprint32": (u32, [C.c_char_p, C.c_size_t]),
     "cdr_workflow_id_to_shard": (i32, [C.c_char_p, C.c_size_t, i32]),
     "cdr_last_kernel_ms": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),

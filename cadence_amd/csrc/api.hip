@@ -338,6 +338,7 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
     dc.state.signal = (cdr_signal_info*)up(WS_CY_SIGNAL, hc.state.signal, t.signal * sizeof(cdr_signal_info));
     dc.state.rp = (cdr_reset_point*)up(WS_CY_RP, hc.state.rp, t.rp * sizeof(cdr_reset_point));
     dc.state.sa = (cdr_kv*)up(WS_CY_SA, hc.state.sa, t.sa * sizeof(cdr_kv));
+    if (hc.in_memory) dc.in_memory = (const uint8_t*)up(WS_CY_INMEM, hc.in_memory, (uint64_t)b->n_wfs);
     dc.state.transfer = dc.state.timer_tasks = nullptr;
     dc.state.n_tasks = nullptr;
     dc.state.last_decision = nullptr;

@@ -20,7 +20,7 @@ enum cdr_ws_slot {
   WS_ROW0, WS_SLEN, WS_LANE, WS_SLAB, WS_ARENA, WS_SFLAGS, WS_SC_OFF, WS_SC_ACT, WS_SC_TIM, WS_SCRATCH,
   WS_WFS, WS_CAPS, WS_KVS, WS_RPS,
   WS_CY_SRC, WS_CY_CAPS, WS_CY_RESULT, WS_CY_EXEC, WS_CY_REPL, WS_CY_VH, WS_CY_ACT, WS_CY_TIMER, WS_CY_CHILD,
-  WS_CY_CANCEL, WS_CY_SIGNAL, WS_CY_RP, WS_CY_SA, WS_CY_DESC,
+  WS_CY_CANCEL, WS_CY_SIGNAL, WS_CY_RP, WS_CY_SA, WS_CY_DESC, WS_CY_INMEM,
   WS_O_RESULT, WS_O_EXEC, WS_O_REPL, WS_O_VH, WS_O_ACT, WS_O_TIMER, WS_O_CHILD, WS_O_CANCEL, WS_O_SIGNAL,
   WS_O_RP, WS_O_SA, WS_O_XFER, WS_O_TTASK, WS_O_NTASKS, WS_O_LD,
   WS_CLS_ROWS, WS_CLS_ROW0, WS_CLS_SLAB,  // class-sorted blocks (cdr_cls_plan_async / cdr_cls_pack_async)
@@ -34,6 +34,8 @@ enum cdr_ws_slot {
   WS_PL_CLS_ROWS, WS_PL_CLS_ROW0, WS_PL_CLS_SLAB,  // the ingested batch's own class-sorted blocks
   // cdr_encode_blobs_async (encode_var.hip)
   WS_ENC_SIZES, WS_ENC_TMP,
+  // cdr_ndc_replicate_async (ndc.hip)
+  WS_NDC_SKIP_RB, WS_NDC_SKIP_AP, WS_NDC_INMEM, WS_NDC_SRC, WS_NDC_CARRY,
   WS_NUM
 };
 

@@ -284,7 +284,22 @@ void pack_chunked(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t ro
 
 extern "C" {
 
+static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals, const cdr_wf_caps* bound);
+
 int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
+  return plan_caps_impl(b, caps, totals, nullptr);
+}
+
+int cdr_plan_ndc_apply(const cdr_batch* b, const cdr_wf_caps* state_caps, cdr_wf_caps* caps, cdr_totals* totals) {
+  if (!state_caps || (b && b->carry)) return CDR_API_EINVAL;
+  return plan_caps_impl(b, caps, totals, state_caps);
+}
+
+}  // extern "C"
+
+// `bound` (cdr_plan_ndc_apply): every entry replays onto a loaded state whose rows are at
+// most its state capacities (known only on the device when the launch is planned)
+static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals, const cdr_wf_caps* bound) {
   if (!b || !caps || !totals) return CDR_API_EINVAL;
   cdr_totals t{};
   for (uint32_t w = 0; w < b->n_wfs; w++) {
@@ -330,6 +345,21 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
       c.timer_live += r.n_timer;
       c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_REG | CDR_CAP_REG2 | CDR_CAP_REG0);
     }
+    if (bound) {  // the loaded rows' bound: the state's capacities
+      if (d.parent >= 0 || d.newrun >= 0) return CDR_API_EINVAL;  // one run per entry
+      const cdr_wf_caps& s = bound[w];
+      c.act_cap += s.act_cap;
+      c.timer_cap += s.timer_cap;
+      c.child_cap += s.child_cap;
+      c.cancel_cap += s.cancel_cap;
+      c.signal_cap += s.signal_cap;
+      c.vh_cap += s.vh_cap;
+      c.rp_cap += s.rp_cap;
+      c.sa_cap += s.sa_cap;
+      c.act_live += s.act_cap;
+      c.timer_live += s.timer_cap;
+      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_REG | CDR_CAP_REG2 | CDR_CAP_REG0);
+    }
     cdr_internal::task_caps(b->events + d.ev_off, d.ev_len, &c.xfer_cap, &c.ttask_cap);
     c.xfer_off = t.xfer;
     t.xfer += c.xfer_cap;
@@ -356,6 +386,8 @@ int cdr_plan_caps(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals) {
   *totals = t;
   return CDR_API_OK;
 }
+
+extern "C" {
 
 int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
                        int32_t* lane_wf, uint32_t* slice_len, uint64_t* slice_row0, uint32_t* slice_flags,
@@ -947,6 +979,7 @@ uint64_t cdr_struct_size(const char* name) {
       {"cdr_vhs", sizeof(cdr_vhs)},
       {"cdr_ndc_task", sizeof(cdr_ndc_task)},
       {"cdr_ndc_decision", sizeof(cdr_ndc_decision)},
+      {"cdr_ndc_round", sizeof(cdr_ndc_round)},
   };
   for (const E& e : table)
     if (std::strcmp(e.n, name) == 0) return e.s;

@@ -18,6 +18,7 @@
 #include <cstdio>
 
 #include "cdr/cdr.h"
+#include "ctx.h"
 
 #define HIPCHK(x)                                                                                     \
   do {                                                                                                \
@@ -272,9 +273,169 @@ __global__ __launch_bounds__(256) void k_vhs_sync(uint32_t n, cdr_vhs* vhs, cdr_
   for (uint32_t i = 0; i < r.n_vh; i++) dst[i] = src[i];
 }
 
+// ---- cdr_ndc_replicate_async's steps (one thread per workflow)
+
+__device__ void zero_result(cdr_wf_result& r, int32_t code) {
+  r = cdr_wf_result{};
+  r.code = code;
+}
+
+// the state records of entry w := the source's (rows at the destination's capacities)
+__device__ void copy_state(const cdr_out& S, const cdr_wf_caps& sc, const cdr_out& D, const cdr_wf_caps& dc, uint32_t w) {
+  const cdr_wf_result r = S.result[w];
+  D.exec[w] = S.exec[w];
+  D.repl[w] = S.repl[w];
+  D.result[w] = r;
+  if (r.code != CDR_OK) return;
+  bool ok = true;
+  auto cp = [&](auto* src, auto* dst, uint64_t so, uint64_t doff, uint32_t n, uint32_t cap) {
+    if (n > cap) {
+      ok = false;
+      return;
+    }
+    for (uint32_t i = 0; i < n; i++) dst[doff + i] = src[so + i];
+  };
+  cp(S.act, D.act, sc.act_off, dc.act_off, r.n_activity, dc.act_cap);
+  cp(S.timer, D.timer, sc.timer_off, dc.timer_off, r.n_timer, dc.timer_cap);
+  cp(S.child, D.child, sc.child_off, dc.child_off, r.n_child, dc.child_cap);
+  cp(S.cancel, D.cancel, sc.cancel_off, dc.cancel_off, r.n_cancel, dc.cancel_cap);
+  cp(S.signal, D.signal, sc.signal_off, dc.signal_off, r.n_signal, dc.signal_cap);
+  cp(S.vh, D.vh, sc.vh_off, dc.vh_off, r.n_vh, dc.vh_cap);
+  cp(S.rp, D.rp, sc.rp_off, dc.rp_off, r.n_reset_points, dc.rp_cap);
+  cp(S.sa, D.sa, sc.sa_off, dc.sa_off, r.n_search_attr, dc.sa_cap);
+  if (!ok) D.result[w].code = CDR_E_BAD_INPUT;
+}
+
+// which workflows the rebuild replays (CDR_NDC_REBUILD of a live state); every output
+// record a step will not write is marked CDR_NOT_RUN; the apply carry's src map
+__global__ __launch_bounds__(256) void k_ndc_round_begin(uint32_t n, const cdr_ndc_decision* dec, cdr_out S,
+                                                         cdr_out RB, cdr_out AP, uint8_t* skip_rb, int32_t* src) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n) return;
+  const cdr_ndc_decision d = dec[w];
+  const bool rb = S.result[w].code == CDR_OK && d.code == CDR_OK && d.action == CDR_NDC_REBUILD;
+  skip_rb[w] = rb ? 0 : 1;
+  if (!rb) zero_result(RB.result[w], CDR_NOT_RUN);
+  zero_result(AP.result[w], CDR_NOT_RUN);
+  src[w] = (int32_t)w;
+}
+
+// after the rebuild (+ refresh + verification): the rebuilt state replaces the workflow's
+// (nDCConflictResolver.prepareMutableState returns it, :107-113) and is applied onto in
+// memory; which workflows the apply replays
+__global__ __launch_bounds__(256) void k_ndc_round_adopt_rebuilt(uint32_t n, const cdr_ndc_decision* dec,
+                                                                 const cdr_wf_caps* sc, cdr_out S,
+                                                                 const cdr_wf_caps* rc, cdr_out RB, uint8_t* skip_ap,
+                                                                 uint8_t* in_mem) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n) return;
+  const cdr_ndc_decision d = dec[w];
+  skip_ap[w] = 1;
+  in_mem[w] = 0;
+  if (S.result[w].code != CDR_OK) return;  // a failed workflow stays failed
+  if (d.code != CDR_OK) {                  // the branch manager's / conflict resolver's error
+    zero_result(S.result[w], d.code);
+    return;
+  }
+  if (d.action == CDR_NDC_REBUILD) {
+    if (RB.result[w].code != CDR_OK) {  // rebuild, refresh or verification failed
+      S.result[w] = RB.result[w];
+      return;
+    }
+    copy_state(RB, rc[w], S, sc[w], w);
+    if (S.result[w].code != CDR_OK) return;
+    in_mem[w] = 1;
+    skip_ap[w] = 0;
+  } else if (d.action == CDR_NDC_APPLY_CURRENT) {
+    skip_ap[w] = 0;
+  }
+}
+
+__global__ void k_ndc_carry_desc(cdr_carry* dst, cdr_carry c) { *dst = c; }
+
+// after the apply (+ VH sync): the applied state is the workflow's
+__global__ __launch_bounds__(256) void k_ndc_round_adopt_applied(uint32_t n, const uint8_t* skip_ap,
+                                                                 const cdr_wf_caps* sc, cdr_out S,
+                                                                 const cdr_wf_caps* ac, cdr_out AP) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n || skip_ap[w]) return;
+  if (AP.result[w].code != CDR_OK)
+    S.result[w] = AP.result[w];
+  else
+    copy_state(AP, ac[w], S, sc[w], w);
+}
+
 }  // namespace
 
 extern "C" {
+
+int cdr_ndc_replicate_async(cdr_ctx* ctx, uint32_t n, const cdr_ndc_round* R, cdr_vhs* vhs, cdr_vh_item* pool,
+                            const cdr_wf_caps* state_caps, const cdr_out* state, void* stream) {
+  if (!ctx || !R || !state || (n && (!R->tasks || !R->task_items || !vhs || !pool || !R->dec || !state_caps)))
+    return CDR_API_EINVAL;
+  if (n > R->rebuild.n_wfs || n > R->apply.n_wfs || R->apply.carry || !R->rebuild_out.transfer ||
+      !R->rebuild_out.timer_tasks || !R->rebuild_out.n_tasks)
+    return CDR_API_EINVAL;
+  if (n == 0) return CDR_API_OK;
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(cdr_ctx_device(ctx)));
+  uint8_t* skip_rb = (uint8_t*)cdr_ws_get(ctx, WS_NDC_SKIP_RB, n);
+  uint8_t* skip_ap = (uint8_t*)cdr_ws_get(ctx, WS_NDC_SKIP_AP, n);
+  uint8_t* in_mem = (uint8_t*)cdr_ws_get(ctx, WS_NDC_INMEM, n);
+  int32_t* src = (int32_t*)cdr_ws_get(ctx, WS_NDC_SRC, n * 4ull);
+  cdr_carry* carry_d = (cdr_carry*)cdr_ws_get(ctx, WS_NDC_CARRY, sizeof(cdr_carry));
+  if (!skip_rb || !skip_ap || !in_mem || !src || !carry_d) return CDR_API_ENOMEM;
+  const dim3 g((n + 255) / 256), b(256);
+  // 1. prepareVersionHistory + prepareMutableState
+  int rc = cdr_ndc_branch_async(ctx, R->tasks, R->task_items, n, vhs, pool, R->dec, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_ndc_round_begin, g, b, 0, st, n, R->dec, *state, R->rebuild_out, R->apply_out, skip_rb, src);
+  HIPCHK(hipGetLastError());
+  // 2. nDCStateRebuilder.rebuild of the REBUILD workflows, refreshTasks, verification
+  cdr_dev_batch rb = R->rebuild;
+  rb.skip = skip_rb;
+  rb.cls_slab = nullptr;
+  rb.cls_row0 = nullptr;
+  rb.cls_rows = nullptr;
+  cdr_out rbo = R->rebuild_out;
+  rbo.transfer = rbo.timer_tasks = nullptr;  // the replay emits no stateBuilder tasks here
+  rbo.n_tasks = nullptr;
+  if ((rc = cdr_replay_sliced_async(ctx, &rb, &rbo, stream))) return rc;
+  if ((rc = cdr_refresh_tasks_async(ctx, &rb, &R->rebuild_out, R->refresh_now, R->refresh_flags, stream))) return rc;
+  if ((rc = cdr_ndc_rebuild_verify_async(ctx, n, R->dec, vhs, pool, R->rebuild.caps, &R->rebuild_out, stream)))
+    return rc;
+  hipLaunchKernelGGL(k_ndc_round_adopt_rebuilt, g, b, 0, st, n, R->dec, state_caps, *state, R->rebuild.caps,
+                     R->rebuild_out, skip_ap, in_mem);
+  HIPCHK(hipGetLastError());
+  // 3. applyNonStartEventsToCurrentBranch: carry-in replay onto the (rebuilt or loaded) state
+  cdr_carry cy{};
+  cy.src = src;
+  cy.caps = state_caps;
+  cy.n_src = n;
+  cy.state = *state;
+  cy.state.transfer = cy.state.timer_tasks = nullptr;
+  cy.state.n_tasks = nullptr;
+  cy.state.last_decision = nullptr;
+  cy.in_memory = in_mem;
+  hipLaunchKernelGGL(k_ndc_carry_desc, dim3(1), dim3(1), 0, st, carry_d, cy);
+  HIPCHK(hipGetLastError());
+  cdr_dev_batch ap = R->apply;
+  ap.skip = skip_ap;
+  ap.carry = carry_d;
+  ap.cls_slab = nullptr;
+  ap.cls_row0 = nullptr;
+  ap.cls_rows = nullptr;
+  cdr_out apo = R->apply_out;
+  apo.transfer = apo.timer_tasks = nullptr;
+  apo.n_tasks = nullptr;
+  if ((rc = cdr_replay_sliced_async(ctx, &ap, &apo, stream))) return rc;
+  if ((rc = cdr_vhs_sync_async(ctx, n, vhs, pool, R->apply.caps, &R->apply_out, stream))) return rc;
+  // 4. the applied states become the workflows'
+  hipLaunchKernelGGL(k_ndc_round_adopt_applied, g, b, 0, st, n, skip_ap, state_caps, *state, R->apply.caps,
+                     R->apply_out);
+  HIPCHK(hipGetLastError());
+  return CDR_API_OK;
+}
 
 int cdr_ndc_branch_async(cdr_ctx* ctx, const cdr_ndc_task* tasks, const cdr_vh_item* task_items, uint32_t n,
                          cdr_vhs* vhs, cdr_vh_item* pool, cdr_ndc_decision* dec, void* stream) {

@@ -549,7 +549,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
                                           (int)(S.elems * CDR_EL_BYTES), 0x00020000);
   S.l4 = lane * 4u;
   const int32_t w = KA()->B.ev.lane_wf[(uint64_t)s * CDR_SLICE_WIDTH + lane];
-  if (w < 0) return;
+  if (w < 0 || (KA()->B.skip && KA()->B.skip[w])) return;  // empty lane / masked entry
 
   // per-workflow descriptor, capacities and output records, re-read where used
 #define B_ (KA()->B)
@@ -651,7 +651,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
     dorig_ts = x.decision_original_scheduled_ts;
     dreq = x.decision_request_id;
     dto = x.decision_timeout;
-    curv = CDR_EMPTY_VERSION;  // :291
+    curv = CDR_EMPTY_VERSION;  // :291 (an in-memory builder keeps its own: after the VH load below)
     if (isRS) {
       const cdr_repl_state rs0 = gget(gp(CY->state.repl) + csrc);
       gput(RS, rs0);
@@ -667,6 +667,10 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
       n_vh = cr.n_vh;
       vh_last_id = it.event_id;
       vh_last_ver = it.version;
+      // cdr_carry.in_memory: the rebuilt builder nDCConflictResolver.rebuild returns
+      // (nDCConflictResolver.go:117-184) never went through Load — its currentVersion is
+      // what the rebuild's replay left, its last version-history item's version
+      if (CY->in_memory && CY->in_memory[w]) curv = vh_last_ver;
     }
     hw_chi = live_chi = cr.n_child;
     for (uint32_t j = 0; j < hw_chi; j++) gput(chi + j, gget(gp(CY->state.child) + cc.child_off + j));
@@ -1685,7 +1689,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
 // turn high-water marks into live counts.
 __global__ __launch_bounds__(256) void k_tables(cdr_dev_batch B, cdr_out O) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= B.n_wfs) return;
+  if (w >= B.n_wfs || (B.skip && B.skip[w])) return;
   cdr_wf_result& r = O.result[w];
   if (r.code != CDR_OK) return;
   const cdr_wf_caps& cp = B.caps[w];
@@ -1715,7 +1719,7 @@ __global__ __launch_bounds__(256) void k_tables(cdr_dev_batch B, cdr_out O) {
 // run inherits the new run's error; a new run its parent never reached is NOT_APPLIED.
 __global__ void k_finalize(cdr_dev_batch B, cdr_out O) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= B.n_wfs) return;
+  if (w >= B.n_wfs || (B.skip && B.skip[w])) return;
   const int32_t c = B.wfs[w].newrun;
   if (c < 0) return;
   cdr_wf_result& P = O.result[w];
@@ -1824,7 +1828,13 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
   int n_side = hwq >= cdr_ctx::N_SIDE + 1 ? cdr_ctx::N_SIDE : 3;
   if (const char* e = std::getenv("CDR_SIDE_STREAMS")) n_side = std::atoi(e) == 3 ? 3 : cdr_ctx::N_SIDE;
   if (n_side == 3) {
-    static const int grouped[cdr_ctx::N_SIDE] = {0, 0, 0, 5, 5, 5, 6};  // wave, reg2, general | reg0, fast, reg | PAR
+    // the wave class alone (its longest histories are a tail nothing should queue
+    // behind) | every lane class | PAR (CDR_SIDE_GROUPS=<7 digits> overrides: class i's stream)
+    int grouped[cdr_ctx::N_SIDE] = {0, 5, 5, 5, 5, 5, 6};
+    if (const char* e = std::getenv("CDR_SIDE_GROUPS"))
+      if (std::strlen(e) == (size_t)cdr_ctx::N_SIDE)
+        for (int i = 0; i < cdr_ctx::N_SIDE; i++)
+          if (e[i] >= '0' && e[i] < '0' + cdr_ctx::N_SIDE) grouped[i] = e[i] - '0';
     for (int i = 0; i < cdr_ctx::N_SIDE; i++) c->side_of[i] = grouped[i];
   }
   bool need[cdr_ctx::N_SIDE] = {};  // only the streams some class launches on (each takes a queue)
@@ -1941,7 +1951,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
                    in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices + in->n_par_slices > 0 && !tasks &&
                    in->cluster.n_clusters <= (int)CDR_REG_NCL;
   // class-decomposed replay of the register-table slices (their class-sorted blocks)
-  const bool cls = reg && c->cls && in->cls_slab && in->cls_row0 && in->cls_rows;
+  const bool cls = reg && c->cls && in->cls_slab && in->cls_row0 && in->cls_rows && !in->skip;
   const bool cls_fb = c->cls != 2;  // 2 (tests): no k_replay_reg pass for the CLS_RETRY entries
   auto retry_of = [](cdr_launch x) {
     x.retry = 1u;

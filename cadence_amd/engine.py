@@ -69,11 +69,15 @@ class Carry:
     mutableStateBuilder.Load + applyEvents path (mutableStateBuilder.go:272-295)."""
     src: np.ndarray
     state: "Outputs"
+    in_memory: "np.ndarray | None" = None  # uint8 per entry: continue an in-memory builder (cdr_carry.in_memory)
 
     def cstruct(self) -> abi.CdrCarry:
         self.src = np.ascontiguousarray(self.src, dtype=np.int32)
         c = abi.CdrCarry()
         c.src = self.src.ctypes.data
+        if self.in_memory is not None:
+            self.in_memory = np.ascontiguousarray(self.in_memory, dtype=np.uint8)
+            c.in_memory = self.in_memory.ctypes.data
         c.caps = C.addressof(self.state.plan.caps)
         c.n_src = self.state.n_wfs
         c.totals = self.state.plan.totals

@@ -1,27 +1,25 @@
-"""NDC replication with forked histories: branch management, conflict-resolution
-rebuild and apply, over batches of workflows.
+"""NDC replication with forked histories over batches of workflows:
+branch management, conflict-resolution rebuild and apply — nDCHistoryReplicator.applyNonStartEvents
+(service/history/nDCHistoryReplicator.go:246-470) for one replication task per workflow per round.
 
-The flow restates nDCHistoryReplicator.applyNonStartEvents
-(service/history/nDCHistoryReplicator.go:246-470) for one replication task per
-workflow at a time:
+``DeviceReplicator`` drives the device-resident pipeline behind the C ABI: the base branch
+replayed into a state buffer, then one ``cdr_ndc_replicate_async`` call per round, which runs
+on the device, with no host round trip and no allocation:
 
-1. ``branch``: nDCBranchMgr.prepareVersionHistory + nDCConflictResolver.prepareMutableState
-   (ndc.hip ``k_ndc_branch``) decide per workflow: skip, apply to the current branch,
-   rebuild the task's branch first, or backfill a non-current branch (VH only).
-2. ``REBUILD`` workflows: nDCStateRebuilder.rebuild replays the branch's events 1..lastItem
-   (the replay kernels, NDC builder, expected next event ID) and
-   nDCConflictResolver.rebuild verifies the rebuilt VersionHistory and switches the
-   current branch (``k_ndc_rebuild_verify``).
-3. applyNonStartEventsToCurrentBranch: the task's events replay onto the current (or
-   rebuilt) state (carry-in replay), and the replay's VersionHistory becomes the current
-   branch's (``k_vhs_sync``).
+1. nDCBranchMgr.prepareVersionHistory + nDCConflictResolver.prepareMutableState
+   (``k_ndc_branch``): skip, apply to the current branch, rebuild the task's branch first,
+   or backfill a non-current branch (VH only);
+2. ``REBUILD`` workflows: nDCStateRebuilder.rebuild (nDCStateRebuilder.go:92-160) replays the
+   branch's events 1..lastItem (the replay kernels, the other workflows masked), then
+   refreshTasks, then nDCConflictResolver.rebuild verifies the rebuilt VersionHistory and
+   switches the current branch (nDCConflictResolver.go:117-184);
+3. applyNonStartEventsToCurrentBranch (:330-398): the task's events replay onto the rebuilt
+   state as the resolver hands it over — in memory, no Load (cdr_carry.in_memory) — or onto
+   the loaded current state; the replay's VersionHistory becomes the current branch's.
 
-The compute steps go through a backend (``GpuBackend`` here: the HIP kernels behind the
-C ABI); this module is the host control flow between them.  After the rebuild the
-reference keeps the rebuilt builder in memory; here the apply step reloads it (carry-in,
-``mutableStateBuilder.Load`` semantics: currentVersion = EmptyVersion until the first
-event of a running workflow sets it) — identical unless a closed workflow receives a
-decision-failure event.
+This module is plumbing: planning, packing and device buffers (the HIP runtime the engine's
+context uses).  The CPU restatement is ``oracle.ndc_replicate`` (replay_ref.cpp
+cdro_ndc_replicate_round), which keeps each rebuilt MutableState itself in memory.
 """
 from __future__ import annotations
 
@@ -55,189 +53,272 @@ TABLE_CAP = {"act": "act_cap", "timer": "timer_cap", "child": "child_cap", "canc
 TABLE_OFF = {t: c.replace("_cap", "_off") for t, c in TABLE_CAP.items()}
 
 
-def gather_outputs(sources):
-    """One Outputs holding, for entry w, the persisted state sources[w] = (Outputs, index)
-    (None: an empty entry), with its own compact Plan — the loaded states of a carry-in."""
-    n = len(sources)
-    caps = (abi.CdrWfCaps * max(1, n))()
-    tot = abi.CdrTotals()
-    for w, src in enumerate(sources):
-        if src is None:
-            continue
-        o, j = src
-        r = o.result[j]
-        for t, cname in TABLE_CAP.items():
-            cnt = getattr(r, engine.TABLE_COUNT[t]) if r.code == abi.OK else 0
-            setattr(caps[w], TABLE_OFF[t], getattr(tot, t))
-            setattr(caps[w], cname, cnt)
-            setattr(tot, t, getattr(tot, t) + cnt)
-    pl = engine.Plan(caps=caps, totals=tot)
-
-    class _B:  # the Outputs constructor only needs n_wfs
-        pass
-    b = _B()
-    b.n_wfs = n
-    out = engine.Outputs(b, pl)
-    for w, src in enumerate(sources):
-        if src is None:
-            out.result[w].code = abi.E_HISTORY_EMPTY
-            continue
-        o, j = src
-        C.memmove(C.byref(out.result[w]), C.byref(o.result[j]), C.sizeof(abi.CdrWfResult))
-        C.memmove(C.byref(out.exec[w]), C.byref(o.exec[j]), C.sizeof(abi.CdrExecInfo))
-        C.memmove(C.byref(out.repl[w]), C.byref(o.repl[j]), C.sizeof(abi.CdrReplState))
-        if o.result[j].code != abi.OK:
-            continue
-        for t in engine.TABLES:
-            cnt = getattr(caps[w], TABLE_CAP[t])
-            if cnt:
-                sz = C.sizeof(engine.TABLE_TYPES[t])
-                src_off = getattr(o.plan.caps[j], TABLE_OFF[t])
-                C.memmove(C.addressof(out.tables[t]) + getattr(caps[w], TABLE_OFF[t]) * sz,
-                          C.addressof(o.tables[t]) + src_off * sz, cnt * sz)
-    return out
-
-
-def _masked(batch: engine.Batch, keep) -> engine.Batch:
-    """The batch with the events of entries not in `keep` removed (ev_len 0)."""
-    wfs = (abi.CdrWfDesc * batch.n_wfs)()
-    C.memmove(wfs, batch.wfs, C.sizeof(wfs))
-    for w in range(batch.n_wfs):
-        if not keep[w]:
-            wfs[w].ev_len = 0
-    return engine._entry_batch(batch, wfs)
-
-
 class GpuBackend:
-    """The HIP path: replays through cdr_replay_batch, branch bookkeeping through the
-    ndc.hip kernels (device buffers via the HIP runtime)."""
+    """k_ndc_branch alone (the branch-kernel parity test): one cdr_ndc_branch_async call."""
 
     def __init__(self, eng: engine.Engine):
         self.eng = eng
 
-    def replay(self, batch: engine.Batch) -> engine.Outputs:
-        return self.eng.replay(batch)
-
-    def _run(self, fn, inputs, outputs):
-        """Upload ctypes arrays, call fn(device pointers...), download `outputs`."""
-        hip = engine._hip()
-        ptrs = {}
-        try:
-            for k, a in {**inputs, **outputs}.items():
-                p = C.c_void_p()
-                nb = max(8, C.sizeof(a))
-                if hip.hipMalloc(C.byref(p), C.c_size_t(nb)) != 0:
-                    raise RuntimeError("hipMalloc failed")
-                ptrs[k] = p
-                if hip.hipMemcpy(p, C.addressof(a), C.c_size_t(C.sizeof(a)), 1) != 0:
-                    raise RuntimeError("hipMemcpy H2D failed")
-            rc = fn(ptrs)
-            if rc:
-                raise RuntimeError(f"ndc kernel rc={rc}")
-            for k, a in outputs.items():  # hipMemcpy D2H synchronises the default stream
-                if hip.hipMemcpy(C.addressof(a), ptrs[k], C.c_size_t(C.sizeof(a)), 2) != 0:
-                    raise RuntimeError("hipMemcpy D2H failed")
-        finally:
-            for p in ptrs.values():
-                hip.hipFree(p)
-
     def branch(self, tasks, items, vhs, pool, n):
-        dec = (abi.CdrNdcDecision * max(1, n))()
-        L = abi.lib()
-        self._run(lambda p: L.cdr_ndc_branch_async(self.eng.ctx, p["tasks"], p["items"], n, p["vhs"], p["pool"],
-                                                   p["dec"], None),
-                  {"tasks": tasks, "items": items}, {"vhs": vhs, "pool": pool, "dec": dec})
-        return dec
-
-    def _out_dev(self, p, out: engine.Outputs):
-        o = abi.CdrOut()
-        o.result, o.exec, o.vh = p["result"], p["exec"], p["vh"]
-        return o
-
-    def rebuild_verify(self, dec, vhs, pool, out: engine.Outputs, n):
-        L = abi.lib()
-
-        def fn(p):
-            o = self._out_dev(p, out)
-            return L.cdr_ndc_rebuild_verify_async(self.eng.ctx, n, p["dec"], p["vhs"], p["pool"], p["caps"],
-                                                  C.byref(o), None)
-        self._run(fn, {"dec": dec, "pool": pool, "caps": out.plan.caps, "vh": out.tables["vh"]},
-                  {"vhs": vhs, "result": out.result, "exec": out.exec})
-
-    def vhs_sync(self, vhs, pool, out: engine.Outputs, n):
-        L = abi.lib()
-
-        def fn(p):
-            o = self._out_dev(p, out)
-            return L.cdr_vhs_sync_async(self.eng.ctx, n, p["vhs"], p["pool"], p["caps"], C.byref(o), None)
-        self._run(fn, {"caps": out.plan.caps, "result": out.result, "exec": out.exec, "vh": out.tables["vh"]},
-                  {"vhs": vhs, "pool": pool})
+        dev = _Dev()
+        try:
+            dec = (abi.CdrNdcDecision * max(1, n))()
+            pv, pp, pd = dev.up(vhs), dev.up(pool), dev.up(dec)
+            rc = abi.lib().cdr_ndc_branch_async(self.eng.ctx, C.c_void_p(dev.up(tasks)), C.c_void_p(dev.up(items)),
+                                                n, C.c_void_p(pv), C.c_void_p(pp), C.c_void_p(pd), None)
+            if rc:
+                raise RuntimeError(f"cdr_ndc_branch_async rc={rc}")
+            dev.down(vhs, pv)
+            dev.down(pool, pp)
+            dev.down(dec, pd)
+            return dec
+        finally:
+            dev.close()
 
 
-def replicate(be, base: engine.Batch, rebuild: engine.Batch, forks, items_cap: int = ITEMS_CAP):
-    """Replicate every workflow's base branch from scratch, then each fork task in turn
-    (forks = [(events batch, tasks, task items), ...], one task per workflow, entry order
-    of `base`).  Returns (final state Outputs, vhs, pool, [decisions per fork],
-    {"replayed_events": n})."""
+# ------------------------------------------------------------ device-resident rounds
+class _Dev:
+    """Device buffers through the HIP runtime the engine's context already uses."""
+
+    def __init__(self):
+        self.hip = engine._hip()
+        self.ptrs = []
+
+    def alloc(self, nbytes: int, zero: bool = True) -> int:
+        p = C.c_void_p()
+        nb = max(8, int(nbytes))
+        if self.hip.hipMalloc(C.byref(p), C.c_size_t(nb)) != 0:
+            raise RuntimeError("hipMalloc failed")
+        self.ptrs.append(p)
+        if zero and self.hip.hipMemset(p, 0, C.c_size_t(nb)) != 0:
+            raise RuntimeError("hipMemset failed")
+        return p.value
+
+    def up(self, x) -> int:
+        if isinstance(x, np.ndarray):
+            x = np.ascontiguousarray(x)
+            nb, src = x.nbytes, x.ctypes.data
+        else:
+            nb, src = C.sizeof(x), C.addressof(x)
+        p = self.alloc(nb, zero=False)
+        if nb and self.hip.hipMemcpy(C.c_void_p(p), C.c_void_p(src), C.c_size_t(nb), 1) != 0:
+            raise RuntimeError("hipMemcpy H2D failed")
+        return p
+
+    def down(self, dst, p: int, nbytes: int | None = None):
+        nb = C.sizeof(dst) if nbytes is None else nbytes
+        if nb and self.hip.hipMemcpy(C.c_void_p(C.addressof(dst)), C.c_void_p(p), C.c_size_t(nb), 2) != 0:
+            raise RuntimeError("hipMemcpy D2H failed")
+
+    def close(self):
+        for p in self.ptrs:
+            self.hip.hipFree(p)
+        self.ptrs = []
+
+
+def _plan_from(caps, totals) -> engine.Plan:
+    return engine.Plan(caps=caps, totals=totals)
+
+
+def offsets_from_caps(caps, n):
+    """Re-derive every table's offsets (exclusive prefix of its capacities) and the totals."""
+    tot = abi.CdrTotals()
+    for w in range(n):
+        for t, cname in TABLE_CAP.items():
+            setattr(caps[w], TABLE_OFF[t], getattr(tot, t))
+            setattr(tot, t, getattr(tot, t) + getattr(caps[w], cname))
+        caps[w].xfer_off, caps[w].ttask_off = tot.xfer, tot.ttask
+        tot.xfer += caps[w].xfer_cap
+        tot.ttask += caps[w].ttask_cap
+    return tot
+
+
+def upload_batch(dev: _Dev, batch: engine.Batch, caps, mode: int = abi.PLAN_WAVE | abi.PLAN_PAR) -> abi.CdrDevBatch:
+    """Host planning + packing (cdr_plan_slices_ex / cdr_pack_slices / cdr_plan_scratch)
+    of `batch` with capacities `caps`, uploaded: a device-resident cdr_dev_batch (no
+    class-sorted blocks)."""
+    L = abi.lib()
+    n = batch.n_wfs
+    ns, rows, nw = C.c_uint32(), C.c_uint64(), C.c_uint32()
+    rc = L.cdr_plan_slices_ex(batch.wfs, caps, n, mode, None, None, None, None, C.byref(ns), C.byref(rows),
+                              C.byref(nw))
+    if rc:
+        raise RuntimeError(f"cdr_plan_slices_ex rc={rc}")
+    lane = np.zeros(max(1, ns.value) * 64, np.int32)
+    slen = np.zeros(max(1, ns.value), np.uint32)
+    row0 = np.zeros(max(1, ns.value), np.uint64)
+    flags = np.zeros(max(1, ns.value), np.uint32)
+    L.cdr_plan_slices_ex(batch.wfs, caps, n, mode, lane.ctypes.data, slen.ctypes.data, row0.ctypes.data,
+                         flags.ctypes.data, C.byref(ns), C.byref(rows), C.byref(nw))
+    bs = batch.cstruct()
+    aw = L.cdr_plan_arena_words(C.byref(bs))
+    slab = np.zeros(max(1, int(rows.value)) * 64 * abi.EL_BYTES, np.uint8)
+    arena = np.zeros(max(1, aw), np.uint64)
+    s = abi.CdrSlices(n_slices=ns.value, n_rows=rows.value, arena_words=aw)
+    s.slice_row0, s.slice_len, s.lane_wf = row0.ctypes.data, slen.ctypes.data, lane.ctypes.data
+    s.slab, s.arena, s.slice_flags = slab.ctypes.data, arena.ctypes.data, flags.ctypes.data
+    rc = L.cdr_pack_slices(C.byref(bs), C.byref(s), 0)
+    if rc:
+        raise RuntimeError(f"cdr_pack_slices rc={rc}")
+    sc_off = np.zeros(max(1, ns.value), np.uint64)
+    sc_act = np.zeros(max(1, ns.value), np.uint32)
+    sc_tim = np.zeros(max(1, ns.value), np.uint32)
+    words, nf = C.c_uint64(), C.c_uint32()
+    rc = L.cdr_plan_scratch(caps, lane.ctypes.data, ns.value, sc_off.ctypes.data, sc_act.ctypes.data,
+                            sc_tim.ctypes.data, flags.ctypes.data, C.byref(words), C.byref(nf))
+    if rc:
+        raise RuntimeError(f"cdr_plan_scratch rc={rc}")
+    db = abi.CdrDevBatch()
+    db.ev.n_slices, db.ev.n_rows, db.ev.arena_words = ns.value, rows.value, aw
+    db.ev.slice_row0, db.ev.slice_len, db.ev.lane_wf = dev.up(row0), dev.up(slen), dev.up(lane)
+    db.ev.slab, db.ev.arena = dev.up(slab), dev.up(arena)
+    db.ev.slice_scratch_off, db.ev.slice_act_slots, db.ev.slice_tim_slots = dev.up(sc_off), dev.up(sc_act), dev.up(sc_tim)
+    db.ev.slice_flags = dev.up(flags)
+    db.scratch = dev.alloc(int(words.value) * 8)
+    db.wfs, db.caps = dev.up(batch.wfs), dev.up(caps)
+    db.kvs = dev.up(batch.kvs) if len(batch.kvs) else dev.alloc(8)
+    db.rps = dev.up(batch.rps) if len(batch.rps) else dev.alloc(8)
+    db.n_wfs = n
+    db.empty_uuid, db.cluster, db.now_ns, db.uuid_seed = batch.empty_uuid, batch.cluster, batch.now_ns, batch.uuid_seed
+    f = flags[:ns.value]
+    db.n_fast_slices = nf.value
+    db.n_wave_slices = int(((f & abi.SLICE_WAVE) != 0).sum())
+    db.n_reg_slices = int(((f & abi.SLICE_REG) != 0).sum())
+    db.n_reg2_slices = int(((f & abi.SLICE_REG2) != 0).sum())
+    db.n_reg0_slices = int(((f & abi.SLICE_REG0) != 0).sum())
+    db.n_par_slices = int(((f & abi.SLICE_PAR) != 0).sum())
+    db.max_act_slots = int(sc_act[:ns.value].max()) if ns.value else 0
+    db.max_tim_slots = int(sc_tim[:ns.value].max()) if ns.value else 0
+    L.cdr_plan_class_ranges(flags.ctypes.data, ns.value, db.class_lo, db.class_hi)
+    return db
+
+
+def alloc_out(dev: _Dev, n: int, totals: abi.CdrTotals, tasks: bool = False) -> abi.CdrOut:
+    o = abi.CdrOut()
+    o.result = dev.alloc(max(1, n) * C.sizeof(abi.CdrWfResult))
+    o.exec = dev.alloc(max(1, n) * C.sizeof(abi.CdrExecInfo))
+    o.repl = dev.alloc(max(1, n) * C.sizeof(abi.CdrReplState))
+    for t in engine.TABLES:
+        setattr(o, t, dev.alloc(max(1, getattr(totals, t)) * C.sizeof(engine.TABLE_TYPES[t])))
+    if tasks:
+        o.transfer = dev.alloc(max(1, totals.xfer) * C.sizeof(abi.CdrTask))
+        o.timer_tasks = dev.alloc(max(1, totals.ttask) * C.sizeof(abi.CdrTask))
+        o.n_tasks = dev.alloc(2 * max(1, n) * 4)
+    return o
+
+
+def download_out(dev: _Dev, o: abi.CdrOut, n: int, pl: engine.Plan, tasks: bool = False) -> engine.Outputs:
+    class _B:
+        pass
+    b = _B()
+    b.n_wfs = n
+    out = engine.Outputs(b, pl, tasks)
+    dev.down(out.result, o.result)
+    dev.down(out.exec, o.exec)
+    dev.down(out.repl, o.repl)
+    for t in engine.TABLES:
+        dev.down(out.tables[t], getattr(o, t))
+    if tasks:
+        dev.down(out.tasks["xfer"], o.transfer)
+        dev.down(out.tasks["ttask"], o.timer_tasks)
+        dev.down(out.tasks["n"], o.n_tasks)
+    return out
+
+
+def state_caps_for(base: engine.Batch, rebuild: engine.Batch, forks):
+    """Per-workflow capacities of the state buffer a replication run keeps: the base replay's
+    flags, room for the largest state any round can leave (base or rebuilt rows + every
+    fork's new rows)."""
     n = base.n_wfs
-    out = be.replay(base)
-    events = int(sum(base.wfs[w].ev_len for w in range(n)))
-    state = [(out, w) for w in range(n)]
-    vhs, pool = new_vhs(n, items_cap)
-    be.vhs_sync(vhs, pool, out, n)
-    decisions = []
-    for fork_batch, tasks, items in forks:
-        dec = be.branch(tasks, items, vhs, pool, n)
-        decisions.append(dec)
-        act = [dec[w].action if dec[w].code == abi.OK and state[w][0].result[state[w][1]].code == abi.OK else -1
-               for w in range(n)]
-        rb = None
-        if any(a == abi.NDC_REBUILD for a in act):
-            keep = [a == abi.NDC_REBUILD for a in act]
-            rb = be.replay(_masked(rebuild, keep))
-            events += int(sum(rebuild.wfs[w].ev_len for w in range(n) if keep[w]))
-            be.rebuild_verify(dec, vhs, pool, rb, n)
-        src, apply = [], []
-        for w in range(n):
-            if act[w] == abi.NDC_REBUILD:
-                src.append((rb, w))
-                apply.append(True)
-            elif act[w] == abi.NDC_APPLY_CURRENT:
-                src.append(state[w])
-                apply.append(True)
-            else:
-                src.append(None)
-                apply.append(False)
-        if not any(apply):
-            continue
-        loaded = gather_outputs(src)
-        ab = _masked(fork_batch, apply)
-        ab.carry = engine.Carry(src=np.array([w if apply[w] else -1 for w in range(n)], np.int32), state=loaded)
-        ap = be.replay(ab)
-        events += int(sum(fork_batch.wfs[w].ev_len for w in range(n) if apply[w]))
-        be.vhs_sync(vhs, pool, ap, n)
-        for w in range(n):
-            if apply[w]:
-                state[w] = (ap, w)
-            elif dec[w].code != abi.OK:
-                state[w] = (_failed(dec[w].code), 0)
-    final = gather_outputs(state)
-    return final, vhs, pool, decisions, {"replayed_events": events}
+    bp = engine.plan(base)
+    parts = [engine.plan(rebuild)] + [engine.plan(fb) for fb, _, _ in forks]
+    caps = (abi.CdrWfCaps * max(1, n))()
+    C.memmove(caps, bp.caps, C.sizeof(abi.CdrWfCaps) * n)
+    for w in range(n):
+        for cname in TABLE_CAP.values():
+            setattr(caps[w], cname, getattr(bp.caps[w], cname) + sum(getattr(p.caps[w], cname) for p in parts))
+    tot = offsets_from_caps(caps, n)
+    return _plan_from(caps, tot)
 
 
-_FAILED = {}
+class DeviceReplicator:
+    """The device-resident replication run over a batch of workflows: the base branch
+    replayed into the state buffer, then one cdr_ndc_replicate_async call per fork round —
+    branch, rebuild + refresh + verify, apply onto the in-memory rebuilt or the loaded
+    state, VH sync, adopt — with every buffer allocated up front."""
 
+    def __init__(self, eng: engine.Engine, base: engine.Batch, rebuild: engine.Batch, forks, items_cap=ITEMS_CAP,
+                 refresh_flags: int = abi.REFRESH_ADVANCED_VISIBILITY):
+        n = base.n_wfs
+        L = abi.lib()
+        self.eng, self.n, self.dev = eng, n, _Dev()
+        dev = self.dev
+        self.state_plan = state_caps_for(base, rebuild, forks)
+        self.base_db = upload_batch(dev, base, self.state_plan.caps)
+        self.state = alloc_out(dev, n, self.state_plan.totals)
+        self.state_caps_d = self.base_db.caps  # the state's capacities (the base batch was planned with them)
+        self.rebuild_plan = engine.plan(rebuild)
+        self.rebuild_db = upload_batch(dev, rebuild, self.rebuild_plan.caps)
+        self.rebuild_out = alloc_out(dev, n, self.rebuild_plan.totals, tasks=True)
+        self.rounds = []
+        for fb, tasks, items in forks:
+            caps = (abi.CdrWfCaps * max(1, n))()
+            tot = abi.CdrTotals()
+            rc = L.cdr_plan_ndc_apply(C.byref(fb.cstruct()), self.state_plan.caps, caps, C.byref(tot))
+            if rc:
+                raise RuntimeError(f"cdr_plan_ndc_apply rc={rc}")
+            pl = _plan_from(caps, tot)
+            r = abi.CdrNdcRound()
+            r.tasks, r.task_items = dev.up(tasks), dev.up(items)
+            r.rebuild, r.rebuild_out = self.rebuild_db, self.rebuild_out
+            r.apply = upload_batch(dev, fb, caps, 0)
+            r.apply_out = alloc_out(dev, n, tot)
+            r.dec = dev.alloc(max(1, n) * C.sizeof(abi.CdrNdcDecision))
+            r.refresh_now = rebuild.now_ns
+            r.refresh_flags = refresh_flags
+            self.rounds.append((r, pl))
+        self.vhs_h, self.pool_h = new_vhs(n, items_cap)
+        self.vhs, self.pool = dev.up(self.vhs_h), dev.up(self.pool_h)
+        self.events = [int(sum(base.wfs[w].ev_len for w in range(n)))] + [
+            int(sum(fb.wfs[w].ev_len for w in range(n))) for fb, _, _ in forks]
 
-def _failed(code: int):
-    """A one-entry Outputs carrying only a failed result (a task that errored)."""
-    if code not in _FAILED:
-        class _B:
-            n_wfs = 1
-        caps = (abi.CdrWfCaps * 1)()
-        o = engine.Outputs(_B(), engine.Plan(caps=caps, totals=abi.CdrTotals()))
-        o.result[0].code = code
-        _FAILED[code] = o
-    return _FAILED[code]
+    def base_replay(self, stream=None):
+        L = abi.lib()
+        rc = L.cdr_replay_sliced_async(self.eng.ctx, C.byref(self.base_db), C.byref(self.state), C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"cdr_replay_sliced_async rc={rc}")
+        rc = L.cdr_vhs_sync_async(self.eng.ctx, self.n, C.c_void_p(self.vhs), C.c_void_p(self.pool),
+                                  C.c_void_p(self.state_caps_d), C.byref(self.state), C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"cdr_vhs_sync_async rc={rc}")
+
+    def round(self, k: int, stream=None):
+        r, _ = self.rounds[k]
+        rc = abi.lib().cdr_ndc_replicate_async(self.eng.ctx, self.n, C.byref(r), C.c_void_p(self.vhs),
+                                               C.c_void_p(self.pool), C.c_void_p(self.state_caps_d),
+                                               C.byref(self.state), C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"cdr_ndc_replicate_async rc={rc}")
+
+    def run(self):
+        """Base replay + every round; returns (state Outputs, vhs, pool, [decisions],
+        [(rebuild Outputs, apply Outputs) per round])."""
+        self.base_replay()
+        per_round, decs = [], []
+        for k, (r, pl) in enumerate(self.rounds):
+            self.round(k)
+            dec = (abi.CdrNdcDecision * max(1, self.n))()
+            self.dev.down(dec, r.dec)
+            decs.append(dec)
+            per_round.append((download_out(self.dev, self.rebuild_out, self.n, self.rebuild_plan, tasks=True),
+                              download_out(self.dev, r.apply_out, self.n, pl)))
+        self.dev.down(self.vhs_h, self.vhs)
+        self.dev.down(self.pool_h, self.pool)
+        state = download_out(self.dev, self.state, self.n, self.state_plan)
+        return state, self.vhs_h, self.pool_h, decs, per_round
+
+    def close(self):
+        self.dev.close()
 
 
 def synth_forked(config: int, n_wfs: int, seed: int, items_cap: int = ITEMS_CAP, **kw):

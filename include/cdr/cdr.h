@@ -244,6 +244,10 @@ typedef struct cdr_dev_batch {
   const uint8_t* cls_slab;
   const uint64_t* cls_row0; /* [n_slices + 1], exclusive scan of the blocks' rows */
   const uint32_t* cls_rows; /* [n_slices * 4] */
+  /* [n_wfs] device, nullable: entries with skip[w] != 0 are not replayed by this launch —
+   * their lanes stay idle and their output records untouched (the caller marks them,
+   * e.g. result.code = CDR_NOT_RUN).  A masked launch replays without class-sorted blocks. */
+  const uint8_t* skip;
 } cdr_dev_batch;
 
 /* Class-sorted blocks (replay_cls.inc).  Every register-table slice (CDR_SLICE_REG /
@@ -619,6 +623,46 @@ int cdr_ndc_rebuild_verify_async(cdr_ctx* ctx, uint32_t n, const cdr_ndc_decisio
                                  const cdr_vh_item* pool, const cdr_wf_caps* caps, const cdr_out* out, void* stream);
 int cdr_vhs_sync_async(cdr_ctx* ctx, uint32_t n, cdr_vhs* vhs, cdr_vh_item* pool, const cdr_wf_caps* caps,
                        const cdr_out* out, void* stream);
+
+/* One round of NDC replication tasks over n workflows, device-resident end to end — the
+ * batch form of nDCHistoryReplicator.applyNonStartEvents (service/history/
+ * nDCHistoryReplicator.go:246-470) for task w of workflow w:
+ *   1. nDCBranchMgr.prepareVersionHistory + nDCConflictResolver.prepareMutableState
+ *      (k_ndc_branch, as cdr_ndc_branch_async) -> dec[w];
+ *   2. CDR_NDC_REBUILD: nDCStateRebuilder.rebuild (nDCStateRebuilder.go:92-160) — entry w of
+ *      `rebuild` replayed on a fresh NDC builder (the other entries masked), the
+ *      next-event check, SetCurrentBranchToken, refreshTasks at refresh_now (its tasks in
+ *      rebuild_out) — then nDCConflictResolver.rebuild's verification and branch switch
+ *      (nDCConflictResolver.go:117-184, as cdr_ndc_rebuild_verify_async);
+ *   3. applyNonStartEventsToCurrentBranch (:330-398): entry w of `apply` replayed onto the
+ *      REBUILT state kept in memory (cdr_carry.in_memory: no Load) or, for
+ *      CDR_NDC_APPLY_CURRENT, onto the loaded current state; its VersionHistory becomes the
+ *      current branch's (as cdr_vhs_sync_async);
+ *   4. `state` (device records with per-entry capacities state_caps) := the applied state;
+ *      a task that fails leaves its error in state->result[w] (that workflow is skipped by
+ *      later rounds); skipped / backfilled tasks leave the state as it was.
+ * `rebuild` / `apply` are device-resident batches (host structs holding device pointers)
+ * with entry w = workflow w and no continue-as-new entries; `apply` is planned with
+ * cdr_plan_ndc_apply(state_caps) and both without class-sorted blocks.  rebuild_out needs
+ * transfer / timer_tasks / n_tasks (the refresher's task lists).  Entries a step does not
+ * run have result.code CDR_NOT_RUN in that step's output.  No device allocation once the
+ * context's workspace is warm; asynchronous on `stream`. */
+typedef struct cdr_ndc_round {
+  const cdr_ndc_task* tasks;     /* [n] device */
+  const cdr_vh_item* task_items; /* device */
+  cdr_dev_batch rebuild;
+  cdr_out rebuild_out;
+  cdr_dev_batch apply;
+  cdr_out apply_out;
+  cdr_ndc_decision* dec; /* [n] device, out */
+  int64_t refresh_now;   /* nDCStateRebuilder.rebuild's `now` */
+  uint32_t refresh_flags, _pad; /* CDR_REFRESH_* of the rebuild's refreshTasks */
+} cdr_ndc_round;
+int cdr_ndc_replicate_async(cdr_ctx* ctx, uint32_t n, const cdr_ndc_round* round, cdr_vhs* vhs, cdr_vh_item* pool,
+                            const cdr_wf_caps* state_caps, const cdr_out* state, void* stream);
+/* Capacities of a round's `apply` batch (cdr_plan_caps restated for carry-in entries whose
+ * loaded state has at most state_caps[w] rows; every entry replays in the general kernel). */
+int cdr_plan_ndc_apply(const cdr_batch* b, const cdr_wf_caps* state_caps, cdr_wf_caps* caps, cdr_totals* totals);
 
 /* ------------------------------------------------------------------ misc */
 

@@ -176,7 +176,9 @@ enum cdr_status {
   CDR_P_CHILD_STARTED_NIL = 33,     /* nil deref mutableStateBuilder.go:3319-3320 */
   CDR_P_VH_ITEM_INVALID = 34,       /* NewVersionHistoryItem panic versionHistory.go:36-42 */
   CDR_P_UNKNOWN_CLUSTER = 35,       /* ClusterNameForFailoverVersion panic metadata.go:193-200 */
-  CDR_NOT_APPLIED = 64              /* new-run history never applied (parent stopped first) */
+  CDR_NOT_APPLIED = 64,             /* new-run history never applied (parent stopped first) */
+  CDR_NOT_RUN = 65                  /* skipped entry of a masked launch (cdr_dev_batch.skip): the
+                                       record was not replayed this time (cdr_ndc_replicate_async) */
 };
 /* cdr_wf_result.flags */
 #define CDR_RF_IN_NEWRUN 0x1u      /* error raised while replaying newRunHistory */
@@ -669,6 +671,13 @@ typedef struct cdr_carry {
   uint32_t n_src, _pad;    /* entries in `state` */
   cdr_totals totals;       /* rows in each table of `state` */
   cdr_out state;           /* read only */
+  /* [n_wfs of the batch], nullable: entry w continues an IN-MEMORY builder rather than a
+   * loaded one — the state nDCConflictResolver.rebuild hands to applyEvents
+   * (nDCConflictResolver.go:117-184, nDCHistoryReplicator.go:330-398) never went through
+   * Load, so its NDC currentVersion is the one the rebuild's replay left: the version of its
+   * last event applied while running, which for a history that ends at (or before) its close
+   * event is its last version-history item's version.  0 = Load (EmptyVersion). */
+  const uint8_t* in_memory;
 } cdr_carry;
 
 /* ==================================================== NDC VERSION HISTORIES ===

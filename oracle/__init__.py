@@ -132,11 +132,7 @@ def synth_digests(config: int, index_map, seed: int, threads: int = 16, chunk: i
 
 
 class NdcBackend:
-    """The CPU restatement behind cadence_amd.ndc.replicate's compute steps: replays by
-    replay_ref.cpp, branch bookkeeping by ndc_ref.cpp."""
-
-    def replay(self, batch):
-        return replay(batch)
+    """ndc_ref.cpp's branch bookkeeping alone (the branch-kernel parity test)."""
 
     def branch(self, tasks, items, vhs, pool, n):
         from cadence_amd import abi
@@ -144,8 +140,50 @@ class NdcBackend:
         lib().cdro_ndc_branch(tasks, items, n, vhs, pool, dec)
         return dec
 
-    def rebuild_verify(self, dec, vhs, pool, out, n):
-        lib().cdro_ndc_rebuild_verify(n, dec, vhs, pool, out.plan.caps, C.byref(out.cstruct()))
 
-    def vhs_sync(self, vhs, pool, out, n):
-        lib().cdro_vhs_sync(n, vhs, pool, out.plan.caps, C.byref(out.cstruct()))
+def ndc_replicate(base, rebuild, forks, items_cap: int = 64, refresh_flags: int = 1, threads: int = 1):
+    """The NDC replication run restated on the CPU (replay_ref.cpp cdro_ndc_replicate_round:
+    per workflow, the rebuilt MutableState kept in memory between nDCStateRebuilder.rebuild
+    and applyEvents, nDCConflictResolver.go:117-184, nDCHistoryReplicator.go:330-398): the
+    base branch replayed into the state buffer, then each fork round.  Returns what
+    cadence_amd.ndc.DeviceReplicator.run returns: (state Outputs, vhs, pool, [decisions],
+    [(rebuild Outputs, apply Outputs) per round])."""
+    from cadence_amd import abi, engine, ndc
+    L = lib()
+    if not hasattr(L, "_ndc_round_bound"):
+        P = C.POINTER
+        L.cdro_ndc_replicate_round.restype = C.c_int
+        L.cdro_ndc_replicate_round.argtypes = [
+            C.c_uint32, P(abi.CdrNdcTask), P(abi.CdrVHItem), P(abi.CdrBatch), P(abi.CdrWfCaps), P(abi.CdrOut),
+            P(abi.CdrBatch), P(abi.CdrWfCaps), P(abi.CdrOut), P(abi.CdrVHS), P(abi.CdrVHItem), P(abi.CdrNdcDecision),
+            P(abi.CdrWfCaps), P(abi.CdrOut), C.c_int64, C.c_uint32, C.c_int]
+        L._ndc_round_bound = True
+    n = base.n_wfs
+    sp = ndc.state_caps_for(base, rebuild, forks)
+    state = engine.Outputs(base, sp)
+    rc = L.cdro_replay_batch(C.byref(base.cstruct()), sp.caps, C.byref(state.cstruct()), threads)
+    if rc:
+        raise RuntimeError(f"cdro_replay_batch rc={rc}")
+    vhs, pool = ndc.new_vhs(n, items_cap)
+    L.cdro_vhs_sync(n, vhs, pool, sp.caps, C.byref(state.cstruct()))
+    rp = engine.plan(rebuild)
+    decs, per_round = [], []
+    for fb, tasks, items in forks:
+        caps = (abi.CdrWfCaps * max(1, n))()
+        tot = abi.CdrTotals()
+        rc = abi.lib().cdr_plan_ndc_apply(C.byref(fb.cstruct()), sp.caps, caps, C.byref(tot))
+        if rc:
+            raise RuntimeError(f"cdr_plan_ndc_apply rc={rc}")
+        ap = engine.Plan(caps=caps, totals=tot)
+        rb_out = engine.Outputs(rebuild, rp, tasks=True)
+        ap_out = engine.Outputs(fb, ap)
+        dec = (abi.CdrNdcDecision * max(1, n))()
+        rc = L.cdro_ndc_replicate_round(n, tasks, items, C.byref(rebuild.cstruct()), rp.caps,
+                                        C.byref(rb_out.cstruct()), C.byref(fb.cstruct()), ap.caps,
+                                        C.byref(ap_out.cstruct()), vhs, pool, dec, sp.caps,
+                                        C.byref(state.cstruct()), rebuild.now_ns, refresh_flags, threads)
+        if rc:
+            raise RuntimeError(f"cdro_ndc_replicate_round rc={rc}")
+        decs.append(dec)
+        per_round.append((rb_out, ap_out))
+    return state, vhs, pool, decs, per_round

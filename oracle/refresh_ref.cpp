@@ -290,6 +290,23 @@ struct Refresh {
 
 }  // namespace
 
+// refreshTasks of entry w alone (cdro_ndc_replicate_round's rebuild step); returns the code
+extern "C" int cdro_refresh_one(const cdr_batch* b, const cdr_wf_caps* caps, cdr_out* out, int64_t now_ns,
+                                uint32_t flags, uint32_t w) {
+  if (!b || !caps || !out || w >= b->n_wfs || !out->transfer || !out->timer_tasks || !out->n_tasks) return -1;
+  Refresh R{b, caps, out, now_ns, flags};
+  out->n_tasks[2 * w] = out->n_tasks[2 * w + 1] = 0;
+  if (out->result[w].code != CDR_OK) return out->result[w].code;
+  const int32_t c = R.one(w);
+  if (c != CDR_OK) {
+    cdr_wf_result& r = out->result[w];
+    r.code = c;
+    r.fail_event_id = 0;
+    r.fail_index = 0;
+  }
+  return c;
+}
+
 extern "C" int cdro_refresh_tasks(const cdr_batch* b, const cdr_wf_caps* caps, cdr_out* out, int64_t now_ns,
                                   uint32_t flags) {
   if (!b || !caps || !out || !out->transfer || !out->timer_tasks || !out->n_tasks) return -1;

@@ -1326,7 +1326,14 @@ void replay_one(const cdr_batch* b, const Ctx* ctx, uint32_t w, const cdr_wf_cap
   cdr_wf_result& r = out->result[w];
   r = cdr_wf_result{};
   MutableState ms(ctx, (int)d.builder, d.failover_version, d.wf_key, d.retention_days);
-  if (b->carry && b->carry->src && b->carry->src[w] >= 0) load_state(ms, *b->carry, (uint32_t)b->carry->src[w]);
+  if (b->carry && b->carry->src && b->carry->src[w] >= 0) {
+    load_state(ms, *b->carry, (uint32_t)b->carry->src[w]);
+    // cdr_carry.in_memory: the builder was never Loaded (nDCConflictResolver.rebuild's
+    // result): its currentVersion is what its replay left — see cdro_ndc_replicate_round,
+    // which keeps the rebuilt MutableState itself and checks this shortcut against it
+    if (b->carry->in_memory && b->carry->in_memory[w] && ms.hasVH && !ms.vh.items.empty())
+      ms.currentVersion = ms.vh.items.back().version;
+  }
   StateBuilder sb{ctx, b, &ms};
   const cdr_event* ev = b->events + d.ev_off;
   const cdr_event* nr = nullptr;
@@ -1446,6 +1453,209 @@ int cdro_vh_add_or_update(cdr_vh_item* items, uint32_t* n, uint32_t cap, int64_t
 }
 
 // WorkflowExecutionInfo.UpdateWorkflowStateCloseStatus: 1 = accepted, 0 = rejected.
+// ---- NDC replication round (nDCHistoryReplicator.applyNonStartEvents,
+// nDCHistoryReplicator.go:246-470), restated per workflow with the rebuilt mutable state
+// KEPT IN MEMORY between nDCStateRebuilder.rebuild (nDCStateRebuilder.go:92-160) and
+// applyNonStartEventsToCurrentBranch (:330-398), as nDCConflictResolver.rebuild
+// (nDCConflictResolver.go:117-184) hands it over — the parity checker of
+// cdr_ndc_replicate_async, which continues from the rebuilt records instead.
+int cdro_ndc_branch(const cdr_ndc_task* tasks, const cdr_vh_item* task_items, uint32_t n, cdr_vhs* vhs,
+                    cdr_vh_item* pool, cdr_ndc_decision* dec);  // ndc_ref.cpp
+int cdro_refresh_one(const cdr_batch* b, const cdr_wf_caps* caps, cdr_out* out, int64_t now_ns, uint32_t flags,
+                     uint32_t w);  // refresh_ref.cpp
+
+static void copy_state(const cdr_out& src, const cdr_wf_caps& sc, cdr_out& dst, const cdr_wf_caps& dc, uint32_t w) {
+  const cdr_wf_result r = src.result[w];
+  dst.exec[w] = src.exec[w];
+  dst.repl[w] = src.repl[w];
+  dst.result[w] = r;
+  if (r.code != CDR_OK) return;
+  auto cp = [&](auto* s, auto* d, uint64_t so, uint64_t doff, uint32_t n, uint32_t cap) {
+    if (n > cap) {
+      dst.result[w].code = CDR_E_BAD_INPUT;
+      return;
+    }
+    for (uint32_t i = 0; i < n; i++) d[doff + i] = s[so + i];
+  };
+  cp(src.act, dst.act, sc.act_off, dc.act_off, r.n_activity, dc.act_cap);
+  cp(src.timer, dst.timer, sc.timer_off, dc.timer_off, r.n_timer, dc.timer_cap);
+  cp(src.child, dst.child, sc.child_off, dc.child_off, r.n_child, dc.child_cap);
+  cp(src.cancel, dst.cancel, sc.cancel_off, dc.cancel_off, r.n_cancel, dc.cancel_cap);
+  cp(src.signal, dst.signal, sc.signal_off, dc.signal_off, r.n_signal, dc.signal_cap);
+  cp(src.vh, dst.vh, sc.vh_off, dc.vh_off, r.n_vh, dc.vh_cap);
+  cp(src.rp, dst.rp, sc.rp_off, dc.rp_off, r.n_reset_points, dc.rp_cap);
+  cp(src.sa, dst.sa, sc.sa_off, dc.sa_off, r.n_search_attr, dc.sa_cap);
+}
+
+static void fail_result(cdr_wf_result& r, int32_t code) {
+  r = cdr_wf_result{};
+  r.code = code;
+}
+
+// applyEvents over every call of entry w of b onto ms (no continue-as-new runs)
+static GoErr apply_calls(const cdr_batch* b, const Ctx* ctx, uint32_t w, MutableState& ms) {
+  const cdr_wf_desc& d = b->wfs[w];
+  const cdr_event* ev = b->events + d.ev_off;
+  StateBuilder sb{ctx, b, &ms};
+  GoErr err;
+  if (d.ev_len == 0) err.code = CDR_E_HISTORY_EMPTY;
+  for (uint64_t s = 0; s < d.ev_len && err.ok();) {
+    uint64_t e = s + 1;
+    while (e < d.ev_len && !(ev[e].flags & CDR_EVF_BATCH_FIRST)) e++;
+    MutableState* nr = nullptr;
+    GoErr ne;
+    err = sb.applyEvents(d.request_id, d.workflow_id, d.run_id, d.domain_id, ev + s, (size_t)(e - s), (int64_t)s,
+                         nullptr, 0, false, 0, 0, &nr, &ne);
+    delete nr;
+    s = e;
+  }
+  if (err.ok() && d.expected_next_event_id != 0 && ms.ei.NextEventID != d.expected_next_event_id) {
+    err.code = CDR_E_REBUILD_NEXT_EVENT_ID;  // nDCStateRebuilder.go:139-143
+    err.event_id = d.ev_len ? ev[d.ev_len - 1].event_id : 0;
+    err.index = (int64_t)d.ev_len;
+  }
+  return err;
+}
+
+// replay_one's epilogue: the result record, and the state when OK; true = OK
+static bool finish(const GoErr& e, const MutableState& ms, const cdr_batch* b, uint32_t w, const cdr_wf_caps* caps,
+                   cdr_out* out) {
+  cdr_wf_result& r = out->result[w];
+  r = cdr_wf_result{};
+  r.code = e.code;
+  r.flags = e.flags;
+  r.fail_event_id = e.event_id;
+  r.fail_index = e.index;
+  if (e.ok() && !write_state(ms, b, w, caps, out)) r.code = CDR_E_BAD_INPUT;
+  return r.code == CDR_OK;
+}
+
+// the current branch's VersionHistory := the applied state's (cdr_vhs_sync's restatement)
+static void sync_vhs(cdr_vhs& s, cdr_vh_item* pool, const cdr_out& o, const cdr_wf_caps& c, uint32_t w) {
+  const cdr_wf_result& r = o.result[w];
+  if (r.code != CDR_OK || r.n_vh > s.items_cap) return;
+  if (s.n_branches == 0) {
+    s.n_branches = 1;
+    s.current = 0;
+  }
+  cdr_vh_branch& b = s.branch[s.current];
+  const cdr_exec_info& x = o.exec[w];
+  b.token = cdr_vh_token{x.branch_tree_id, 0, x.branch_id_lo, x.branch_id_hi};
+  b.n_items = r.n_vh;
+  b._pad = 0;
+  for (uint32_t i = 0; i < r.n_vh; i++) pool[s.items_off + (uint64_t)s.current * s.items_cap + i] = o.vh[c.vh_off + i];
+}
+
+int cdro_ndc_replicate_round(uint32_t n, const cdr_ndc_task* tasks, const cdr_vh_item* task_items,
+                             const cdr_batch* rebuild, const cdr_wf_caps* rebuild_caps, cdr_out* rebuild_out,
+                             const cdr_batch* apply, const cdr_wf_caps* apply_caps, cdr_out* apply_out,
+                             cdr_vhs* vhs, cdr_vh_item* pool, cdr_ndc_decision* dec, const cdr_wf_caps* state_caps,
+                             cdr_out* state, int64_t refresh_now, uint32_t refresh_flags, int threads) {
+  if (rebuild->n_wfs < n || apply->n_wfs < n) return -1;
+  Ctx rctx{rebuild, rebuild->empty_uuid}, actx{apply, apply->empty_uuid};
+  auto one = [&](uint32_t w) {
+    cdro_ndc_branch(tasks + w, task_items, 1, vhs + w, pool, dec + w);  // nDCBranchMgr + prepareMutableState
+    fail_result(rebuild_out->result[w], CDR_NOT_RUN);
+    fail_result(apply_out->result[w], CDR_NOT_RUN);
+    const cdr_ndc_decision d = dec[w];
+    if (state->result[w].code != CDR_OK) return;  // a failed workflow stays failed
+    if (d.code != CDR_OK) {
+      fail_result(state->result[w], d.code);
+      return;
+    }
+    if (d.action != CDR_NDC_REBUILD && d.action != CDR_NDC_APPLY_CURRENT) return;  // skip / backfill (VH only)
+    const cdr_wf_desc& ad = apply->wfs[w];
+    MutableState* ms = nullptr;
+    if (d.action == CDR_NDC_REBUILD) {
+      // nDCStateRebuilder.rebuild: a fresh NDC builder (initializeBuilders :165-176), every
+      // event 1 .. lastItem, the next-event check, SetCurrentBranchToken, refreshTasks
+      const cdr_wf_desc& rd = rebuild->wfs[w];
+      ms = new MutableState(&rctx, (int)rd.builder, rd.failover_version, rd.wf_key, rd.retention_days);
+      GoErr e = apply_calls(rebuild, &rctx, w, *ms);
+      ms->vh.has_token = true;  // SetCurrentBranchToken(targetBranchToken) (:144-146)
+      ms->vh.tree = d.rebuild_token.tree;
+      ms->vh.br_lo = d.rebuild_token.branch_lo;
+      ms->vh.br_hi = d.rebuild_token.branch_hi;
+      if (!finish(e, *ms, rebuild, w, rebuild_caps, rebuild_out)) {
+        state->result[w] = rebuild_out->result[w];
+        delete ms;
+        return;
+      }
+      const int32_t rc = cdro_refresh_one(rebuild, rebuild_caps, rebuild_out, refresh_now, refresh_flags, w);
+      if (rc != CDR_OK) {
+        state->result[w] = rebuild_out->result[w];
+        delete ms;
+        return;
+      }
+      // the refreshed timer-task marks belong to the in-memory state too
+      const cdr_wf_caps& rc0 = rebuild_caps[w];
+      for (uint32_t k = 0; k < rebuild_out->result[w].n_activity; k++) {
+        const cdr_activity_info& a = rebuild_out->act[rc0.act_off + k];
+        ms->pendingActivityInfoIDs[a.schedule_id].TimerTaskStatus = a.timer_task_status;
+      }
+      for (uint32_t k = 0; k < rebuild_out->result[w].n_timer; k++) {
+        const cdr_timer_info& t = rebuild_out->timer[rc0.timer_off + k];
+        ms->pendingTimerInfoIDs[t.timer_id].TaskID = t.task_id;
+      }
+      // nDCConflictResolver.rebuild: the rebuilt VersionHistory must Equal the branch's
+      cdr_vhs& s = vhs[w];
+      const cdr_vh_branch& br = s.branch[d.branch_index];
+      bool eq = br.n_items == ms->vh.items.size() && br.token.tree == d.rebuild_token.tree &&
+                br.token.branch_lo == d.rebuild_token.branch_lo && br.token.branch_hi == d.rebuild_token.branch_hi;
+      const cdr_vh_item* want = pool + s.items_off + (uint64_t)d.branch_index * s.items_cap;
+      for (size_t i = 0; eq && i < ms->vh.items.size(); i++)
+        eq = ms->vh.items[i].eventID == want[i].event_id && ms->vh.items[i].version == want[i].version;
+      if (!eq) {  // :161-165 (the failed record keeps its flags, as cdr_ndc_rebuild_verify_async)
+        cdr_wf_result& r = rebuild_out->result[w];
+        const uint32_t fl = r.flags;
+        fail_result(r, CDR_E_REBUILD_VH_MISMATCH);
+        r.flags = fl;
+        state->result[w] = r;
+        delete ms;
+        return;
+      }
+      s.current = d.branch_index;  // SetCurrentVersionHistoryIndex (:172-174)
+      ms->ctx = &actx;             // the rebuilt builder continues with the task's events
+    } else {
+      // the persisted state, loaded (mutableStateBuilder.Load)
+      ms = new MutableState(&actx, (int)ad.builder, ad.failover_version, ad.wf_key, ad.retention_days);
+      cdr_carry cy{};
+      cy.caps = state_caps;
+      cy.state = *state;
+      load_state(*ms, cy, w);
+    }
+    // applyNonStartEventsToCurrentBranch: stateBuilder.applyEvents onto that state
+    GoErr e = apply_calls(apply, &actx, w, *ms);
+    if (!finish(e, *ms, apply, w, apply_caps, apply_out)) {
+      state->result[w] = apply_out->result[w];
+    } else {
+      sync_vhs(vhs[w], pool, *apply_out, apply_caps[w], w);
+      copy_state(*apply_out, apply_caps[w], *state, state_caps[w], w);
+    }
+    delete ms;
+  };
+  if (threads <= 1) {
+    for (uint32_t w = 0; w < n; w++) one(w);
+    return 0;
+  }
+  std::atomic<uint32_t> next{0};
+  std::vector<std::thread> th;
+  auto work = [&] {
+    for (uint32_t w0; (w0 = next.fetch_add(64)) < n;)
+      for (uint32_t w = w0; w < std::min(n, w0 + 64); w++) one(w);
+  };
+  for (int t = 1; t < threads; t++) {
+    try {
+      th.emplace_back(work);
+    } catch (const std::system_error&) {
+      break;
+    }
+  }
+  work();
+  for (auto& t : th) t.join();
+  return 0;
+}
+
 int cdro_state_transition(int from_state, int from_close, int to_state, int to_close) {
   ExecutionInfo e;
   e.State = from_state;

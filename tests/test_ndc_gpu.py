@@ -118,16 +118,34 @@ def test_ndc_branch_kernel_matches_oracle(engine_gpu, seed):
         assert want in seen, (want, seen)
 
 
+def _same_outputs(batch_n, a, b, what, tasks=False):
+    class _B:
+        n_wfs = batch_n
+    bad = engine.compare(_B(), a, b)
+    if tasks:
+        bad += engine.compare_tasks(_B(), a, b)
+    assert not bad, what + ": " + "\n".join(bad[:10])
+
+
 def _replicate_both(eng, base, rebuild, forks):
+    """The device pipeline (cdr_ndc_replicate_async per round) against the CPU restatement
+    (oracle.ndc_replicate: the rebuilt MutableState kept in memory): final states, version
+    histories, decisions, and each round's rebuild (+ refreshTasks) and apply records."""
     import oracle
-    got = ndc.replicate(ndc.GpuBackend(eng), base, rebuild, forks)
-    ref = ndc.replicate(oracle.NdcBackend(), base, rebuild, forks)
+    rep = ndc.DeviceReplicator(eng, base, rebuild, forks)
+    try:
+        got = rep.run()
+    finally:
+        rep.close()
+    ref = oracle.ndc_replicate(base, rebuild, forks, threads=4)
     n = base.n_wfs
-    bad = engine.compare(base, got[0], ref[0])
-    assert not bad, "\n".join(bad[:10])
+    _same_outputs(n, got[0], ref[0], "final state")
     assert _vhs_state(got[1], got[2], n) == _vhs_state(ref[1], ref[2], n)
-    for dg, dr in zip(got[3], ref[3]):
-        assert [bytes(dg[w]) for w in range(n)] == [bytes(dr[w]) for w in range(n)]
+    for k, (dg, dr) in enumerate(zip(got[3], ref[3])):
+        assert [bytes(dg[w]) for w in range(n)] == [bytes(dr[w]) for w in range(n)], k
+        (rg, ag), (rr, ar) = got[4][k], ref[4][k]
+        _same_outputs(n, rg, rr, f"round {k} rebuild", tasks=True)
+        _same_outputs(n, ag, ar, f"round {k} apply")
     return got
 
 
@@ -140,6 +158,28 @@ def test_handcrafted_three_branches_gpu(engine_gpu):
 @pytest.mark.parametrize("seed", [0x5EED0C05, 7])
 def test_forked_config5_gpu(engine_gpu, seed):
     base, rebuild, forks = ndc.synth_forked(5, 400, seed)
-    final, vhs, pool, decs, info = _replicate_both(engine_gpu, base, rebuild, forks)
+    final, vhs, pool, decs, rounds = _replicate_both(engine_gpu, base, rebuild, forks)
     assert engine.status_histogram(final) == {"OK": 400}
     assert {abi.NDC_ACTIONS[decs[1][w].action] for w in range(400)} == {"REBUILD", "BACKFILL"}
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_forked_config5_faults_gpu(engine_gpu, seed):
+    """Faulted forks: failing rebuilds / applies leave their errors in the state, later
+    rounds skip those workflows — identically on both sides."""
+    base, rebuild, forks = ndc.synth_forked(5, 300, seed, error_rate=0.2)
+    final, *_ = _replicate_both(engine_gpu, base, rebuild, forks)
+    assert len(engine.status_histogram(final)) > 1
+
+
+def test_in_memory_carry_gpu(engine_gpu):
+    """GPU twin of the in-memory carry KAT: the general kernel's carry prologue keeps the
+    rebuilt builder's currentVersion when cdr_carry.in_memory says so."""
+    import numpy as np
+    from . import test_ndc
+    suf, pre_out, outs = test_ndc.in_memory_case()
+    for mem in (0, 1):
+        suf.carry = engine.Carry(src=np.array([0], np.int32), state=pre_out, in_memory=np.array([mem], np.uint8))
+        got = engine_gpu.replay(suf)
+        bad = engine.compare(suf, got, outs[mem])
+        assert not bad, (mem, bad[:5])

@@ -5,8 +5,11 @@ profiles/<name>_pmc.txt and profiles/traffic_latest.json (read by bench.py).
 HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of
 a coalesced streaming read (128-B requests tallied at 64 B), so it is doubled;
-WRITE_SIZE is taken as is.  Counters are averaged over the profiled dispatches.
-usage: tools/traffic.py <tag> <workload> <profile-name> [kernel-substring]"""
+WRITE_SIZE is taken as is.  Counters are averaged over the profiled dispatches — or, with
+an anchor kernel (a multi-kernel step: C3-C5 run several replay kernels per step), summed
+over every matching dispatch and divided by the anchor's dispatch count (one per step).
+Writes profiles/traffic_<workload>.json (and traffic_latest.json).
+usage: tools/traffic.py <tag> <workload> <profile-name> [kernel-substring] [anchor-kernel]"""
 import collections
 import csv
 import glob
@@ -20,19 +23,29 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     tag, workload, name = sys.argv[1:4]
     kern = sys.argv[4] if len(sys.argv) > 4 else "k_replay"
+    anchor = sys.argv[5] if len(sys.argv) > 5 else None
     agg = collections.defaultdict(float)
     nd = collections.defaultdict(set)
+    steps = collections.defaultdict(set)  # per counter pass: the anchor's dispatches
+    kernels = collections.defaultdict(set)
     for f in glob.glob(os.path.join(ROOT, "gpurun_out", f"{tag}_pmc", "*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
+            if anchor and anchor in r["Kernel_Name"]:
+                steps[r["Counter_Name"]].add(r["Dispatch_Id"])
             if kern not in r["Kernel_Name"]:
                 continue
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
             nd[r["Counter_Name"]].add(r["Dispatch_Id"])
-    avg = {c: v / len(nd[c]) for c, v in agg.items()}
+            kernels[r["Kernel_Name"].split("(")[0]].add(r["Dispatch_Id"])
+    if anchor:
+        avg = {c: v / max(1, len(steps[c])) for c, v in agg.items()}
+    else:
+        avg = {c: v / len(nd[c]) for c, v in agg.items()}
     lines = [f"{c:24s} {v:.6g}" for c, v in sorted(avg.items())]
     waves = avg.get("SQ_WAVES", 0)
     out = {"workload": workload, "kernel": kern, "source": f"rocprofv3 --pmc passes, tools/pmc.sh ({tag})",
-           "counters": avg}
+           "per": f"step (sum over the matching kernels / {anchor} dispatches)" if anchor else "dispatch",
+           "kernels": sorted(kernels), "counters": avg}
     sha = os.path.join(ROOT, "gpurun_out", f"{tag}_pmc", "lib_sha1")
     if os.path.exists(sha):
         out["lib_sha1"] = open(sha).read().strip()
@@ -49,6 +62,7 @@ def main():
                 lines.append(f"{c} per wave            {avg[c] / waves:.1f}")
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     open(os.path.join(ROOT, "profiles", f"{name}_pmc.txt"), "w").write("\n".join(lines) + "\n")
+    json.dump(out, open(os.path.join(ROOT, "profiles", f"traffic_{workload}.json"), "w"), indent=1)
     json.dump(out, open(os.path.join(ROOT, "profiles", "traffic_latest.json"), "w"), indent=1)
     print("\n".join(lines))
 
