@@ -358,6 +358,9 @@ EXPORTS = {
     "cdr_encode_blobs_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut),
                                      C.POINTER(CdrStrtab), C.c_void_p, C.c_void_p, u64, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),
+    "cdr_encode_cql_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut),
+                                     C.POINTER(CdrStrtab), C.c_void_p, C.c_void_p, u64, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p]),
     "cdr_plan_class_ranges": (i32, [C.c_void_p, u32, C.c_void_p, C.c_void_p]),
     "cdr_compact_async": (i32, [C.c_void_p, i32, C.POINTER(CdrDevBatch), C.POINTER(CdrOut), C.c_void_p,
                                 C.c_void_p, C.c_void_p]),

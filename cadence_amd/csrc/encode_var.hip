@@ -393,8 +393,306 @@ __device__ void exec_row(Out& o, const Strs& S, const cdr_exec_info& x, const cd
   o.b(0);
 }
 
+// ================================================================ the Cassandra form
+// The bound values of the CQL statements the Cassandra persistence writes a row with
+// (common/persistence/cassandra/cassandraPersistenceUtil.go, templates in
+// cassandraPersistence.go:114-306,439-...): each a CQL native-protocol [bytes] value —
+// big-endian int32 length (-1 = null), then the value as gocql
+// (github.com/gocql/gocql v0.0.0-20171220143535-56a164ee9f31, go.mod:22; not vendored in
+// the reference, its marshalling restated from the CQL v4 protocol and gocql's marshal.go)
+// encodes it for the column's CQL type.
+struct Cql {
+  Out& o;
+  const Strs& S;
+  __device__ void i64(int64_t v) { o.be32(8), o.be64((uint64_t)v); }
+  __device__ void i32(int32_t v) { o.be32(4), o.be32((uint32_t)v); }
+  __device__ void boo(bool v) { o.be32(1), o.b(v ? 1u : 0u); }
+  __device__ void dbl(double v) { o.be32(8), o.be64((uint64_t)__double_as_longlong(v)); }
+  __device__ void null() { o.be32(0xFFFFFFFFu); }
+  __device__ void empty() { o.be32(0); }  // "" text; the zero time.Time (marshalTimestamp: []byte{})
+  // timestamp: milliseconds since the epoch, UTC().Unix()*1e3 + Nanosecond()/1e6 = floor(ns / 1e6)
+  __device__ void ts(int64_t ns, bool zero) {
+    if (zero) return empty();
+    const int64_t q = ns / 1000000, r = ns % 1000000;
+    i64(r < 0 ? q - 1 : q);
+  }
+  __device__ void text(uint32_t h) {
+    if (!S.ok(h)) o.err = o.err ? o.err : CDR_BLOB_E_HANDLE;
+    const uint64_t n = S.len(h);
+    o.be32((uint32_t)n);
+    if (n) o.raw(S.at(h), n);
+  }
+  __device__ void blob_or_null(uint32_t h) {  // a []byte field: handle 0 is Go's nil
+    if (h == 0) return null();
+    text(h);
+  }
+  __device__ void lit(const char* s, uint32_t n) { o.be32(n), o.lit(s, n); }
+  // uuid from a Go string: gocql ParseUUID (a '-' where an even number of hex digits has
+  // been read is skipped; exactly 32 hex digits) — CDR_BLOB_E_UUID where it fails
+  __device__ void uuid_str(uint32_t h) {
+    uint8_t u[16] = {};
+    const uint64_t n = S.len(h);
+    const uint8_t* s = S.at(h);
+    uint32_t j = 0;
+    bool ok = S.ok(h);
+    for (uint64_t i = 0; ok && i < n; i++) {
+      const uint32_t c = s[i];
+      if (c == '-' && (j & 1) == 0) continue;
+      const int v = c >= '0' && c <= '9' ? (int)(c - '0') : c >= 'a' && c <= 'f' ? (int)(c - 'a' + 10)
+                    : c >= 'A' && c <= 'F' ? (int)(c - 'A' + 10) : -1;
+      if (v < 0 || j >= 32) {
+        ok = false;
+        break;
+      }
+      u[j >> 1] |= (uint8_t)(v << ((j & 1) ? 0 : 4));
+      j++;
+    }
+    if (!ok || j != 32) o.err = o.err ? o.err : CDR_BLOB_E_UUID;
+    o.be32(16);
+    for (int i = 0; i < 16; i++) o.b(u[i]);
+  }
+  __device__ void uuid_val(uint64_t lo, uint64_t hi) { o.be32(16), o.be64(hi), o.be64(lo); }  // ParseUUID(uuid_text)
+  __device__ void uuid_const(uint32_t first_nibble) {  // emptyDomainID / emptyRunID "x0000000-0000-f000-f000-000000000000"
+    o.be32(16), o.be32(first_nibble << 28), o.be32(0x0000F000u), o.be32(0xF0000000u), o.be32(0);
+  }
+  // list<text> from a handle holding the thrift list<string> wire body (element type,
+  // i32 count, elements as i32 length + bytes): the CQL body is the same minus the type byte
+  __device__ void list_text(uint32_t h) {
+    if (h == 0) return null();
+    if (!S.ok(h) || S.len(h) < 5) {
+      o.err = o.err ? o.err : CDR_BLOB_E_HANDLE;
+      return null();
+    }
+    o.be32((uint32_t)(S.len(h) - 1));
+    o.raw(S.at(h) + 1, S.len(h) - 1);
+  }
+};
+
+__device__ void activity_cql(Out& o, const Strs& S, const cdr_activity_info& a) {  // updateActivityInfos :1264-1337
+  Cql q{o, S};
+  const bool tset = (a.flags & CDR_AI_STARTED_TIME_SET) != 0;
+  q.i64(a.schedule_id);  // activity_map[ ? ]
+  q.i64(a.version);
+  q.i64(a.schedule_id);
+  q.i64(a.scheduled_event_batch_id);
+  q.null();  // scheduled_event: nil on replay (FromDataBlob(nil) = nil, "")
+  q.ts(a.scheduled_time, false);
+  q.i64(a.started_id);
+  q.null();  // started_event
+  q.ts(a.started_time, !tset);
+  q.text(a.activity_id);
+  q.text(a.request_id);
+  q.null();  // details
+  q.i32(a.s2s);
+  q.i32(a.s2c);
+  q.i32(a.stc);
+  q.i32(a.hb);
+  q.boo((a.flags & CDR_AI_CANCEL_REQUESTED) != 0);
+  q.i64(a.cancel_request_id);
+  q.ts(a.last_heartbeat_time, !tset);
+  q.i32(a.timer_task_status);
+  q.i32(a.attempt);
+  q.text(a.task_list);
+  q.empty();  // started_identity ""
+  q.boo((a.flags & CDR_AI_HAS_RETRY) != 0);
+  q.i32(a.initial_interval);
+  q.dbl(a.backoff_coefficient);
+  q.i32(a.maximum_interval);
+  q.ts(a.expiration_time, false);
+  q.i32(a.maximum_attempts);
+  q.list_text(a.nonretriable);
+  q.empty();  // last_failure_reason ""
+  q.empty();  // last_worker_identity ""
+  q.null();   // last_failure_details nil
+  q.empty();  // event_data_encoding "" (no scheduled event)
+}
+__device__ void timer_cql(Out& o, const Strs& S, const cdr_timer_info& t) {  // updateTimerInfos :1384-1422
+  Cql q{o, S};
+  q.text(t.timer_id);  // timer_map[ ? ]
+  q.i64(t.version);
+  q.text(t.timer_id);
+  q.i64(t.started_id);
+  q.ts(t.expiry_time, false);
+  q.i64(t.task_id);
+}
+__device__ void child_cql(Out& o, const Strs& S, const cdr_child_info& c) {  // updateChildExecutionInfos :1444-1503
+  Cql q{o, S};
+  q.i64(c.initiated_id);  // child_executions_map[ ? ]
+  q.i64(c.version);
+  q.i64(c.initiated_id);
+  q.i64(c.initiated_event_batch_id);
+  q.null();  // initiated_event: nil on replay
+  q.i64(c.started_id);
+  q.text(c.started_workflow_id);
+  if (S.len(c.started_run_id) == 0 && S.ok(c.started_run_id))
+    q.uuid_const(3);  // emptyRunID
+  else
+    q.uuid_str(c.started_run_id);
+  q.null();  // started_event
+  q.uuid_val(c.create_request_lo, c.create_request_hi);
+  q.empty();  // event_data_encoding ""
+  q.text(c.domain_name);
+  q.text(c.workflow_type);
+  q.i32(c.parent_close_policy);
+}
+__device__ void cancel_cql(Out& o, const Strs& S, const cdr_cancel_info& c) {  // updateRequestCancelInfos :1530-1568
+  Cql q{o, S};
+  q.i64(c.initiated_id);  // request_cancel_map[ ? ]
+  q.i64(c.version);
+  q.i64(c.initiated_id);
+  q.i64(c.initiated_event_batch_id);
+  o.be32(36), o.uuid_text(c.cancel_request_lo, c.cancel_request_hi);  // cancel_request_id text
+}
+__device__ void signal_cql(Out& o, const Strs& S, const cdr_signal_info& g) {  // updateSignalInfos :1590-1631
+  Cql q{o, S};
+  q.i64(g.initiated_id);  // signal_map[ ? ]
+  q.i64(g.version);
+  q.i64(g.initiated_id);
+  q.i64(g.initiated_event_batch_id);
+  q.uuid_val(g.signal_request_lo, g.signal_request_hi);
+  q.text(g.signal_name);
+  q.blob_or_null(g.input);
+  q.blob_or_null(g.control);
+}
+
+// updateExecution (:625-890): the workflow_execution UDT, then replication_state (2DC:
+// templateUpdateWorkflowExecutionWithReplicationQuery) or next_event_id, version_histories,
+// version_histories_encoding (NDC), or next_event_id alone (local)
+__device__ void exec_cql(Out& o, const Strs& S, const cdr_exec_info& x, const cdr_exec_persist& ps, uint32_t builder,
+                         const cdr_repl_state* rs, const cdr_vh_item* vh, uint32_t n_vh, const cdr_reset_point* rp,
+                         uint32_t n_rp, const cdr_kv* sa, uint32_t n_sa, const uint32_t* cluster_names,
+                         uint32_t n_clusters) {
+  Cql q{o, S};
+  q.uuid_str(x.domain_id);
+  q.text(x.workflow_id);
+  q.uuid_str(x.run_id);
+  if (!S.ok(x.parent_domain_id)) o.err = o.err ? o.err : CDR_BLOB_E_HANDLE;
+  if (S.len(x.parent_domain_id) != 0) {
+    q.uuid_str(x.parent_domain_id);
+    q.text(x.parent_workflow_id);
+    q.uuid_str(x.parent_run_id);
+    q.i64(x.initiated_id);
+  } else {
+    q.uuid_const(1);  // emptyDomainID
+    q.empty();
+    q.uuid_const(3);  // emptyRunID
+    q.i64(-7);        // emptyInitiatedID
+  }
+  q.i64(x.completion_event_batch_id);
+  q.null();   // completion_event: not in the replay projection
+  q.empty();  // its encoding ""
+  q.text(x.task_list);
+  q.text(x.workflow_type);
+  q.i32(x.workflow_timeout);
+  q.i32(x.decision_timeout_value);
+  q.blob_or_null(ps.execution_context);
+  q.i32(x.state);
+  q.i32(x.close_status);
+  q.i64(x.last_first_event_id);
+  q.i64(x.last_event_task_id);
+  q.i64(x.next_event_id);
+  q.i64(x.last_processed_event);
+  q.ts(ps.start_time, ps.start_time == ZERO_TIME_NANOS);
+  q.ts(ps.last_updated_time, ps.last_updated_time == ZERO_TIME_NANOS);
+  q.uuid_str(x.create_request_id);
+  q.i32((int32_t)x.signal_count);
+  q.i64(ps.history_size);
+  q.i64(x.decision_version);
+  q.i64(x.decision_schedule_id);
+  q.i64(x.decision_started_id);
+  q.text(x.decision_request_id);
+  q.i32(x.decision_timeout);
+  q.i64(x.decision_attempt);
+  q.i64(x.decision_started_ts);
+  q.i64(x.decision_scheduled_ts);
+  q.i64(x.decision_original_scheduled_ts);
+  q.boo((x.flags & CDR_XI_CANCEL_REQUESTED) != 0);
+  q.empty();  // cancel_request_id: replay never sets it
+  q.text(ps.sticky_task_list);
+  q.i32((int32_t)ps.sticky_s2s_timeout);
+  q.text(ps.client_library_version);
+  q.text(ps.client_feature_version);
+  q.text(ps.client_impl);
+  const bool has_rp = (x.flags & CDR_XI_HAS_RESET_POINTS) != 0;
+  Out cnt{nullptr, 0, 0, 0, 0, 0};
+  reset_points(cnt, S, rp, n_rp, has_rp);
+  o.be32((uint32_t)cnt.pos);
+  reset_points(o, S, rp, n_rp, has_rp);
+  q.lit("thriftrw", 8);
+  q.i32((int32_t)x.attempt);
+  q.boo((x.flags & CDR_XI_HAS_RETRY) != 0);
+  q.i32(x.initial_interval);
+  q.dbl(x.backoff_coefficient);
+  q.i32(x.maximum_interval);
+  q.ts(x.expiration_time, !(x.flags & CDR_XI_HAS_EXPIRATION));
+  q.i32(x.maximum_attempts);
+  q.list_text(x.nonretriable);
+  q.i32(-1);  // defaultEventStoreVersionValue
+  cnt.pos = 0;
+  branch_token(cnt, S, x);
+  const uint64_t token_len = cnt.pos;
+  if (x.flags & CDR_XI_HAS_BRANCH) {
+    o.be32((uint32_t)token_len);
+    branch_token(o, S, x);
+  } else {
+    q.null();
+  }
+  q.text(x.cron_schedule);
+  q.i32(x.expiration_seconds);
+  if (x.flags & CDR_XI_HAS_SEARCH_ATTR) {  // map<text, blob>
+    uint64_t n = 4;
+    for (uint32_t i = 0; i < n_sa; i++) n += 8 + S.len(sa[i].key) + S.len(sa[i].value);
+    o.be32((uint32_t)n), o.be32(n_sa);
+    for (uint32_t i = 0; i < n_sa; i++) {
+      const cdr_kv kv = sa[i];
+      if (!S.ok(kv.key) || !S.ok(kv.value)) o.err = o.err ? o.err : CDR_BLOB_E_HANDLE;
+      o.be32((uint32_t)S.len(kv.key)), o.raw(S.at(kv.key), S.len(kv.key));
+      o.be32((uint32_t)S.len(kv.value)), o.raw(S.at(kv.value), S.len(kv.value));
+    }
+  } else {
+    q.null();
+  }
+  uint64_t m0 = 0, m1 = 0;  // memo: the thrift map body minus its key / value type bytes
+  if ((x.flags & CDR_XI_HAS_MEMO) && x.memo && memo_fields(S, x.memo, m0, m1, o.err)) {
+    o.be32((uint32_t)(m1 - m0 - 2));
+    o.raw(S.at(x.memo) + m0 + 2, m1 - m0 - 2);
+  } else {
+    q.null();
+  }
+  if (builder == CDR_BUILDER_2DC) {  // replication_state
+    q.i64(rs->current_version);
+    q.i64(rs->start_version);
+    q.i64(rs->last_write_version);
+    q.i64(rs->last_write_event_id);
+    uint32_t cnt_c = 0;
+    uint64_t n = 4;
+    for (uint32_t i = 0; i < n_clusters && i < CDR_MAX_CLUSTERS; i++)
+      if ((rs->lri_mask >> i) & 1u) cnt_c++, n += 4 + S.len(cluster_names[i]) + 4 + 24;
+    o.be32((uint32_t)n), o.be32(cnt_c);
+    for (uint32_t i = 0; i < n_clusters && i < CDR_MAX_CLUSTERS; i++) {
+      if (!((rs->lri_mask >> i) & 1u)) continue;
+      q.text(cluster_names[i]);
+      o.be32(24);  // frozen<replication_info>{version, last_event_id}
+      q.i64(rs->lri_version[i]);
+      q.i64(rs->lri_last_event_id[i]);
+    }
+    q.i64(x.next_event_id);
+  } else if (builder == CDR_BUILDER_NDC) {
+    q.i64(x.next_event_id);
+    const uint64_t tl = (x.flags & CDR_XI_VH_BRANCH) ? token_len : 0;
+    cnt.pos = 0;
+    version_histories(cnt, S, x, vh, n_vh, tl);
+    o.be32((uint32_t)cnt.pos);
+    version_histories(o, S, x, vh, n_vh, tl);
+    q.lit("thriftrw", 8);
+  } else {
+    q.i64(x.next_event_id);
+  }
+}
+
 struct BlobArgs {
   int table;
+  int cql;  // 1: the Cassandra form (cdr_encode_cql_async)
   Strs S;
   const cdr_exec_persist* persist;
   const uint32_t* cluster_names;
@@ -408,6 +706,20 @@ __device__ void emit_row(const BlobArgs& A, const cdr_dev_batch& B, const cdr_ou
                          Out& o) {
   const cdr_wf_result& r = O.result[w];
   const cdr_wf_caps& c = B.caps[w];
+  if (A.cql) {
+    switch (A.table) {
+      case 0: activity_cql(o, A.S, O.act[row]); break;
+      case 1: timer_cql(o, A.S, O.timer[row]); break;
+      case 2: child_cql(o, A.S, O.child[row]); break;
+      case 3: cancel_cql(o, A.S, O.cancel[row]); break;
+      case 4: signal_cql(o, A.S, O.signal[row]); break;
+      default:
+        exec_cql(o, A.S, O.exec[w], A.persist[w], B.wfs[w].builder, O.repl + w, O.vh + c.vh_off, r.n_vh,
+                 O.rp + c.rp_off, r.n_reset_points, O.sa + c.sa_off, r.n_search_attr, A.cluster_names,
+                 B.cluster.n_clusters);
+    }
+    return;
+  }
   switch (A.table) {
     case 0: activity_row(o, A.S, O.act[row]); break;
     case 2: child_row(o, A.S, O.child[row]); break;
@@ -429,7 +741,9 @@ __global__ __launch_bounds__(256) void k_blobs(BlobArgs A, cdr_dev_batch B, cdr_
   uint64_t off0 = w;
   uint32_t cap = 1, n = ok ? 1u : 0u;
   if (A.table == 0) off0 = c.act_off, cap = c.act_cap, n = ok ? r.n_activity : 0u;
+  if (A.table == 1) off0 = c.timer_off, cap = c.timer_cap, n = ok ? r.n_timer : 0u;
   if (A.table == 2) off0 = c.child_off, cap = c.child_cap, n = ok ? r.n_child : 0u;
+  if (A.table == 3) off0 = c.cancel_off, cap = c.cancel_cap, n = ok ? r.n_cancel : 0u;
   if (A.table == 4) off0 = c.signal_off, cap = c.signal_cap, n = ok ? r.n_signal : 0u;
   for (uint32_t j = 0; j < cap; j++) {
     const uint64_t row = off0 + j;
@@ -457,20 +771,41 @@ __global__ __launch_bounds__(256) void k_blobs(BlobArgs A, cdr_dev_batch B, cdr_
     }                                                                                                 \
   } while (0)
 
+static int encode_var(int cql, cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out,
+                      const cdr_strtab* strs, const cdr_exec_persist* persist, const uint32_t* cluster_names,
+                      uint64_t n_rows, uint64_t* row_off, uint8_t* blobs, int32_t* row_status, void* stream);
+
 extern "C" int cdr_encode_blobs_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out,
                                       const cdr_strtab* strs, const cdr_exec_persist* persist,
                                       const uint32_t* cluster_names, uint64_t n_rows, uint64_t* row_off,
                                       uint8_t* blobs, int32_t* row_status, void* stream) {
-  if (!ctx || !in || !out || !strs || !row_off || !out->result) return CDR_API_EINVAL;
   if (table != 0 && table != 2 && table != 4 && table != 5) return CDR_API_EINVAL;
-  if ((table == 0 && !out->act) || (table == 2 && !out->child) || (table == 4 && !out->signal)) return CDR_API_EINVAL;
+  return encode_var(0, ctx, table, in, out, strs, persist, cluster_names, n_rows, row_off, blobs, row_status, stream);
+}
+
+extern "C" int cdr_encode_cql_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out,
+                                    const cdr_strtab* strs, const cdr_exec_persist* persist,
+                                    const uint32_t* cluster_names, uint64_t n_rows, uint64_t* row_off,
+                                    uint8_t* values, int32_t* row_status, void* stream) {
+  if (table < 0 || table > 5) return CDR_API_EINVAL;
+  return encode_var(1, ctx, table, in, out, strs, persist, cluster_names, n_rows, row_off, values, row_status, stream);
+}
+
+static int encode_var(int cql, cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out,
+                      const cdr_strtab* strs, const cdr_exec_persist* persist, const uint32_t* cluster_names,
+                      uint64_t n_rows, uint64_t* row_off, uint8_t* blobs, int32_t* row_status, void* stream) {
+  if (!ctx || !in || !out || !strs || !row_off || !out->result) return CDR_API_EINVAL;
+  if ((table == 0 && !out->act) || (table == 1 && !out->timer) || (table == 2 && !out->child) ||
+      (table == 3 && !out->cancel) || (table == 4 && !out->signal))
+    return CDR_API_EINVAL;
   if (table == 5 && (!out->exec || !out->repl || !persist || !out->vh || !out->rp || !out->sa || n_rows < in->n_wfs ||
                      (in->cluster.n_clusters > 0 && !cluster_names)))
     return CDR_API_EINVAL;
   if (strs->n == 0 || !strs->bytes || !strs->off) return CDR_API_EINVAL;
   HIPCHK(hipSetDevice(cdr_ctx_device(ctx)));
   hipStream_t st = (hipStream_t)stream;
-  BlobArgs A{table, Strs{strs->bytes, strs->off, strs->n}, persist, cluster_names, nullptr, row_off, blobs, row_status};
+  BlobArgs A{table, cql, Strs{strs->bytes, strs->off, strs->n}, persist, cluster_names, nullptr, row_off, blobs,
+             row_status};
   const dim3 grid((in->n_wfs + 255) / 256), blk(256);
   if (!blobs) {  // size pass + exclusive scan into row_off[0 .. n_rows]
     uint64_t* sizes = (uint64_t*)cdr_ws_get(ctx, WS_ENC_SIZES, (n_rows + 1) * sizeof(uint64_t));

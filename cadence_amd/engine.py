@@ -474,13 +474,16 @@ class Engine:
                 hip.hipFree(p)
 
     def encode_blobs(self, batch: Batch, out: Outputs, table: str, strings: list, persist=None,
-                     cluster_names=None):
+                     cluster_names=None, form: str = "sql"):
         """Variable-size sqlblobs row blobs through cdr_encode_blobs_async (size pass +
         scan, then the write pass) for table "act", "child", "signal" or "exec", with
         `strings[h]` (bytes) the string table: ({row: blob}, {row: CDR_BLOB_* status}) for
         the rows of OK entries (exec: row = entry).  `persist` is a cdr_exec_persist array
-        and `cluster_names` a list of handles (table "exec")."""
-        tid = {"act": 0, "child": 2, "signal": 4, "exec": 5}[table]
+        and `cluster_names` a list of handles (table "exec").  form="cql": the Cassandra
+        form instead (cdr_encode_cql_async: each row's CQL bound values), tables "act",
+        "timer", "child", "cancel", "signal", "exec"."""
+        tid = {"act": 0, "timer": 1, "child": 2, "cancel": 3, "signal": 4, "exec": 5}[table]
+        fn = "cdr_encode_cql_async" if form == "cql" else "cdr_encode_blobs_async"
         hip = _hip()
         pl = out.plan
         ptrs = []
@@ -521,7 +524,7 @@ class Engine:
             o.result = up(out.result)
             for t in ("exec", "repl"):
                 setattr(o, t, up(getattr(out, t)))
-            for t in ("act", "child", "signal", "vh", "rp", "sa"):
+            for t in ("act", "timer", "child", "cancel", "signal", "vh", "rp", "sa"):
                 setattr(o, t, up(out.tables[t]))
             n_rows = batch.n_wfs if table == "exec" else max(1, getattr(pl.totals, table))
             pp = up(persist) if persist is not None else None
@@ -529,21 +532,22 @@ class Engine:
             row_off = dalloc(8 * (n_rows + 1))
             status = dalloc(4 * n_rows)
             L = abi.lib()
-            rc = L.cdr_encode_blobs_async(self.ctx, tid, C.byref(db), C.byref(o), C.byref(st), pp, cn, n_rows,
-                                          row_off, None, status, None)
+            rc = getattr(L, fn)(self.ctx, tid, C.byref(db), C.byref(o), C.byref(st), pp, cn, n_rows,
+                                row_off, None, status, None)
             if rc:
-                raise RuntimeError(f"cdr_encode_blobs_async (sizes) rc={rc}")
+                raise RuntimeError(f"{fn} (sizes) rc={rc}")
             offs = np.frombuffer(down(row_off, 8 * (n_rows + 1)), np.uint64)
             total = int(offs[-1])
             blobs = dalloc(total)
-            rc = L.cdr_encode_blobs_async(self.ctx, tid, C.byref(db), C.byref(o), C.byref(st), pp, cn, n_rows,
-                                          row_off, blobs, status, None)
+            rc = getattr(L, fn)(self.ctx, tid, C.byref(db), C.byref(o), C.byref(st), pp, cn, n_rows,
+                                row_off, blobs, status, None)
             if rc:
-                raise RuntimeError(f"cdr_encode_blobs_async (write) rc={rc}")
+                raise RuntimeError(f"{fn} (write) rc={rc}")
             raw = down(blobs, total)
             stat = np.frombuffer(down(status, 4 * n_rows), np.int32)
             got, codes = {}, {}
-            cnt = {"act": "n_activity", "child": "n_child", "signal": "n_signal"}.get(table)
+            cnt = {"act": "n_activity", "timer": "n_timer", "child": "n_child", "cancel": "n_cancel",
+                   "signal": "n_signal"}.get(table)
             for w in range(batch.n_wfs):
                 if out.result[w].code != abi.OK:
                     continue
@@ -577,9 +581,10 @@ def _bytes(x) -> bytes:
     return bytes(memoryview(x).cast("B"))
 
 
-def compare(batch: Batch, a: Outputs, b: Outputs, limit: int = 10):
+def compare(batch: Batch, a: Outputs, b: Outputs, limit: int = 10, last_decision: bool = True):
     """Field-by-field comparison of two output sets (result of every workflow; the
-    persisted state of every OK workflow).  Returns a list of mismatch strings."""
+    persisted state of every OK workflow; applyEvents' lastDecision unless
+    last_decision=False).  Returns a list of mismatch strings."""
     bad = []
     for w in range(batch.n_wfs):
         ra, rb = a.result[w], b.result[w]
@@ -595,7 +600,7 @@ def compare(batch: Batch, a: Outputs, b: Outputs, limit: int = 10):
             if batch.wfs[w].builder == abi.BUILDER_2DC and _bytes(a.repl[w]) != _bytes(b.repl[w]):
                 bad.append(f"wf {w}: replication state differs")
             la, lb = a.last_decision[w], b.last_decision[w]
-            if _bytes(la) != _bytes(lb):
+            if last_decision and _bytes(la) != _bytes(lb):
                 bad.append(f"wf {w}: lastDecision differs in "
                            f"{[f for f, _ in abi.CdrLastDecision._fields_ if getattr(la, f) != getattr(lb, f)]}")
             for t in TABLES:

@@ -571,6 +571,36 @@ int cdr_encode_blobs_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, con
                            const cdr_strtab* strs, const cdr_exec_persist* persist, const uint32_t* cluster_names,
                            uint64_t n_rows, uint64_t* row_off, uint8_t* blobs, int32_t* row_status, void* stream);
 
+/* The Cassandra persistence's form of the same rows (common/persistence/cassandra/
+ * cassandraPersistenceUtil.go; CQL templates cassandraPersistence.go:114-306,439-520): per row
+ * the values the statement that writes it binds, in order, each a CQL native-protocol [bytes]
+ * value — big-endian int32 length (-1 = null), then the value as gocql (v0.0.0-20171220143535-
+ * 56a164ee9f31, go.mod:22) marshals it for the column's CQL type: bigint / int big-endian,
+ * boolean one byte, double IEEE big-endian, timestamp milliseconds since the epoch (the zero
+ * time.Time: zero bytes), text / blob the bytes (a nil []byte: null), uuid the 16 bytes gocql's
+ * ParseUUID reads from the string (CDR_BLOB_E_UUID where it fails), list<text> / map<text, blob>
+ * an int32 count and the [bytes] elements, a UDT its fields' [bytes] in declaration order.
+ *   table 0  activity_map[schedule_id] = activity_info (updateActivityInfos :1264-1337): the
+ *            key, then the UDT's 33 fields
+ *   table 1  timer_map[timer_id] = timer_info (updateTimerInfos :1384-1422)
+ *   table 2  child_executions_map[initiated_id] = child_execution_info (:1444-1503; "" started
+ *            run -> emptyRunID)
+ *   table 3  request_cancel_map[initiated_id] = request_cancel_info (:1530-1568)
+ *   table 4  signal_map[initiated_id] = signal_info (:1590-1631)
+ *   table 5  the execution row's SET values of updateExecution (:625-890): the
+ *            workflow_execution UDT's 58 fields (no parent -> emptyDomainID / "" / emptyRunID /
+ *            emptyInitiatedID), then the 2DC replication_state's 5 (last_replication_info
+ *            a map<text, frozen<replication_info>> keyed by cluster_names) and next_event_id,
+ *            or next_event_id, version_histories and its encoding (NDC), or next_event_id
+ *            (local); what the projection does not carry comes from `persist`, as for table 5
+ *            of cdr_encode_blobs_async
+ * The statements' WHERE / IF values (shard, row type, the execution's keys, the condition) are
+ * the caller's.  Map iteration order is Go's random order in the reference; maps are written
+ * in input / cluster-index order.  Two calls (sizes, then values) as cdr_encode_blobs_async. */
+int cdr_encode_cql_async(cdr_ctx* ctx, int table, const cdr_dev_batch* in, const cdr_out* out,
+                         const cdr_strtab* strs, const cdr_exec_persist* persist, const uint32_t* cluster_names,
+                         uint64_t n_rows, uint64_t* row_off, uint8_t* values, int32_t* row_status, void* stream);
+
 /* Stream compaction of the per-workflow pending tables into dense tables
  * (device pointers): for each table, rows [caps.off, caps.off + result.n) of every
  * workflow are copied to dense[row_base[w] ...]; row_base is an exclusive scan of
