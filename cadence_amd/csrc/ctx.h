@@ -76,11 +76,11 @@ struct cdr_ctx {
   static constexpr int N_SIDE = 7;  // + the PAR slices' stream
   hipStream_t side[N_SIDE] = {};
   hipEvent_t fork = nullptr, join[N_SIDE] = {};
-  // class i launches on side[side_of[i]]: every class on its own stream when the runtime
-  // has the hardware queues for it (GPU_MAX_HW_QUEUES >= 8), else three streams — the PAR
-  // slices; the few-and-long classes (wave, 12-activity, general); the bulk classes
-  // (small-table, fast, 6-activity) — so that with HIP's default 4 queues the caller's
-  // stream and the three sides each get a queue of their own
+  // class i launches on side[side_of[i]] (N_SIDE: on the caller's stream): every class on
+  // its own stream when the runtime has the hardware queues for it (GPU_MAX_HW_QUEUES >= 8),
+  // else three side streams and the caller's — the PAR slices; the wave and 12-activity
+  // classes; the small-table class; the general, fast and 6-activity classes on the
+  // caller's stream — so that with HIP's default 4 queues each stream has a queue of its own
   int side_of[N_SIDE] = {0, 1, 2, 3, 4, 5, 6};
   int concurrent = 1;
   // grow-only device workspace of the host-buffer calls

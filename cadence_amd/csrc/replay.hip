@@ -1828,17 +1828,22 @@ cdr_ctx* cdr_create(int device, const cdr_opts* opts) {
   int n_side = hwq >= cdr_ctx::N_SIDE + 1 ? cdr_ctx::N_SIDE : 3;
   if (const char* e = std::getenv("CDR_SIDE_STREAMS")) n_side = std::atoi(e) == 3 ? 3 : cdr_ctx::N_SIDE;
   if (n_side == 3) {
-    // the wave class alone (its longest histories are a tail nothing should queue
-    // behind) | every lane class | PAR (CDR_SIDE_GROUPS=<7 digits> overrides: class i's stream)
-    int grouped[cdr_ctx::N_SIDE] = {0, 5, 5, 5, 5, 5, 6};
+    // four streams, one per queue: the wave and 12-activity classes (few slices, long
+    // histories) | the small-table class | the general, fast and 6-activity classes on the
+    // caller's stream | PAR.  Measured at 4 queues (tools/gpu_groups.sh, 1M workflows,
+    // ms/step C3 / C4 / C5): 5.32 / 14.0 / 8.72 against 6.40 / 19.0 / 11.7 with every lane
+    // class on one side stream and 5.98 / 16.3 / 10.1 with a stream per class
+    // (CDR_SIDE_GROUPS=<7 digits> overrides: class i's stream, 7 = the caller's stream)
+    int grouped[cdr_ctx::N_SIDE] = {0, 0, 7, 5, 7, 7, 6};
     if (const char* e = std::getenv("CDR_SIDE_GROUPS"))
       if (std::strlen(e) == (size_t)cdr_ctx::N_SIDE)
         for (int i = 0; i < cdr_ctx::N_SIDE; i++)
-          if (e[i] >= '0' && e[i] < '0' + cdr_ctx::N_SIDE) grouped[i] = e[i] - '0';
+          if (e[i] >= '0' && e[i] <= '0' + cdr_ctx::N_SIDE) grouped[i] = e[i] - '0';
     for (int i = 0; i < cdr_ctx::N_SIDE; i++) c->side_of[i] = grouped[i];
   }
   bool need[cdr_ctx::N_SIDE] = {};  // only the streams some class launches on (each takes a queue)
-  for (int i = 0; i < cdr_ctx::N_SIDE; i++) need[c->side_of[i]] = true;
+  for (int i = 0; i < cdr_ctx::N_SIDE; i++)
+    if (c->side_of[i] < cdr_ctx::N_SIDE) need[c->side_of[i]] = true;
   for (int i = 0; i < cdr_ctx::N_SIDE; i++) {
     if (!need[i]) continue;
     if (n_cu > 0) {
@@ -2002,8 +2007,8 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   bool used[cdr_ctx::N_SIDE] = {};  // side stream j carries a forked class
   bool any_fork = false;
   for (int i = 0; i < cdr_ctx::N_SIDE; i++) {
-    any_fork |= (fk[i] = c->concurrent && on[i] && kinds > 1);
-    used[c->side_of[i]] |= fk[i];
+    any_fork |= (fk[i] = c->concurrent && on[i] && kinds > 1 && c->side_of[i] < cdr_ctx::N_SIDE);
+    if (fk[i]) used[c->side_of[i]] = true;
   }
   if (any_fork) HIPCHK(hipEventRecord(c->fork, st));
   for (int j = 0; j < cdr_ctx::N_SIDE; j++)
