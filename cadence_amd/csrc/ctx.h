@@ -36,6 +36,7 @@ enum cdr_ws_slot {
   WS_ENC_SIZES, WS_ENC_TMP,
   // cdr_ndc_replicate_async (ndc.hip)
   WS_NDC_SKIP_RB, WS_NDC_SKIP_AP, WS_NDC_INMEM, WS_NDC_SRC, WS_NDC_CARRY,
+  WS_RETRY,  // the class kernels' retry lists: 8 counters, then a list of n_slices per class
   WS_NUM
 };
 

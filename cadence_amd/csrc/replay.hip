@@ -493,6 +493,10 @@ struct cdr_launch {
   uint32_t reg;     // CDR_SLICE_REG slices go to k_replay_reg (else here)
   uint32_t s0;      // slice of block 0 (the launch covers its kernel class's slice range)
   uint32_t retry;   // k_replay_reg: only the entries k_replay_cls left CLS_RETRY
+  // k_replay_cls lists each slice where it left an entry CLS_RETRY (rlist[*rcount++]); the
+  // retry pass of k_replay_reg walks that list (null: every slice of its range)
+  uint32_t* rlist;
+  uint32_t* rcount;
 };
 // result code k_replay_cls leaves on an entry it hands to k_replay_reg (never returned)
 #define CLS_RETRY 0x7FFF
@@ -1962,6 +1966,9 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
     x.retry = 1u;
     return x;
   };
+  // the retry passes walk k_replay_cls's lists with this many workgroups at most
+  constexpr uint32_t RETRY_WGS = 256;
+  auto retry_grid = [&](dim3 g) { return dim3(g.x < RETRY_WGS ? g.x : RETRY_WGS); };
   const bool wave = in->n_wave_slices > 0;
   const bool general = (fast ? in->n_fast_slices : 0u) +
                            (reg ? in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices + in->n_par_slices : 0u) +
@@ -1969,7 +1976,21 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
                        in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
-  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u, 0u};
+  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u, 0u, 0u, nullptr, nullptr};
+  // retry lists (k_replay_cls -> k_replay_reg): counters zeroed on the launch stream
+  uint32_t* rws = nullptr;
+  if (cls && cls_fb) {
+    rws = (uint32_t*)cdr_ws_get(c, WS_RETRY, (16ull + (uint64_t)cdr_ctx::N_SIDE * blocks) * 4ull);
+    if (!rws) return CDR_API_ENOMEM;
+    HIPCHK(hipMemsetAsync(rws, 0, 16 * 4, st));
+  }
+  auto with_list = [&](cdr_launch x, int cls_id) {
+    if (rws) {
+      x.rcount = rws + cls_id;
+      x.rlist = rws + 16 + (uint64_t)cls_id * blocks;
+    }
+    return x;
+  };
   // each kernel over its class's slice range (cdr_plan_class_ranges), or every slice
   bool ranged = false;
   for (int c = 0; c < 6; c++) ranged |= in->class_hi[c] > 0;
@@ -2028,11 +2049,12 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       if (cls) {
         typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, true> LC;
         hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_CLS2, true>),
-                           dim3(npar), dim3(4 * CDR_SLICE_WIDTH), LC::bytes, sx(6), Lp);
+                           dim3(npar), dim3(4 * CDR_SLICE_WIDTH), LC::bytes, sx(6), with_list(Lp, 6));
       }
       if (!cls || cls_fb)
-        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR>), dim3(npar),
-                           dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6), cls ? retry_of(Lp) : Lp);
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR>),
+                           cls ? retry_grid(dim3(npar)) : dim3(npar), dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6),
+                           cls ? retry_of(with_list(Lp, 6)) : Lp);
     }
         break;
       case 0:
@@ -2044,11 +2066,11 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       if (cls) {
         typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LC;
         hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_CLS2>), gr2,
-                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(1), Lr2);
+                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(1), with_list(Lr2, 1));
       }
       if (!cls || cls_fb)
-        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), gr2,
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), cls ? retry_of(Lr2) : Lr2);
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), cls ? retry_grid(gr2) : gr2,
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), cls ? retry_of(with_list(Lr2, 1)) : Lr2);
     }
         break;
       case 2:
@@ -2071,11 +2093,11 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       if (cls) {
         typedef ClsLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LC;
         hipLaunchKernelGGL((k_replay_cls<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_CLS0>), gr0,
-                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(3), Lr0);
+                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(3), with_list(Lr0, 3));
       }
       if (!cls || cls_fb)
-        hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), gr0,
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), cls ? retry_of(Lr0) : Lr0);
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), cls ? retry_grid(gr0) : gr0,
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), cls ? retry_of(with_list(Lr0, 3)) : Lr0);
     }
         break;
       case 4:
@@ -2087,11 +2109,11 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       if (cls) {
         typedef ClsLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LC;
         hipLaunchKernelGGL((k_replay_cls<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_CLS>), gr1,
-                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(5), Lr1);
+                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(5), with_list(Lr1, 5));
       }
       if (!cls || cls_fb)
-        hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), gr1,
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), cls ? retry_of(Lr1) : Lr1);
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), cls ? retry_grid(gr1) : gr1,
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), cls ? retry_of(with_list(Lr1, 5)) : Lr1);
     }
         break;
     }
