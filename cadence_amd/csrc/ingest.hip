@@ -61,6 +61,11 @@ __device__ __forceinline__ uint64_t slot0(uint64_t h, uint64_t mask) { return cd
 __device__ void tab_insert(const STab& T, uint64_t h, uint64_t ref, uint32_t len, uint32_t handle) {
   uint64_t i = slot0(h, T.mask);
   for (uint64_t probe = 0; probe <= T.mask; probe++, i = (i + 1) & T.mask) {
+    // most string fields repeat a string already in the table (task lists, types, ids):
+    // a plain load finds those without an atomic on a slot every lane of the chip hits
+    const unsigned long long seen = __hip_atomic_load(&T.key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seen == (unsigned long long)h) return;
+    if (seen != 0ull) continue;
     const unsigned long long k = atomicCAS(&T.key[i], 0ull, (unsigned long long)h);
     if (k == 0ull) {  // this lane owns the slot
       T.ref[i] = ref;
@@ -84,15 +89,25 @@ __device__ uint32_t tab_lookup(const STab& T, uint64_t h) {
 }
 
 // ---------------------------------------------------------------- reader
-// Bytes come through a 16-byte aligned window held in registers (one global_load_dwordx4
-// per 16 bytes instead of a load per byte); the last 16 bytes of the buffer, which an
-// aligned window could overrun, are read byte by byte.
+// Each wavefront first copies its 64 consecutive blobs — one contiguous byte range — into
+// LDS with 16-byte loads (64 lanes x 16 B per instruction, coalesced), so the parse reads
+// bytes from LDS; a wave whose range exceeds its share of LDS (CDR_INGEST_STAGE) reads
+// through a 16-byte aligned window held in registers (one global_load_dwordx4 per 16
+// bytes instead of a load per byte), as does any byte outside the staged range; the last
+// 16 bytes of the buffer, which an aligned window could overrun, are read byte by byte.
+#ifndef CDR_INGEST_STAGE
+#define CDR_INGEST_STAGE 12288 /* bytes of blob data staged in LDS per wavefront */
+#endif
+#define LDS3 __attribute__((address_space(3)))
+extern __shared__ uint4 ing_lds[];
 struct Rd {
   const uint8_t* b;  // blob_bytes
   uint64_t pos, end;
   uint64_t total;    // bytes in blob_bytes
   uint64_t wb;       // window address (16-aligned), ~0 = empty
   uint64_t w0, w1;
+  const LDS3 uint8_t* sb;  // the wave's staged bytes: addresses [s_lo, s_lo + s_n)
+  uint64_t s_lo, s_n;
   int32_t err;
   __device__ void init(const uint8_t* base, uint64_t p, uint64_t e, uint64_t t) {
     b = base;
@@ -100,11 +115,14 @@ struct Rd {
     end = e;
     total = t;
     wb = ~0ull;
+    sb = nullptr;
+    s_lo = s_n = 0;
     err = CDR_DEC_OK;
   }
   __device__ uint32_t at(uint64_t p) {
     // the window is aligned in the address space (the buffer itself need not be)
     const uint64_t addr = (uint64_t)(uintptr_t)(b + p), a = addr & ~15ull;
+    if (addr - s_lo < s_n) return sb[addr - s_lo];
     if (a != wb) {
       const uint64_t lo = (uint64_t)(uintptr_t)b;
       if (a < lo || a + 16 > lo + total) return b[p];
@@ -726,13 +744,57 @@ struct Blob {
   }
 };
 
+// the wave's blobs [wb0, wb0 + 64) into its LDS share when their bytes fit: returns the
+// staged address range (lo, n; n = 0: nothing staged)
+__device__ void stage_blobs(const Ctx& C, uint32_t n_blobs, uint32_t wb0, uint32_t lane, LDS3 uint4* dst,
+                            uint64_t* lo_out, uint64_t* n_out) {
+  *lo_out = *n_out = 0;
+  if (wb0 >= n_blobs) return;
+  const uint32_t wb1 = wb0 + 64 < n_blobs ? wb0 + 64 : n_blobs;
+  const uint64_t base = (uint64_t)(uintptr_t)C.bytes;
+  const uint64_t A = base + C.blob_off[wb0], E = base + C.blob_off[wb1];
+  const uint64_t A16 = A & ~15ull;
+  if (E <= A || E - A16 > CDR_INGEST_STAGE) return;
+  const uint64_t lim = base + C.total;
+  for (uint64_t i = (uint64_t)lane * 16u; A16 + i < E; i += 64u * 16u) {
+    const uint64_t a = A16 + i;
+    uint4 v;
+    if (a >= base && a + 16 <= lim) {
+      v = *reinterpret_cast<const uint4*>((uintptr_t)a);
+    } else {  // the buffer's first / last partial 16 bytes
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t j = 0; j < 16; j++)
+        if (a + j >= base && a + j < lim) w[j >> 2] |= (uint32_t)C.bytes[a + j - base] << (8 * (j & 3));
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    LDS3 uint32_t* d4 = (LDS3 uint32_t*)dst + (i >> 2);
+    d4[0] = v.x;
+    d4[1] = v.y;
+    d4[2] = v.z;
+    d4[3] = v.w;
+  }
+  *lo_out = A16;
+  *n_out = E - A16;
+}
+
 template <int P>
 __global__ __launch_bounds__(256) void k_blob(Ctx C, uint32_t n_blobs) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  LDS3 uint4* stage = (LDS3 uint4*)ing_lds + (uint64_t)wv * (CDR_INGEST_STAGE / 16);
+  uint64_t s_lo, s_n;
+  stage_blobs(C, n_blobs, b - lane, lane, stage, &s_lo, &s_n);
+  // the wave's LDS writes complete before any of its lanes reads them (one wave: in order)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   uint64_t n_str = 0;
   uint32_t bad = 0;
   if (b < n_blobs && (P == COUNT || C.status[b] == CDR_DEC_OK)) {  // a failed blob contributes nothing
     Blob<P> x(C, b);
+    x.r.sb = (const LDS3 uint8_t*)stage;
+    x.r.s_lo = s_lo;
+    x.r.s_n = s_n;
     x.run();
     if (P == COUNT) {
       C.counts[4ull * b] = x.r.ok() ? x.n_ev : 0u;
@@ -869,7 +931,7 @@ extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_inge
   uint64_t* tot2 = reinterpret_cast<uint64_t*>(misc) + 2;
   HIPCHK(hipMemsetAsync(misc, 0, 64, st));
   C.totals = reinterpret_cast<unsigned long long*>(tot2);
-  if (nb) hipLaunchKernelGGL(k_blob<COUNT>, grid(nb), blk, 0, st, C, nb);
+  if (nb) hipLaunchKernelGGL(k_blob<COUNT>, grid(nb), blk, 4 * CDR_INGEST_STAGE, st, C, nb);
   HIPCHK(hipGetLastError());
   // string fields -> table capacity (2x, power of two)
   uint64_t htot[2] = {0, 0};
@@ -889,7 +951,7 @@ extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_inge
   C.T = T;
   // ---- pass 2: seeds, then every string of the blobs; rank the new ones by hash
   hipLaunchKernelGGL(k_seed, grid(in->n_seeds), blk, 0, st, T, in->seed_bytes, in->seed_off, in->n_seeds);
-  if (nb) hipLaunchKernelGGL(k_blob<INTERN>, grid(nb), blk, 0, st, C, nb);
+  if (nb) hipLaunchKernelGGL(k_blob<INTERN>, grid(nb), blk, 4 * CDR_INGEST_STAGE, st, C, nb);
   HIPCHK(hipGetLastError());
   unsigned long long *k1, *k2;
   uint64_t *i1, *i2;
@@ -967,7 +1029,7 @@ extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_inge
   C.events = out->events;
   C.kvs = out->kvs;
   C.rps = out->rps;
-  if (nb) hipLaunchKernelGGL(k_blob<FILL>, grid(nb), blk, 0, st, C, nb);
+  if (nb) hipLaunchKernelGGL(k_blob<FILL>, grid(nb), blk, 4 * CDR_INGEST_STAGE, st, C, nb);
   HIPCHK(hipGetLastError());
   out->ev_off = ev_off;
   out->blob_status = status;
