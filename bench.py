@@ -321,6 +321,98 @@ def parity_check(db, ctx, stream, config, mine, seed):
                       "oracle/digest_ref.cpp), CopyToPersistence mutableStateBuilder.go:257-270"}
 
 
+def ndc_forks_line(args):
+    """configs[4]'s conflict-resolution path at scale: the forked config-5 population
+    (cadence_amd.ndc.synth_forked: a base branch and two fork rounds per workflow,
+    nDC_integration_test.go:224-308) replicated device-resident (cdr_ndc_replicate_async,
+    nDCHistoryReplicator.go:330-398 -> nDCConflictResolver.go:117-184 -> nDCStateRebuilder.go:
+    92-160).  A step = the base branch replayed into the state buffer + both rounds (branch,
+    rebuild replay + refreshTasks + verify, apply onto the rebuilt state in memory or the loaded
+    one, VersionHistories sync).  value = events replayed per second (base + rebuilt + applied
+    events); parity: the final state, the VersionHistories and each round's decisions against
+    oracle.ndc_replicate, entry by entry."""
+    import torch
+    from cadence_amd import engine, ndc
+    torch.cuda.set_device(0)
+    eng = engine.Engine(0)
+    n = args.wfs
+    t0 = time.perf_counter()
+    base, rebuild, forks = ndc.synth_forked(5, n, args.seed)
+    rep = ndc.DeviceReplicator(eng, base, rebuild, forks)
+    setup_s = time.perf_counter() - t0
+    log(f"NDC forks: {n} workflows, host synth + plan + upload {setup_s:.1f}s")
+    state, vhs, pool, decs, rounds = rep.run()  # warm-up (and the decisions the events count from)
+    ev_base = rep.events[0]
+    lens_rb = np.array([rebuild.wfs[w].ev_len for w in range(n)], np.int64)
+    ev_rounds = []
+    for k, (fb, _, _) in enumerate(forks):
+        act = np.array([decs[k][w].action for w in range(n)], np.int32)
+        lens_fb = np.array([fb.wfs[w].ev_len for w in range(n)], np.int64)
+        ev_rounds.append(int(lens_fb[act != 0].sum() + lens_rb[act == 2].sum()))
+    events = ev_base + sum(ev_rounds)
+    for _ in range(args.warmup):
+        rep.reset()
+        rep.base_replay()
+        for k in range(len(rep.rounds)):
+            rep.round(k)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(args.steps):
+        rep.reset()
+        rep.base_replay()
+        for k in range(len(rep.rounds)):
+            rep.round(k)
+    e1.record()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / args.steps
+    parity = None
+    if not args.no_parity:
+        import oracle
+        t1 = time.perf_counter()
+        g_state, g_vhs, g_pool, g_decs, _ = rep.run()
+        r_state, r_vhs, r_pool, r_decs, _ = oracle.ndc_replicate(base, rebuild, forks, threads=host_cores()[0])
+        bad = engine.compare(base, g_state, r_state, limit=10 ** 9)
+        bad_dec = sum(1 for k in range(len(forks)) for w in range(n)
+                      if bytes(g_decs[k][w]) != bytes(r_decs[k][w]))
+        vb = sum(1 for w in range(n) if ndc.branch_items(g_vhs, g_pool, w, g_vhs[w].current) !=
+                 ndc.branch_items(r_vhs, r_pool, w, r_vhs[w].current) or g_vhs[w].n_branches != r_vhs[w].n_branches)
+        parity = {"checked": True, "entries": n, "mismatched_entries": len({b.split(':')[0] for b in bad}),
+                  "mismatched_decisions": bad_dec, "mismatched_version_histories": vb,
+                  "first_mismatches": bad[:4], "seconds": time.perf_counter() - t1,
+                  "method": "engine.compare of the final persisted state + each round's decisions + the current "
+                            "branch's VersionHistory, GPU vs oracle.ndc_replicate"}
+        log(f"NDC parity: {parity['mismatched_entries']} states, {bad_dec} decisions, {vb} VHs differ "
+            f"({parity['seconds']:.1f}s)")
+    acts = {abi.NDC_ACTIONS[a]: int(c) for k in range(len(forks))
+            for a, c in zip(*np.unique([decs[k][w].action for w in range(n)], return_counts=True))}
+    # algorithmic bytes per step: every replayed event's slab element (60 B, cdr.h row layout)
+    # + the per-workflow records each replay writes (SURVEY 8(d): 264 B), base + 2 rounds x
+    # (rebuild + apply)
+    alg = events * 60 + n * 264 * (1 + 2 * len(forks))
+    line = {
+        "metric": "history events replayed/sec + workflows rebuilt/sec (node), % of HBM roofline",
+        "value": events / (ms / 1e3), "unit": "events/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms, "wall_ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic forked config 5 (cadence_amd.ndc.synth_forked)",
+        "config": {"workload": f"C5-forked-{n}wf-ndc-replicate", "workflows_per_gpu": n, "rounds": len(forks),
+                   "events_per_step": events, "events_base": ev_base, "events_rounds": ev_rounds,
+                   "decisions": acts, "parallelism": "shard1"},
+        "workflows_per_s": n / (ms / 1e3),
+        "roofline": {"bound": "hbm", "achieved": alg / (ms / 1e3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": alg / (ms / 1e3) / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                     "traffic_note": "no PMC pass of this line", "algorithmic_bytes_per_step": alg,
+                     "kernel": "k_ndc_branch + k_replay* + k_refresh + k_ndc_verify/apply (one step)"},
+        "host": {"setup_s": setup_s},
+        "parity": parity, "parity_checked": parity is not None,
+    }
+    print(json.dumps(line), flush=True)
+    rep.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -343,7 +435,12 @@ def main():
     ap.add_argument("--cls-in-step", action="store_true",
                     help="class-sorted blocks built on the device (k_cls_count / k_cls_fill) INSIDE every timed step, "
                          "instead of emitted by the host packer")
+    ap.add_argument("--ndc-forks", action="store_true",
+                    help="configs[4]'s conflict-resolution line: the forked config-5 population replicated on "
+                         "the device (base branch + 2 fork rounds per step); --wfs workflows")
     args = ap.parse_args()
+    if args.ndc_forks:
+        return ndc_forks_line(args)
 
     import torch
     world, rank, local = dist_env()

@@ -322,6 +322,7 @@ def _hip():
         L.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
         L.hipFree.argtypes = [C.c_void_p]
         L.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        L.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
         L.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
         L.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
         L.hipStreamDestroy.argtypes = [C.c_void_p]

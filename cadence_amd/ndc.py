@@ -279,8 +279,17 @@ class DeviceReplicator:
             self.rounds.append((r, pl))
         self.vhs_h, self.pool_h = new_vhs(n, items_cap)
         self.vhs, self.pool = dev.up(self.vhs_h), dev.up(self.pool_h)
+        self.vhs_fresh = dev.up(self.vhs_h)  # NewVersionHistories for every workflow (reset())
         self.events = [int(sum(base.wfs[w].ev_len for w in range(n)))] + [
             int(sum(fb.wfs[w].ev_len for w in range(n))) for fb, _, _ in forks]
+
+    def reset(self, stream=None):
+        """A fresh run: every workflow's VersionHistories back to empty (the base replay
+        re-creates the state buffer itself); a device-to-device copy on the stream."""
+        hip = self.dev.hip
+        if hip.hipMemcpyAsync(C.c_void_p(self.vhs), C.c_void_p(self.vhs_fresh),
+                              C.c_size_t(C.sizeof(self.vhs_h)), 3, C.c_void_p(stream)) != 0:
+            raise RuntimeError("hipMemcpyAsync D2D failed")
 
     def base_replay(self, stream=None):
         L = abi.lib()
@@ -303,6 +312,7 @@ class DeviceReplicator:
     def run(self):
         """Base replay + every round; returns (state Outputs, vhs, pool, [decisions],
         [(rebuild Outputs, apply Outputs) per round])."""
+        self.reset()
         self.base_replay()
         per_round, decs = [], []
         for k, (r, pl) in enumerate(self.rounds):
