@@ -337,7 +337,15 @@ def ndc_forks_line(args):
     eng = engine.Engine(0)
     n = args.wfs
     t0 = time.perf_counter()
+    import threading
+    beat = threading.Event()
+
+    def heartbeat():  # long host phases at 1M workflows: a progress line every minute
+        while not beat.wait(60):
+            log(f"NDC forks: {time.perf_counter() - t0:.0f}s")
+    threading.Thread(target=heartbeat, daemon=True).start()
     base, rebuild, forks = ndc.synth_forked(5, n, args.seed)
+    log(f"NDC forks: synthesized {n} forked workflows ({time.perf_counter() - t0:.0f}s)")
     rep = ndc.DeviceReplicator(eng, base, rebuild, forks)
     setup_s = time.perf_counter() - t0
     log(f"NDC forks: {n} workflows, host synth + plan + upload {setup_s:.1f}s")
@@ -409,6 +417,7 @@ def ndc_forks_line(args):
         "host": {"setup_s": setup_s},
         "parity": parity, "parity_checked": parity is not None,
     }
+    beat.set()
     print(json.dumps(line), flush=True)
     rep.close()
 

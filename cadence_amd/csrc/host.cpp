@@ -356,8 +356,11 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
       c.vh_cap += s.vh_cap;
       c.rp_cap += s.rp_cap;
       c.sa_cap += s.sa_cap;
-      c.act_live += s.act_cap;
-      c.timer_live += s.timer_cap;
+      // live rows: at most the state's peak live sets (the sum of its parts' simulated
+      // peaks, cadence_amd/ndc.py state_caps_for), not its capacities (every row any part
+      // ever added): the general kernel sizes its working slots by these
+      c.act_live += s.act_live;
+      c.timer_live += s.timer_live;
       c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_REG | CDR_CAP_REG2 | CDR_CAP_REG0);
     }
     cdr_internal::task_caps(b->events + d.ev_off, d.ev_len, &c.xfer_cap, &c.ttask_cap);

@@ -51,6 +51,9 @@ def branch_items(vhs, pool, w: int, b: int):
 TABLE_CAP = {"act": "act_cap", "timer": "timer_cap", "child": "child_cap", "cancel": "cancel_cap",
              "signal": "signal_cap", "vh": "vh_cap", "rp": "rp_cap", "sa": "sa_cap"}
 TABLE_OFF = {t: c.replace("_cap", "_off") for t, c in TABLE_CAP.items()}
+# peak live activities / user timers: a state the rounds leave holds at most the sum of its
+# parts' peaks (the apply batches' working slots are sized by it, cdr_plan_ndc_apply)
+TUPLE_LIVE = ("act_live", "timer_live")
 
 
 class GpuBackend:
@@ -225,17 +228,18 @@ def download_out(dev: _Dev, o: abi.CdrOut, n: int, pl: engine.Plan, tasks: bool 
     return out
 
 
-def state_caps_for(base: engine.Batch, rebuild: engine.Batch, forks):
+def state_caps_for(base: engine.Batch, rebuild: engine.Batch, forks, live_sum: bool = False):
     """Per-workflow capacities of the state buffer a replication run keeps: the base replay's
     flags, room for the largest state any round can leave (base or rebuilt rows + every
-    fork's new rows)."""
+    fork's new rows).  live_sum: the peak live sets summed over the parts too (the bound an
+    apply batch's working slots are sized by, cdr_plan_ndc_apply); else the base's own."""
     n = base.n_wfs
     bp = engine.plan(base)
     parts = [engine.plan(rebuild)] + [engine.plan(fb) for fb, _, _ in forks]
     caps = (abi.CdrWfCaps * max(1, n))()
     C.memmove(caps, bp.caps, C.sizeof(abi.CdrWfCaps) * n)
     for w in range(n):
-        for cname in TABLE_CAP.values():
+        for cname in (TUPLE_LIVE if live_sum else ()) + tuple(TABLE_CAP.values()):
             setattr(caps[w], cname, getattr(bp.caps[w], cname) + sum(getattr(p.caps[w], cname) for p in parts))
     tot = offsets_from_caps(caps, n)
     return _plan_from(caps, tot)
@@ -254,6 +258,7 @@ class DeviceReplicator:
         self.eng, self.n, self.dev = eng, n, _Dev()
         dev = self.dev
         self.state_plan = state_caps_for(base, rebuild, forks)
+        live_bound = state_caps_for(base, rebuild, forks, live_sum=True).caps
         self.base_db = upload_batch(dev, base, self.state_plan.caps)
         self.state = alloc_out(dev, n, self.state_plan.totals)
         self.state_caps_d = self.base_db.caps  # the state's capacities (the base batch was planned with them)
@@ -264,7 +269,7 @@ class DeviceReplicator:
         for fb, tasks, items in forks:
             caps = (abi.CdrWfCaps * max(1, n))()
             tot = abi.CdrTotals()
-            rc = L.cdr_plan_ndc_apply(C.byref(fb.cstruct()), self.state_plan.caps, caps, C.byref(tot))
+            rc = L.cdr_plan_ndc_apply(C.byref(fb.cstruct()), live_bound, caps, C.byref(tot))
             if rc:
                 raise RuntimeError(f"cdr_plan_ndc_apply rc={rc}")
             pl = _plan_from(caps, tot)
