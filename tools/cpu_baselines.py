@@ -25,15 +25,16 @@ def main():
     rows = {}
     for c in args.configs:
         t0 = time.perf_counter()
-        # C1 is the reference's single-workflow CPU case: a sample of single histories
-        n = args.wfs if c != 1 else min(args.wfs, 2000)
+        # C1 (configs[0]) is the reference's CPU case at its own size: 10k echo workflows
+        n = args.wfs if c != 1 else 10000
         r = bench.cpu_baseline(c, n, 0x5EED0000 + c, min_seconds=args.seconds)
         r["wall_s"] = time.perf_counter() - t0
         rows[f"C{c}"] = r
         print(json.dumps({f"C{c}": r}), flush=True)
     if args.out:
         with open(args.out, "w") as f:
-            json.dump({"source": "tools/cpu_baselines.py", "host_cpus": os.cpu_count(), "configs": rows}, f, indent=1)
+            json.dump({"source": "tools/cpu_baselines.py", "host_cpus": os.cpu_count(),
+                       "cores_used": bench.host_cores(), "configs": rows}, f, indent=1)
 
 
 if __name__ == "__main__":
