@@ -461,6 +461,8 @@ def main():
         dist = None
         torch.cuda.set_device(0)
     L = abi.lib()
+    if L.cdr_build_flags():  # a profiling / tuning variant never reaches a reported line
+        raise SystemExit(f"libcdr.so is a variant build (cdr_build_flags = {L.cdr_build_flags():#x}); rebuild it")
     ctx = L.cdr_create(torch.cuda.current_device(), None)
     if not ctx:
         raise SystemExit("cdr_create failed (no GPU?) — the engine has no CPU fallback")

@@ -380,6 +380,7 @@ EXPORTS = {
     "cdr_workflow_id_to_shard": (i32, [C.c_char_p, C.c_size_t, i32]),
     "cdr_last_kernel_ms": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "cdr_version": (C.c_char_p, []),
+    "cdr_build_flags": (u32, []),
     "cdr_timing_begin": (i32, [C.c_void_p, u32]),
     "cdr_timing_read": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(u32)]),
     "cdr_synth_shards": (i32, [u64, i32, C.c_void_p]),

@@ -2151,6 +2151,19 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   return CDR_API_OK;
 }
 
+uint32_t cdr_build_flags(void) {
+  uint32_t f = 0;
+#ifdef CDR_PAR_PROF
+  f |= 1u;
+#endif
+  if (CDR_PAR_PRIO != 0 || CDR_FDEPTH != 2 || CDR_DEPTH != 1 || CDR_TYPED != 1 || CDR_FAST_DELTA != 1 ||
+      CDR_VHBF != 1 || CDR_CLS_DEPTH != 1 || CDR_CLS_PDEPTH != 4 || CDR_CLS_DEPTH_PAR != 4 ||
+      CDR_CLS_PDEPTH_PAR != 16 || CDR_WPE_FAST != 3 || CDR_WPE != 3 || CDR_WPE_CLS != 4 || CDR_WPE_CLS0 != 4 ||
+      CDR_WPE_CLS2 != 2 || FAST_CK != 8u)
+    f |= 2u;
+  return f;
+}
+
 int cdr_last_kernel_ms(cdr_ctx* c, float* replay_ms, float* finalize_ms) {
   if (!c || !c->timed) return CDR_API_EINVAL;
   HIPCHK(hipEventSynchronize(c->ev[2]));

@@ -711,6 +711,12 @@ int cdr_timing_read(cdr_ctx* ctx, float* ms, uint32_t* n);
 
 const char* cdr_version(void);
 
+/* Compile-time variant flags of this build (0 = the product build): bit 0 the PAR
+ * profiling variant (CDR_PAR_PROF: writes per-wave times into result fields), bit 1 any
+ * tuning knob off its default (prefetch depths, wave priority, kernel variants).  bench.py
+ * refuses to report a line from a library that is not 0. */
+uint32_t cdr_build_flags(void);
+
 #ifdef __cplusplus
 }
 #endif

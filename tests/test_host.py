@@ -34,6 +34,12 @@ def test_library_exports_every_declared_symbol():
     assert set(abi.EXPORTS) >= declared - {"cdr_struct_size"}
 
 
+def test_in_tree_library_is_the_product_build():
+    """No profiling or tuning variant (cdr_build_flags) in the library the tests, smoke()
+    and bench.py load."""
+    assert abi.lib().cdr_build_flags() == 0
+
+
 def test_struct_layouts_match_mirrors():
     abi.check_layouts()
 
