@@ -2024,17 +2024,31 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const bool on[cdr_ctx::N_SIDE] = {wv, reg2, gen, reg0, fst, reg1, par};
   int kinds = 0;
   for (bool o : on) kinds += o ? 1 : 0;
-  bool fk[cdr_ctx::N_SIDE];  // class i forks onto side[side_of[i]]
+  // this launch's class -> stream map: a class sharing a stream with another takes the PAR
+  // stream instead when the batch has no PAR slices (that stream's queue would sit idle)
+  int so[cdr_ctx::N_SIDE];
+  for (int i = 0; i < cdr_ctx::N_SIDE; i++) so[i] = c->side_of[i];
+  if (!on[6] && so[6] < cdr_ctx::N_SIDE)
+    for (int i = 0; i < 6; i++)
+      if (on[i] && so[i] < cdr_ctx::N_SIDE && so[i] != so[6]) {
+        bool shared = false;
+        for (int j = 0; j < i; j++) shared |= on[j] && so[j] == so[i];
+        if (shared) {
+          so[i] = so[6];
+          break;
+        }
+      }
+  bool fk[cdr_ctx::N_SIDE];  // class i forks onto side[so[i]]
   bool used[cdr_ctx::N_SIDE] = {};  // side stream j carries a forked class
   bool any_fork = false;
   for (int i = 0; i < cdr_ctx::N_SIDE; i++) {
-    any_fork |= (fk[i] = c->concurrent && on[i] && kinds > 1 && c->side_of[i] < cdr_ctx::N_SIDE);
-    if (fk[i]) used[c->side_of[i]] = true;
+    any_fork |= (fk[i] = c->concurrent && on[i] && kinds > 1 && so[i] < cdr_ctx::N_SIDE);
+    if (fk[i]) used[so[i]] = true;
   }
   if (any_fork) HIPCHK(hipEventRecord(c->fork, st));
   for (int j = 0; j < cdr_ctx::N_SIDE; j++)
     if (used[j]) HIPCHK(hipStreamWaitEvent(c->side[j], c->fork, 0));
-  auto sx = [&](int i) { return fk[i] ? c->side[c->side_of[i]] : st; };
+  auto sx = [&](int i) { return fk[i] ? c->side[so[i]] : st; };
   // each class's launches (its stream sx(i)); the order they are issued in decides which
   // class's workgroups take the CUs first (CDR_LAUNCH_ORDER overrides: a digit string of
   // side-stream indices, default \"6012345\": PAR, wave, 12-activity, general, small-table,
