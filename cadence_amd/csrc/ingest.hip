@@ -109,7 +109,7 @@ struct Rd {
   const LDS3 uint8_t* sb;  // the wave's staged bytes: addresses [s_lo, s_lo + s_n)
   uint64_t s_lo, s_n;
   int32_t err;
-  __device__ void init(const uint8_t* base, uint64_t p, uint64_t e, uint64_t t) {
+  __device__ __forceinline__ void init(const uint8_t* base, uint64_t p, uint64_t e, uint64_t t) {
     b = base;
     pos = p;
     end = e;
@@ -119,7 +119,7 @@ struct Rd {
     s_lo = s_n = 0;
     err = CDR_DEC_OK;
   }
-  __device__ uint32_t at(uint64_t p) {
+  __device__ __forceinline__ uint32_t at(uint64_t p) {
     // the window is aligned in the address space (the buffer itself need not be)
     const uint64_t addr = (uint64_t)(uintptr_t)(b + p), a = addr & ~15ull;
     if (addr - s_lo < s_n) return sb[addr - s_lo];
@@ -134,8 +134,8 @@ struct Rd {
     const uint32_t o = (uint32_t)(addr - a);
     return (uint32_t)(((o < 8) ? (w0 >> (8 * o)) : (w1 >> (8 * (o - 8)))) & 0xFFu);
   }
-  __device__ bool ok() const { return err == CDR_DEC_OK; }
-  __device__ bool need(uint64_t n) {
+  __device__ __forceinline__ bool ok() const { return err == CDR_DEC_OK; }
+  __device__ __forceinline__ bool need(uint64_t n) {
     if (err) return false;
     if (end - pos < n) {
       err = CDR_DEC_TRUNCATED;
@@ -144,27 +144,27 @@ struct Rd {
     }
     return true;
   }
-  __device__ uint32_t u8() {
+  __device__ __forceinline__ uint32_t u8() {
     if (!need(1)) return 0;
     return at(pos++);
   }
-  __device__ uint32_t be16() {
+  __device__ __forceinline__ uint32_t be16() {
     if (!need(2)) return 0;
     const uint32_t v = (at(pos) << 8) | at(pos + 1);
     pos += 2;
     return v;
   }
-  __device__ uint32_t be32() {
+  __device__ __forceinline__ uint32_t be32() {
     if (!need(4)) return 0;
     const uint32_t v = (at(pos) << 24) | (at(pos + 1) << 16) | (at(pos + 2) << 8) | at(pos + 3);
     pos += 4;
     return v;
   }
-  __device__ uint64_t be64() {
+  __device__ __forceinline__ uint64_t be64() {
     const uint64_t hi = be32();
     return (hi << 32) | be32();
   }
-  __device__ int32_t size() {  // a length / count: negative is a decode error
+  __device__ __forceinline__ int32_t size() {  // a length / count: negative is a decode error
     const int32_t n = (int32_t)be32();
     if (n < 0 && !err) err = CDR_DEC_BAD_SIZE;
     return n < 0 ? 0 : n;
@@ -178,7 +178,7 @@ struct Rd {
   }
 };
 
-__device__ uint32_t fixed_size(uint32_t t) {
+__device__ __forceinline__ uint32_t fixed_size(uint32_t t) {
   switch (t) {
     case T_BOOL: case T_BYTE: return 1;
     case T_I16: return 2;
@@ -189,7 +189,7 @@ __device__ uint32_t fixed_size(uint32_t t) {
 }
 
 // skip one value of wire type t (iterative: an explicit stack of open containers)
-__device__ void skip(Rd& r, uint32_t t) {
+__device__ __forceinline__ void skip_body(Rd& r, uint32_t t) {
   struct Fr {
     uint32_t kind, t1, t2;
     uint32_t n;  // remaining elements (maps: 2 per pair)
@@ -249,6 +249,43 @@ __device__ void skip(Rd& r, uint32_t t) {
   }
 }
 
+// a container skipped out of line: the reader's fields go by value and the new position /
+// error come back in registers, so a call site does not force the caller's reader (or any
+// other parser state) into scratch memory; the walker's own stack lives in the callee's frame
+struct SkipRes {
+  uint64_t pos;
+  int32_t err;
+};
+__device__ __attribute__((noinline)) SkipRes skip_v(const uint8_t* b, uint64_t pos, uint64_t end, uint64_t total,
+                                                    const LDS3 uint8_t* sb, uint64_t s_lo, uint64_t s_n, uint32_t t) {
+  Rd r;
+  r.init(b, pos, end, total);
+  r.sb = sb;
+  r.s_lo = s_lo;
+  r.s_n = s_n;
+  skip_body(r, t);
+  return SkipRes{r.pos, r.err};
+}
+__device__ __forceinline__ void skip(Rd& r, uint32_t t) {
+  if (r.err) return;
+  const SkipRes x = skip_v(r.b, r.pos, r.end, r.total, r.sb, r.s_lo, r.s_n, t);
+  r.pos = x.pos;
+  r.err = x.err;
+}
+
+// skip one value: a fixed-size or string value inline; a container through skip() (a call:
+// its explicit stack lives in scratch, so the common field types must not pay for it)
+__device__ __forceinline__ void skip1(Rd& r, uint32_t t) {
+  if (const uint32_t fs = fixed_size(t)) {
+    if (r.need(fs)) r.pos += fs;
+  } else if (t == T_STRING) {
+    const uint32_t n = (uint32_t)r.size();
+    if (r.need(n)) r.pos += n;
+  } else {
+    skip(r, t);
+  }
+}
+
 // ---------------------------------------------------------------- one blob
 enum Pass { COUNT = 0, INTERN = 1, FILL = 2 };
 
@@ -271,12 +308,12 @@ struct Ctx {  // per launch
 
 template <int P>
 struct Blob {
-  const Ctx& C;
+  const Ctx C;  // by value: a reference to the kernel argument would copy it to scratch
   Rd r;
   uint32_t n_ev = 0, n_kv = 0, n_rp = 0, n_str = 0;
   uint64_t ev0 = 0, kv0 = 0, rp0 = 0;
 
-  __device__ Blob(const Ctx& c, uint32_t b) : C(c) {
+  __device__ __forceinline__ Blob(const Ctx& c, uint32_t b) : C(c) {
     r.init(c.bytes, c.blob_off[b], c.blob_off[b + 1], c.total);
     if (P == FILL) {
       ev0 = c.bases[3ull * b];
@@ -286,7 +323,7 @@ struct Blob {
   }
 
   // a string / binary value (the field's wire type already checked): its handle
-  __device__ uint32_t str() {
+  __device__ __forceinline__ uint32_t str() {
     const uint32_t n = (uint32_t)r.size();
     if (!r.need(n)) return 0;
     const uint64_t at = r.pos;
@@ -302,9 +339,9 @@ struct Blob {
     return tab_lookup(C.T, h);
   }
   // a whole value of wire type t interned by its bytes (structures kept as one handle)
-  __device__ uint32_t raw(uint32_t t) {
+  __device__ __forceinline__ uint32_t raw(uint32_t t) {
     const uint64_t at = r.pos;
-    skip(r, t);
+    skip1(r, t);  // (a container: skip())
     if (!r.ok() || r.pos == at) return 0;
     const uint32_t n = (uint32_t)(r.pos - at);
     n_str++;
@@ -316,14 +353,14 @@ struct Blob {
     }
     return tab_lookup(C.T, h);
   }
-  __device__ uint32_t domain_id(uint32_t name, bool* missing) {
+  __device__ __forceinline__ uint32_t domain_id(uint32_t name, bool* missing) {
     const uint32_t id = (P == FILL && name < C.n_seeds) ? C.dom_id[name] : UNASSIGNED;
     *missing = id == UNASSIGNED;
     return id == UNASSIGNED ? 0u : id;
   }
   // iterate the fields of a struct: f(field type, field id) must consume the value
   template <class F>
-  __device__ void fields(F&& f) {
+  __device__ __forceinline__ void fields(F&& f) {
     while (r.ok()) {
       const uint32_t ft = r.u8();
       if (!r.ok() || ft == T_STOP) return;
@@ -332,41 +369,41 @@ struct Blob {
       f(ft, fid);
     }
   }
-  __device__ int64_t i64(uint32_t ft) {
+  __device__ __forceinline__ int64_t i64(uint32_t ft) {
     if (ft != T_I64) {
-      skip(r, ft);
+      skip1(r, ft);
       return 0;
     }
     return (int64_t)r.be64();
   }
   // name of a WorkflowType / TaskList / ActivityType (field 10)
-  __device__ uint32_t name_of(uint32_t ft) {
+  __device__ __forceinline__ uint32_t name_of(uint32_t ft) {
     if (ft != T_STRUCT) {
-      skip(r, ft);
+      skip1(r, ft);
       return 0;
     }
     uint32_t h = 0;
     fields([&](uint32_t t, uint32_t id) {
       if (id == 10 && t == T_STRING) h = str();
-      else skip(r, t);
+      else skip1(r, t);
     });
     return h;
   }
   // shared.WorkflowExecution{10 workflowId, 20 runId}
-  __device__ void execution(uint32_t ft, uint32_t* wid, uint32_t* rid) {
+  __device__ __forceinline__ void execution(uint32_t ft, uint32_t* wid, uint32_t* rid) {
     if (ft != T_STRUCT) {
-      skip(r, ft);
+      skip1(r, ft);
       return;
     }
     fields([&](uint32_t t, uint32_t id) {
       if (id == 10 && t == T_STRING) *wid = str();
       else if (id == 20 && t == T_STRING) *rid = str();
-      else skip(r, t);
+      else skip1(r, t);
     });
   }
   // RetryPolicy (shared.thrift RetryPolicy): the fields the record keeps
   template <class A>
-  __device__ void retry(A& a) {
+  __device__ __forceinline__ void retry(A& a) {
     fields([&](uint32_t t, uint32_t id) {
       if (id == 10 && t == T_I32) a.retry_initial_s = (int32_t)r.be32();
       else if (id == 20 && t == T_DOUBLE) a.backoff_coefficient = __longlong_as_double((long long)r.be64());
@@ -378,17 +415,17 @@ struct Blob {
         r.u8();
         const int32_t cnt = r.size();
         r.pos = r.ok() ? at : r.pos;
-        a.nonretriable = cnt > 0 ? raw(T_LIST) : (skip(r, T_LIST), 0u);
-      } else skip(r, t);
+        a.nonretriable = cnt > 0 ? raw(T_LIST) : (skip1(r, T_LIST), 0u);
+      } else skip1(r, t);
     });
   }
   // SearchAttributes{10: map<string, binary>} -> kv rows; returns the pair count
-  __device__ uint32_t search_attrs(uint32_t* off) {
+  __device__ __forceinline__ uint32_t search_attrs(uint32_t* off) {
     uint32_t cnt = 0;
     *off = (uint32_t)(kv0 + n_kv);
     fields([&](uint32_t t, uint32_t id) {
       if (id != 10 || t != T_MAP) {
-        skip(r, t);
+        skip1(r, t);
         return;
       }
       const uint32_t kt = r.u8(), vt = r.u8();
@@ -400,27 +437,27 @@ struct Blob {
           n_kv++;
           cnt++;
         } else {  // not a map<string, binary>: thriftrw reads no entries
-          skip(r, kt);
-          skip(r, vt);
+          skip1(r, kt);
+          skip1(r, vt);
         }
       }
     });
     return cnt;
   }
   // ResetPoints{10: list<ResetPointInfo>} -> reset-point rows; false when field 10 is absent
-  __device__ bool reset_points(uint32_t* off, uint32_t* len) {
+  __device__ __forceinline__ bool reset_points(uint32_t* off, uint32_t* len) {
     bool have = false;
     *off = (uint32_t)(rp0 + n_rp);
     *len = 0;
     fields([&](uint32_t t, uint32_t id) {
       if (id != 10 || t != T_LIST) {
-        skip(r, t);
+        skip1(r, t);
         return;
       }
       const uint32_t et = r.u8();
       const int32_t n = r.size();
       if (et != T_STRUCT) {  // not a list of structs: no points
-        for (int32_t i = 0; i < n && r.ok(); i++) skip(r, et);
+        for (int32_t i = 0; i < n && r.ok(); i++) skip1(r, et);
         return;
       }
       have = true;
@@ -444,7 +481,7 @@ struct Blob {
             p.flags |= CDR_RP_HAS_EXPIRING;
           } else if (id2 == 60 && t2 == T_BOOL) {
             p.flags |= CDR_RP_HAS_RESETTABLE | (r.u8() ? CDR_RP_RESETTABLE : 0u);
-          } else skip(r, t2);
+          } else skip1(r, t2);
         });
         if (P == FILL) C.rps[rp0 + n_rp] = p;
         n_rp++;
@@ -455,7 +492,7 @@ struct Blob {
   }
 
   // WorkflowExecutionStartedEventAttributes (shared.thrift, field 40 of HistoryEvent)
-  __device__ void started(cdr_attr_wf_started& s) {
+  __device__ __forceinline__ void started(cdr_attr_wf_started& s) {
     fields([&](uint32_t t, uint32_t id) {
       switch (id) {
         case 10: s.workflow_type = name_of(t); break;
@@ -465,7 +502,7 @@ struct Blob {
             s.flags |= CDR_SF_HAS_PARENT_DOMAIN;
             s.parent_domain_id = domain_id(str(), &miss);
             s.flags |= miss ? CDR_SF_PARENT_DOMAIN_MISSING : 0u;
-          } else skip(r, t);
+          } else skip1(r, t);
           break;
         case 14:
           if (t == T_STRUCT) s.flags |= CDR_SF_HAS_PARENT_EXEC;
@@ -475,54 +512,54 @@ struct Blob {
           if (t == T_I64) {
             s.flags |= CDR_SF_HAS_PARENT_INITIATED;
             s.parent_initiated_id = (int64_t)r.be64();
-          } else skip(r, t);
+          } else skip1(r, t);
           break;
         case 20: s.task_list = name_of(t); break;
-        case 40: if (t == T_I32) s.exec_timeout_s = (int32_t)r.be32(); else skip(r, t); break;
-        case 50: if (t == T_I32) s.task_timeout_s = (int32_t)r.be32(); else skip(r, t); break;
-        case 54: if (t == T_STRING) s.continued_run_id = str(); else skip(r, t); break;
+        case 40: if (t == T_I32) s.exec_timeout_s = (int32_t)r.be32(); else skip1(r, t); break;
+        case 50: if (t == T_I32) s.task_timeout_s = (int32_t)r.be32(); else skip1(r, t); break;
+        case 54: if (t == T_STRING) s.continued_run_id = str(); else skip1(r, t); break;
         case 55:
           if (t == T_I32) {  // ContinueAsNewInitiator: Decider 0, RetryPolicy 1, CronSchedule 2
             const int32_t v = (int32_t)r.be32();
             s.flags |= CDR_SF_HAS_INITIATOR | (v == 2 ? CDR_SF_CRON_INITIATOR : 0u) |
                        (v == 1 ? CDR_SF_RETRY_INITIATOR : 0u) | (v == 0 ? CDR_SF_DECIDER_INITIATOR : 0u);
-          } else skip(r, t);
+          } else skip1(r, t);
           break;
         case 70:
           if (t == T_STRUCT) {
             s.flags |= CDR_SF_HAS_RETRY;
             retry(s);
-          } else skip(r, t);
+          } else skip1(r, t);
           break;
-        case 80: if (t == T_I32) s.attempt = (int32_t)r.be32(); else skip(r, t); break;
-        case 90: if (t == T_I64) s.expiration_ts = (int64_t)r.be64(); else skip(r, t); break;
-        case 100: if (t == T_STRING) s.cron_schedule = str(); else skip(r, t); break;
-        case 110: if (t == T_I32) s.first_decision_backoff_s = (int32_t)r.be32(); else skip(r, t); break;
+        case 80: if (t == T_I32) s.attempt = (int32_t)r.be32(); else skip1(r, t); break;
+        case 90: if (t == T_I64) s.expiration_ts = (int64_t)r.be64(); else skip1(r, t); break;
+        case 100: if (t == T_STRING) s.cron_schedule = str(); else skip1(r, t); break;
+        case 110: if (t == T_I32) s.first_decision_backoff_s = (int32_t)r.be32(); else skip1(r, t); break;
         case 120:
           if (t == T_STRUCT) {
             s.flags |= CDR_SF_HAS_MEMO;
             s.memo = raw(T_STRUCT);
-          } else skip(r, t);
+          } else skip1(r, t);
           break;
         case 121:
           if (t == T_STRUCT) {
             s.flags |= CDR_SF_HAS_SEARCH_ATTR;
             s.search_attr_len = search_attrs(&s.search_attr_off);
-          } else skip(r, t);
+          } else skip1(r, t);
           break;
         case 130:
           if (t == T_STRUCT) {
             if (reset_points(&s.reset_points_off, &s.reset_points_len)) s.flags |= CDR_SF_HAS_RESET_POINTS;
             else s.reset_points_off = s.reset_points_len = 0;
-          } else skip(r, t);
+          } else skip1(r, t);
           break;
-        default: skip(r, t); break;
+        default: skip1(r, t); break;
       }
     });
   }
 
   // StartChild / SignalExternal / RequestCancelExternal ...Initiated
-  __device__ void external(uint32_t attr, cdr_attr_external& x) {
+  __device__ __forceinline__ void external(uint32_t attr, cdr_attr_external& x) {
     // field ids: domain, workflowId (child), WorkflowExecution, workflowType (child),
     // signalName, input, control, childWorkflowOnly, parentClosePolicy
     const bool child = attr == 340, sig = attr == 420;
@@ -543,7 +580,7 @@ struct Blob {
       else if (id == f_ctl && t == T_STRING) x.control = str();
       else if (f_only && id == f_only && t == T_BOOL) x.flags |= r.u8() ? CDR_XF_CHILD_ONLY : 0u;
       else if (child && id == 81 && t == T_I32) x.parent_close_policy = (int32_t)r.be32();
-      else skip(r, t);
+      else skip1(r, t);
     });
     (void)have_dom;
     x.domain = dom_name;
@@ -553,7 +590,7 @@ struct Blob {
   }
 
   // the attribute struct (HistoryEvent field `attr`) into the record's union
-  __device__ void attributes(uint32_t attr, cdr_event& e) {
+  __device__ __forceinline__ void attributes(uint32_t attr, cdr_event& e) {
     // decision / activity events: field ids of scheduledEventId, startedEventId,
     // requestId, activityId, timeoutType, attempt, binaryChecksum (0 = none)
     struct Ids {
@@ -589,7 +626,7 @@ struct Blob {
           if (id == 10) e.a.dt_sched.task_list = name_of(t);
           else if (id == 20 && t == T_I32) e.a.dt_sched.start_to_close_s = (int32_t)r.be32();
           else if (id == 30 && t == T_I64) e.a.dt_sched.attempt = (int64_t)r.be64();
-          else skip(r, t);
+          else skip1(r, t);
         });
         return;
       case 130: {
@@ -605,7 +642,7 @@ struct Blob {
           else if (id == 110 && t == T_STRUCT) {
             a.flags |= CDR_AF_HAS_RETRY;
             retry(a);
-          } else skip(r, t);
+          } else skip1(r, t);
         });
         if (a.domain) {  // the target domain's ID (refreshTasks, getTargetDomainID)
           bool miss;
@@ -622,7 +659,7 @@ struct Blob {
             const int64_t v = (int64_t)r.be64();
             if (attr == 180) a.start_to_fire_s = v;
             else if (attr != 240) a.started_event_id = v;
-          } else skip(r, t);
+          } else skip1(r, t);
         });
         return;
       }
@@ -630,13 +667,13 @@ struct Blob {
       case 330:
         fields([&](uint32_t t, uint32_t id) {
           if (id == 10 && t == T_STRING) e.a.can.new_execution_run_id = str();
-          else skip(r, t);
+          else skip1(r, t);
         });
         return;
       case 450:
         fields([&](uint32_t t, uint32_t id) {
           if (id == 20 && t == T_STRUCT) e.a.upsert.search_attr_len = search_attrs(&e.a.upsert.search_attr_off);
-          else skip(r, t);
+          else skip1(r, t);
         });
         return;
       default: break;
@@ -667,7 +704,7 @@ struct Blob {
           e.a.at.attempt = (int32_t)r.be32();
         } else if (m.cks && id == m.cks && t == T_STRING) {
           e.a.dt.binary_checksum = str();
-        } else skip(r, t);
+        } else skip1(r, t);
       });
       return;
     }
@@ -678,15 +715,15 @@ struct Blob {
         else if (m.we && id == m.we) {
           uint32_t wid = 0;
           execution(t, &wid, &e.a.ref.run_id);
-        } else skip(r, t);
+        } else skip1(r, t);
       });
       return;
     }
-    skip(r, T_STRUCT);  // an attribute struct the record form does not keep
+    skip1(r, T_STRUCT);  // an attribute struct the record form does not keep
   }
 
   // HistoryEvent (shared.thrift:868-916)
-  __device__ void event(bool first) {
+  __device__ __forceinline__ void event(bool first) {
     cdr_event e;
     uint64_t* z = reinterpret_cast<uint64_t*>(&e);
 #pragma unroll
@@ -695,12 +732,12 @@ struct Blob {
       switch (id) {
         case 10: e.event_id = i64(t); break;
         case 20: e.timestamp = i64(t); break;
-        case 30: if (t == T_I32) e.type = r.be32(); else skip(r, t); break;
+        case 30: if (t == T_I32) e.type = r.be32(); else skip1(r, t); break;
         case 35: e.version = i64(t); break;
         case 36: e.task_id = i64(t); break;
         default:
           if (t == T_STRUCT && id >= 40 && id <= 450 && id % 10 == 0) attributes(id, e);
-          else skip(r, t);
+          else skip1(r, t);
           break;
       }
     });
@@ -716,7 +753,7 @@ struct Blob {
   }
 
   // codec preamble + History{10: list<HistoryEvent>}
-  __device__ void run() {
+  __device__ __forceinline__ void run() {
     if (r.end <= r.pos) {
       r.err = CDR_DEC_MISSING_VERSION;
       return;
@@ -727,13 +764,13 @@ struct Blob {
     }
     fields([&](uint32_t t, uint32_t id) {
       if (id != 10 || t != T_LIST) {
-        skip(r, t);
+        skip1(r, t);
         return;
       }
       const uint32_t et = r.u8();
       const int32_t n = r.size();
       if (et != T_STRUCT) {  // not a list of structs: thriftrw reads no events
-        for (int32_t i = 0; i < n && r.ok(); i++) skip(r, et);
+        for (int32_t i = 0; i < n && r.ok(); i++) skip1(r, et);
         return;
       }
       // a repeated field 10 replaces the events read so far (FromWire assigns each occurrence)

@@ -5,6 +5,7 @@ import collections
 import csv
 import glob
 import os
+import re
 import sys
 
 d = sys.argv[1]
@@ -15,7 +16,8 @@ for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=T
     for r in csv.DictReader(open(f)):
         if kern not in r["Kernel_Name"]:
             continue
-        k = (r["Kernel_Name"].split("(")[0], r["Counter_Name"])
+        m = re.search(r"(k_\w+(<[^>]*>)?)", r["Kernel_Name"])
+        k = (m.group(1) if m else r["Kernel_Name"].split("(")[0], r["Counter_Name"])
         agg[k] += float(r["Counter_Value"])
         nd[k].add(r["Dispatch_Id"])
 waves = {}
