@@ -866,14 +866,32 @@ __global__ void k_seed(STab T, const uint8_t* bytes, const uint64_t* off, uint32
 // seeds may collide with one another only by equal strings; the first claimant keeps its
 // handle, the table's value is what lookups return
 
-__global__ void k_collect_new(STab T, unsigned long long* keys, uint64_t* idx, uint32_t* n_new) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > T.mask) return;
-  if (T.key[i] != 0ull && T.val[i] == UNASSIGNED) {
-    const uint32_t j = atomicAdd(n_new, 1u);
-    keys[j] = T.key[i];
+// the new strings' slots, one counter atomic per wavefront (its lanes' positions from the
+// ballot), not one per string on a single address
+__device__ __forceinline__ void collect_chunk(const STab& T, unsigned long long* keys, uint64_t* idx, uint32_t* n_new,
+                                              uint64_t i) {
+  const bool in = i <= T.mask;
+  const unsigned long long k = in ? T.key[i] : 0ull;
+  const bool take = in && k != 0ull && T.val[i] == UNASSIGNED;
+  const uint64_t m = __builtin_amdgcn_ballot_w64(take);
+  if (!m) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(n_new, (uint32_t)__builtin_popcountll(m));
+  base = __shfl(base, (int)leader, 64);
+  if (take) {
+    const uint32_t j = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    keys[j] = k;
     idx[j] = i;
   }
+}
+
+__global__ void k_collect_new(STab T, unsigned long long* keys, uint64_t* idx, uint32_t* n_new) {
+  // a grid-stride walk: the table has ~4 slots per string field, and one wavefront per
+  // 64 slots would make the launch dispatch-bound
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 <= T.mask; i0 += (uint64_t)gridDim.x * blockDim.x)
+    collect_chunk(T, keys, idx, n_new, i0 + threadIdx.x);
 }
 
 __global__ void k_rank(STab T, const uint64_t* idx_sorted, uint32_t n_new, uint32_t n_seeds, uint64_t* str_ref,
@@ -1001,7 +1019,8 @@ extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_inge
   if ((rc = ws(ctx, WS_IN_DOM, (n_str_fields + 1) > in->n_seeds ? (n_str_fields + 1) * 2 : in->n_seeds * 2ull,
                &k2)))
     return rc;
-  hipLaunchKernelGGL(k_collect_new, grid(cap), blk, 0, st, T, k1, i1, misc + 1);
+  hipLaunchKernelGGL(k_collect_new, dim3(cap / 256 < 4096 ? (uint32_t)((cap + 255) / 256) : 4096u), blk, 0, st, T, k1,
+                     i1, misc + 1);
   HIPCHK(hipGetLastError());
   uint32_t hm[2];
   HIPCHK(hipMemcpyAsync(hm, misc, 8, hipMemcpyDeviceToHost, st));
