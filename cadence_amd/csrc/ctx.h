@@ -27,7 +27,7 @@ enum cdr_ws_slot {
   // cdr_ingest_decode (ingest.hip)
   WS_IN_COUNTS, WS_IN_BASES, WS_IN_STATUS, WS_IN_ESTATUS, WS_IN_EVOFF, WS_IN_TKEY, WS_IN_TVAL, WS_IN_TREF,
   WS_IN_TLEN, WS_IN_SKEY, WS_IN_SIDX, WS_IN_SKEY2, WS_IN_SIDX2, WS_IN_TMP, WS_IN_DOM, WS_IN_EVENTS, WS_IN_KVS,
-  WS_IN_RPS, WS_IN_STRREF, WS_IN_STRLEN, WS_IN_MISC,
+  WS_IN_RPS, WS_IN_STRREF, WS_IN_STRLEN, WS_IN_MISC, WS_IN_GMAX, WS_IN_WBASE, WS_IN_CTMP,
   // cdr_ingest_plan (ingest.hip)
   WS_PL_CAPS, WS_PL_AWORDS, WS_PL_ABASE, WS_PL_WFS, WS_PL_LANE, WS_PL_SLEN, WS_PL_ROW0, WS_PL_SFLAGS, WS_PL_SCOFF,
   WS_PL_SCACT, WS_PL_SCTIM, WS_PL_SCRATCH, WS_PL_SLAB, WS_PL_ARENA,

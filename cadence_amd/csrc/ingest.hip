@@ -866,32 +866,57 @@ __global__ void k_seed(STab T, const uint8_t* bytes, const uint64_t* off, uint32
 // seeds may collide with one another only by equal strings; the first claimant keeps its
 // handle, the table's value is what lookups return
 
-// the new strings' slots, one counter atomic per wavefront (its lanes' positions from the
-// ballot), not one per string on a single address
-__device__ __forceinline__ void collect_chunk(const STab& T, unsigned long long* keys, uint64_t* idx, uint32_t* n_new,
-                                              uint64_t i) {
-  const bool in = i <= T.mask;
-  const unsigned long long k = in ? T.key[i] : 0ull;
-  const bool take = in && k != 0ull && T.val[i] == UNASSIGNED;
-  const uint64_t m = __builtin_amdgcn_ballot_w64(take);
-  if (!m) return;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(n_new, (uint32_t)__builtin_popcountll(m));
-  base = __shfl(base, (int)leader, 64);
-  if (take) {
-    const uint32_t j = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    keys[j] = k;
-    idx[j] = i;
-  }
+// the new strings' slots (key set, value UNASSIGNED), in two passes over the table and no
+// shared counter: each of COLLECT_WG workgroups counts the new slots of its span of the
+// table, the counts are scanned, and each workgroup writes its slots from its offset (one
+// atomic per wavefront on a single counter took 8.9 ms: millions of new strings)
+constexpr uint32_t COLLECT_WG = 2048;
+__device__ __forceinline__ bool is_new(const STab& T, uint64_t i, unsigned long long* k) {
+  *k = i <= T.mask ? T.key[i] : 0ull;
+  return *k != 0ull && T.val[i] == UNASSIGNED;
 }
-
-__global__ void k_collect_new(STab T, unsigned long long* keys, uint64_t* idx, uint32_t* n_new) {
-  // a grid-stride walk: the table has ~4 slots per string field, and one wavefront per
-  // 64 slots would make the launch dispatch-bound
-  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 <= T.mask; i0 += (uint64_t)gridDim.x * blockDim.x)
-    collect_chunk(T, keys, idx, n_new, i0 + threadIdx.x);
+__global__ __launch_bounds__(256) void k_collect_count(STab T, uint32_t* counts) {
+  const uint64_t span = ((T.mask + 1 + COLLECT_WG - 1) / COLLECT_WG + 255) & ~255ull;
+  const uint64_t lo = (uint64_t)blockIdx.x * span;
+  uint32_t c = 0;
+  for (uint64_t i = lo + threadIdx.x; i < lo + span && i <= T.mask; i += 256) {
+    unsigned long long k;
+    c += is_new(T, i, &k) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+  __shared__ uint32_t part[4];
+  if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+__global__ __launch_bounds__(256) void k_collect_write(STab T, const uint32_t* offs, unsigned long long* keys,
+                                                       uint64_t* idx) {
+  const uint64_t span = ((T.mask + 1 + COLLECT_WG - 1) / COLLECT_WG + 255) & ~255ull;
+  const uint64_t lo = (uint64_t)blockIdx.x * span;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  __shared__ uint32_t part[4];
+  uint32_t base = offs[blockIdx.x];
+  for (uint64_t c0 = lo; c0 < lo + span && c0 <= T.mask; c0 += 256) {
+    const uint64_t i = c0 + threadIdx.x;
+    unsigned long long k;
+    const bool take = i < lo + span && is_new(T, i, &k);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(take);
+    __syncthreads();  // the previous chunk's reads of part[] are done
+    if (lane == 0) part[wv] = (uint32_t)__builtin_popcountll(m);
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t v = 0; v < 4; v++) {
+      before += v < wv ? part[v] : 0u;
+      total += part[v];
+    }
+    if (take) {
+      const uint32_t j = base + before +
+                         __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      keys[j] = k;
+      idx[j] = i;
+    }
+    base += total;
+  }
 }
 
 __global__ void k_rank(STab T, const uint64_t* idx_sorted, uint32_t n_new, uint32_t n_seeds, uint64_t* str_ref,
@@ -1019,8 +1044,20 @@ extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_inge
   if ((rc = ws(ctx, WS_IN_DOM, (n_str_fields + 1) > in->n_seeds ? (n_str_fields + 1) * 2 : in->n_seeds * 2ull,
                &k2)))
     return rc;
-  hipLaunchKernelGGL(k_collect_new, dim3(cap / 256 < 4096 ? (uint32_t)((cap + 255) / 256) : 4096u), blk, 0, st, T, k1,
-                     i1, misc + 1);
+  {  // the new strings: per-span counts, their scan, then the slots (k_collect_count / _write)
+    uint32_t *ccount, *coffs;
+    if ((rc = ws(ctx, WS_IN_GMAX, COLLECT_WG + 1ull, &ccount)) || (rc = ws(ctx, WS_IN_WBASE, COLLECT_WG + 1ull, &coffs)))
+      return rc;
+    HIPCHK(hipMemsetAsync(ccount + COLLECT_WG, 0, 4, st));
+    hipLaunchKernelGGL(k_collect_count, dim3(COLLECT_WG), blk, 0, st, T, ccount);
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ccount, coffs, (int)(COLLECT_WG + 1), st));
+    void* tmp = cdr_ws_get(ctx, WS_IN_CTMP, tb);
+    if (!tmp) return CDR_API_ENOMEM;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, ccount, coffs, (int)(COLLECT_WG + 1), st));
+    hipLaunchKernelGGL(k_collect_write, dim3(COLLECT_WG), blk, 0, st, T, coffs, k1, i1);
+    HIPCHK(hipMemcpyAsync(misc + 1, coffs + COLLECT_WG, 4, hipMemcpyDeviceToDevice, st));
+  }
   HIPCHK(hipGetLastError());
   uint32_t hm[2];
   HIPCHK(hipMemcpyAsync(hm, misc, 8, hipMemcpyDeviceToHost, st));
