@@ -103,3 +103,29 @@ def test_in_memory_carry_keeps_the_rebuilt_current_version():
     # the transient decision (ReplicateTransientDecisionTaskScheduled) takes GetCurrentVersion()
     assert (x0.decision_schedule_id, x0.decision_attempt) == (x1.decision_schedule_id, x1.decision_attempt) == (5, 1)
     assert (x0.decision_version, x1.decision_version) == (-24, 3)  # Load: EmptyVersion; in memory: the last item's
+
+
+def test_apply_working_slots_bounded_by_live_rows():
+    """cdr_plan_ndc_apply sizes an apply entry's live sets (the general kernel's working
+    slots) by the loaded state's peak live rows — the sum of the parts' simulated peaks —
+    not by its table capacities (every row any part ever added)."""
+    import ctypes as C
+    base, rebuild, forks = ndc.synth_forked(5, 200, 0x5EED0C05)
+    caps_tab = ndc.state_caps_for(base, rebuild, forks).caps
+    bound = ndc.state_caps_for(base, rebuild, forks, live_sum=True).caps
+    parts = [engine.plan(base), engine.plan(rebuild)] + [engine.plan(fb) for fb, _, _ in forks]
+    L = abi.lib()
+    fb = forks[0][0]
+    own = engine.plan(fb).caps
+    caps = (abi.CdrWfCaps * fb.n_wfs)()
+    tot = abi.CdrTotals()
+    assert L.cdr_plan_ndc_apply(C.byref(fb.cstruct()), bound, caps, C.byref(tot)) == 0
+    tighter = 0
+    for w in range(fb.n_wfs):
+        peak = sum(p.caps[w].act_live for p in parts)
+        assert bound[w].act_live == peak
+        assert bound[w].act_cap == caps_tab[w].act_cap  # the tables keep their capacities
+        assert caps[w].act_live == own[w].act_live + peak
+        assert caps[w].act_cap == own[w].act_cap + caps_tab[w].act_cap
+        tighter += caps[w].act_live < own[w].act_live + caps_tab[w].act_cap
+    assert tighter > 0
