@@ -199,10 +199,11 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
       c.flags |= CDR_CAP_LANE;
   }
   reg = reg && !(c.flags & CDR_CAP_FAST) && lv_max[0] <= CDR_REG_NT && lv_max[1] <= CDR_REG_NX &&
-        lv_max[2] <= CDR_REG_NX && lv_max[3] <= CDR_REG_NX && rp_cks.size() <= CDR_REG_NRP &&
-        sa_keys.size() <= CDR_REG_NSA;
-  if (reg && live_max <= (int64_t)CDR_REG_NA) c.flags |= CDR_CAP_REG;
-  else if (reg && live_max <= (int64_t)CDR_REG2_NA) c.flags |= CDR_CAP_REG2;
+        lv_max[2] <= CDR_REG_NX && lv_max[3] <= CDR_REG_NX && sa_keys.size() <= CDR_REG_NSA;
+  // the 12-activity variant also keeps more reset points (CDR_REG2_NRP): histories with more
+  // distinct checksums than CDR_REG_NRP go there rather than to the wave kernel
+  if (reg && live_max <= (int64_t)CDR_REG_NA && rp_cks.size() <= CDR_REG_NRP) c.flags |= CDR_CAP_REG;
+  else if (reg && live_max <= (int64_t)CDR_REG2_NA && rp_cks.size() <= CDR_REG2_NRP) c.flags |= CDR_CAP_REG2;
   if ((c.flags & CDR_CAP_REG) && live_max <= (int64_t)CDR_REG0_NA && lv_max[0] <= CDR_REG0_NT &&
       lv_max[1] <= CDR_REG0_NX && lv_max[2] <= CDR_REG0_NX && lv_max[3] <= CDR_REG0_NX)
     c.flags |= CDR_CAP_REG0;

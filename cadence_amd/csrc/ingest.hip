@@ -1138,7 +1138,7 @@ extern "C" int cdr_ingest_decode(cdr_ctx* ctx, const cdr_ingest_in* in, cdr_inge
 // cdr_plan_caps restated per entry on the device (host.cpp caps_one / task_caps): the
 // live sets of the wave kernel's lane tables tracked up to CDR_WAVE_SLOTS + 1 keys (one
 // past any bound a flag tests), the reset-point checksum and search-attribute key lists
-// of the register-table envelope up to CDR_REG_NRP / CDR_REG_NSA + 1.
+// of the register-table envelope up to CDR_REG2_NRP / CDR_REG_NSA + 1.
 #include "pack_event.h"
 
 namespace {
@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(64) void k_caps(const cdr_event* events, const uint
   bool reg = n > 0 && n < (1u << 20);
   int64_t last_id = 0;
   uint64_t call_start = 0;
-  Live<CDR_REG_NRP + 1> rp_cks;
+  Live<CDR_REG2_NRP + 1> rp_cks;
   Live<CDR_REG_NSA + 1> sa_keys;
   uint32_t x = 0, t = 0;  // task bounds
   uint64_t aw = 0;
@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(64) void k_caps(const cdr_event* events, const uint
     last_id = e.event_id;
     if (type == CDR_EV_WF_STARTED) {  // a second Started resets the row lists
       const cdr_attr_wf_started& a = e.a.started;
-      rp_cks = Live<CDR_REG_NRP + 1>();
+      rp_cks = Live<CDR_REG2_NRP + 1>();
       sa_keys = Live<CDR_REG_NSA + 1>();
       if (a.flags & CDR_SF_HAS_RESET_POINTS)
         for (uint32_t q = 0; q < a.reset_points_len; q++) {
@@ -1301,10 +1301,9 @@ __global__ __launch_bounds__(64) void k_caps(const cdr_event* events, const uint
       lv1.max + lv2.max + lv3.max <= CDR_LANE_MAX_EXT && n <= CDR_LANE_MAX_LEN)
     c.flags |= CDR_CAP_LANE;
   reg = reg && !(c.flags & CDR_CAP_FAST) && lv0.max <= CDR_REG_NT && lv1.max <= CDR_REG_NX &&
-        lv2.max <= CDR_REG_NX && lv3.max <= CDR_REG_NX && rp_cks.size() <= CDR_REG_NRP &&
-        sa_keys.size() <= CDR_REG_NSA;
-  if (reg && live_max <= (int64_t)CDR_REG_NA) c.flags |= CDR_CAP_REG;
-  else if (reg && live_max <= (int64_t)CDR_REG2_NA) c.flags |= CDR_CAP_REG2;
+        lv2.max <= CDR_REG_NX && lv3.max <= CDR_REG_NX && sa_keys.size() <= CDR_REG_NSA;
+  if (reg && live_max <= (int64_t)CDR_REG_NA && rp_cks.size() <= CDR_REG_NRP) c.flags |= CDR_CAP_REG;
+  else if (reg && live_max <= (int64_t)CDR_REG2_NA && rp_cks.size() <= CDR_REG2_NRP) c.flags |= CDR_CAP_REG2;
   if ((c.flags & CDR_CAP_REG) && live_max <= (int64_t)CDR_REG0_NA && lv0.max <= CDR_REG0_NT &&
       lv1.max <= CDR_REG0_NX && lv2.max <= CDR_REG0_NX && lv3.max <= CDR_REG0_NX)
     c.flags |= CDR_CAP_REG0;

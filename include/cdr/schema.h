@@ -610,6 +610,9 @@ typedef struct cdr_wf_caps {
  * histories, C4/C5 tails): the kernel's second variant, at lower occupancy */
 #define CDR_CAP_REG2 0x10u
 #define CDR_REG2_NA 12u
+#define CDR_REG2_NRP 12u /* ... and up to 12 reset points (Started's rolled-over ones + new checksums) */
+/* the reset-point capacity of the register-table variant with na activity slots */
+#define CDR_REG_NRP_OF(na) ((na) >= CDR_REG2_NA ? CDR_REG2_NRP : CDR_REG_NRP)
 /* the envelope's small corner (at most CDR_REG0_NA live activities, CDR_REG0_NT live user
  * timers, CDR_REG0_NX live children / request-cancels / signals each): the variant whose
  * tables leave room for 3 waves per SIMD (168 VGPRs); such entries carry CDR_CAP_REG too */

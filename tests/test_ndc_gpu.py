@@ -182,3 +182,36 @@ def test_in_memory_carry_gpu(engine_gpu):
         got = engine_gpu.replay(suf)
         bad = engine.compare(suf, got, outs[mem])
         assert not bad, (mem, bad[:5])
+
+
+def test_forked_config5_1m_digests_gpu(engine_gpu):
+    """The device-resident replication run at full size (1M forked config-5 workflows: base
+    branch + two rounds, cdr_ndc_replicate_async) against oracle.ndc_replicate: every
+    workflow's final persisted state by entry digest (k_digest / digest_ref.cpp), every
+    round's decision and the current branch's VersionHistory (bench.py --ndc-forks times the
+    same run, profiles/r3_ndc/bench_ndc_forks_1m.json)."""
+    import oracle
+    n = 1_000_000
+    base, rebuild, forks = ndc.synth_forked(5, n, 0x5EED0C05)
+    rep = ndc.DeviceReplicator(engine_gpu, base, rebuild, forks)
+    try:
+        _, g_vhs, g_pool, g_decs, _ = rep.run()
+        per_d = rep.dev.alloc(n * 8)
+        tot_d = rep.dev.alloc(8)
+        rc = abi.lib().cdr_entry_digests_async(engine_gpu.ctx, C.byref(rep.base_db), C.byref(rep.state),
+                                               C.c_void_p(per_d), C.c_void_p(tot_d), None)
+        assert rc == 0
+        got_c = (C.c_uint64 * n)()
+        rep.dev.down(got_c, per_d, n * 8)
+        got = np.frombuffer(got_c, np.uint64).copy()
+    finally:
+        rep.close()
+    r_state, r_vhs, r_pool, r_decs, _ = oracle.ndc_replicate(base, rebuild, forks, threads=16)
+    want, _ = oracle.entry_digests(base, ndc.state_caps_for(base, rebuild, forks), r_state, threads=16)
+    assert engine.status_histogram(r_state).get("OK", 0) >= n - 16  # a few forks the generator makes unrelatable
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, bad[:10]
+    for k in range(len(forks)):
+        assert all(bytes(g_decs[k][w]) == bytes(r_decs[k][w]) for w in range(n)), k
+    assert all(ndc.branch_items(g_vhs, g_pool, w, g_vhs[w].current) ==
+               ndc.branch_items(r_vhs, r_pool, w, r_vhs[w].current) for w in range(n))
