@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <queue>
 #include <system_error>
 #include <thread>
 #include <vector>
@@ -517,6 +518,34 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     return e ? (uint32_t)std::strtoul(e, nullptr, 0) : (uint32_t)CDR_PAR_SOLO;
   }();
   const uint32_t solo = std::min<uint32_t>(solo_max, (uint32_t)pars.size());
+  // balanced PAR slices: a PAR slice's roles each walk its histories one at a time, so the
+  // slice's time follows the summed lengths of its histories, and the kernel ends with its
+  // heaviest slice (longest-first runs of 16 put the 16 longest histories in slice 0).
+  // Longest-processing-time-first over the non-solo slices: each history (longest first)
+  // joins the lightest slice with room; pars is then laid out slice by slice, UINT32_MAX
+  // filling short slices
+  static const bool par_lpt = [] {
+    const char* e = std::getenv("CDR_PAR_PACK");  // A/B knob: "sorted" = the round-3 runs of 16
+    return !(e && std::strcmp(e, "sorted") == 0);
+  }();
+  if (par_lpt && pars.size() > solo + CDR_PAR_LANES) {
+    const uint32_t nb = (uint32_t)((pars.size() - solo + CDR_PAR_LANES - 1) / CDR_PAR_LANES);
+    std::vector<std::vector<uint32_t>> bins(nb);
+    typedef std::pair<uint64_t, uint32_t> Load;  // (summed events, bin)
+    std::priority_queue<Load, std::vector<Load>, std::greater<Load>> light;
+    for (uint32_t b = 0; b < nb; b++) light.push(Load(0, b));
+    for (size_t i = solo; i < pars.size(); i++) {
+      const Load l = light.top();
+      light.pop();
+      bins[l.second].push_back(pars[i]);
+      if (bins[l.second].size() < CDR_PAR_LANES) light.push(Load(l.first + wfs[pars[i]].ev_len, l.second));
+    }
+    pars.resize(solo);
+    for (uint32_t b = 0; b < nb; b++) {
+      pars.insert(pars.end(), bins[b].begin(), bins[b].end());
+      pars.resize(solo + (size_t)(b + 1) * CDR_PAR_LANES, UINT32_MAX);
+    }
+  }
   // PAR slice s takes pars[par_at(s) ...] (solo slices first, then CDR_PAR_LANES per slice)
   auto par_at = [&](uint32_t s) -> size_t { return s < solo ? s : solo + (size_t)(s - solo) * CDR_PAR_LANES; };
   const uint32_t np = solo + (uint32_t)((pars.size() - solo + CDR_PAR_LANES - 1) / CDR_PAR_LANES);

@@ -289,8 +289,9 @@ def _plan(b, pl, mode):
 
 def test_par_slices_plan():
     """CDR_PLAN_PAR: the long register-table histories the long-history rule would give wave
-    slices become the FIRST slices, CDR_PAR_LANES (16) to a slice, longest first, flagged
-    CDR_SLICE_PAR; the scratch planner keeps the flag (register-table lanes); the class
+    slices become the FIRST slices, CDR_PAR_LANES (16) to a slice, flagged CDR_SLICE_PAR, and
+    balanced: longest-first into the lightest slice, so the summed lengths of any two slices
+    differ by at most one history's length; the scratch planner keeps the flag (register-table lanes); the class
     ranges leave them out (they are launched as slices 0 .. n_par - 1)."""
     b = engine.synth_batch(4, 3000, seed=13)
     pl = engine.plan(b)
@@ -304,7 +305,12 @@ def test_par_slices_plan():
     ws = [int(x) for s in par for x in lp[s] if x >= 0]
     assert len(ws) == n_long and all((lp[s][16:] == -1).all() for s in par)
     lens = [int(b.wfs[w].ev_len) for w in ws]
-    assert lens == sorted(lens, reverse=True)
+    for s in par:  # lanes filled from 0
+        k = int((lp[s] >= 0).sum())
+        assert (lp[s][:k] >= 0).all()
+    sums = [sum(int(b.wfs[w].ev_len) for w in lp[s] if w >= 0) for s in par]
+    if len(par) > 1:
+        assert max(sums) - min(sums) <= max(lens)
     assert all(pl.caps[w].flags & (abi.CAP_REG | abi.CAP_REG2) for w in ws)
     assert all(int(slen[s]) == max(int(b.wfs[w].ev_len) for w in lp[s] if w >= 0) for s in par)
     assert sorted(int(x) for x in lp.ravel() if x >= 0) == list(range(b.n_wfs))  # every entry once

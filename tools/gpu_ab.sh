@@ -1,17 +1,15 @@
 #!/bin/bash
-# parity + smoke + A/B of variant libraries + PMC passes of the main library
-# usage: tools/gpu_ab.sh <tag> <variant.so>...   (env PERF_ARGS: extra tools/perf.py args)
+# interleaved A/B of an env setting: ROUNDS passes over SETTINGS (each "VAR=val[,VAR=val]"),
+# one perf.py process per (pass, setting), so box drift hits every setting alike
 set -o pipefail
-tag=${1:-ab}; shift
-mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py tests/test_golden.py -q -x --timeout 120 \
-    --timeout-method thread > gpurun_out/${tag}_parity.log 2>&1 &&
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 &&
-timeout -k 10 300 python -u tools/perf.py $PERF_ARGS cadence_amd/libcdr.so "$@" > gpurun_out/${tag}_perf.log 2>&1 &&
-bash tools/pmc.sh ${tag}
-rc=$?
-echo "EXIT $rc"
-tail -2 gpurun_out/${tag}_parity.log
-tail -1 gpurun_out/${tag}_smoke.log 2>/dev/null
-grep -v "amdgpu.ids" gpurun_out/${tag}_perf.log 2>/dev/null | tail -6
-exit $rc
+out=gpurun_out/${1:-ab}; mkdir -p $out
+export TMPDIR=/tmp
+for c in ${CONFIGS:-4 5}; do
+  for r in $(seq ${ROUNDS:-3}); do
+    for s in ${SETTINGS:?}; do
+      tag=c${c}_r${r}_${s//[=,]/_}
+      env ${s//,/ } timeout -k 10 200 python3 -u tools/perf.py --config $c --rounds 2 --reps 5 cadence_amd/libcdr.so > $out/$tag.log 2>&1 || { tail -5 $out/$tag.log; exit 1; }
+      echo "C$c r$r $s $(grep median_ms $out/$tag.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["median_ms"], d["checksum"])')"
+    done
+  done
+done
