@@ -15,7 +15,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from cadence_amd import abi, engine, ingest  # noqa: E402
+from cadence_amd import abi, engine, ingest, ndc  # noqa: E402
 
 
 def main():
@@ -77,6 +77,22 @@ def main():
         if rep:  # the first round grows the workspace
             dec_t.append(t1 - t0)
             plan_t.append(t3 - t2)
+    # end to end: the planned device batch replayed (decode + plan + pack + replay); the
+    # output buffers are allocated once (sized by the plan's totals), outside the timing
+    dev = ndc._Dev()
+    o = ndc.alloc_out(dev, b.n_wfs, tot)
+    rep_t = []
+    for rep in range(args.reps + 1):
+        assert hip.hipDeviceSynchronize() == 0
+        t0 = time.perf_counter()
+        assert L.cdr_replay_sliced_async(eng.ctx, C.byref(db), C.byref(o), None) == 0
+        assert hip.hipDeviceSynchronize() == 0
+        if rep:
+            rep_t.append(time.perf_counter() - t0)
+    res = (abi.CdrWfResult * b.n_wfs)()
+    dev.down(res, o.result)
+    n_ok = int(sum(1 for w in range(b.n_wfs) if res[w].code == 0))
+    dev.close()
     # the host path on the same batch: cdr_plan_caps + slices + cdr_pack_slices (+ H2D of the slab)
     t0 = time.perf_counter()
     pl = engine.plan(b)
@@ -102,15 +118,18 @@ def main():
     host_h2d_s = time.perf_counter() - t0
     for p in ptrs:
         hip.hipFree(p)
-    dec_s, plan_s = float(np.median(dec_t)), float(np.median(plan_t))
+    dec_s, plan_s, rep_s = float(np.median(dec_t)), float(np.median(plan_t)), float(np.median(rep_t))
     print(json.dumps({
         "config": args.config, "workflows": args.wfs, "events": n_ev, "blobs": int(inp.n_blobs),
         "blob_bytes": int(enc.blob_bytes.nbytes), "blob_h2d_s": h2d_s,
         "device_decode_s": dec_s, "device_plan_pack_s": plan_s,
         "device_events_per_s": n_ev / (dec_s + plan_s), "decode_gbs": enc.blob_bytes.nbytes / dec_s / 1e9,
+        "device_replay_s": rep_s, "device_e2e_events_per_s": n_ev / (dec_s + plan_s + rep_s),
+        "replay_ok_workflows": n_ok,
         "host_plan_pack_s": host_pack_s, "host_slab_h2d_s": host_h2d_s,
         "host_events_per_s": n_ev / (host_pack_s + host_h2d_s),
         "note": "device: blobs resident in HBM, decode + caps/plan/pack timed wall-clock incl. its host syncs; "
+                "e2e adds the replay of the planned batch (cdr_replay_sliced_async, wall-clock); "
                 "host: cdr_plan_caps + cdr_plan_slices_ex + cdr_pack_slices(16 threads) + slab H2D from cdr_event records"}))
 
 
