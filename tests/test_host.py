@@ -371,3 +371,42 @@ def test_register_lanes_ordered_by_entity_counts():
             assert key(a) >= key(c), (a, c, key(a), key(c))
             pairs += 1
     assert pairs > 100
+
+
+def test_lane_order_restated():
+    """Lane slices without wave/PAR routing (plan mode 0): entries in kernel-group order
+    (fast, 3-, 6-, 12-activity register tables, general), within a group by length class
+    (16 per octave, descending), then — register-table groups — scheduled activities, started
+    timers and initiated externals, then working-slot footprint and length (all descending),
+    stable; each group starts a fresh slice (host.cpp cdr_plan_slices_ex)."""
+    import math
+    for cfg in (2, 3, 4, 5):
+        b = engine.synth_batch(cfg, 3000, seed=17 + cfg)
+        pl = engine.plan(b)
+        lane, slen, _, _ = _plan(b, pl, 0)
+        caps = np.ctypeslib.as_array(pl.caps)
+        lens = np.ctypeslib.as_array(b.wfs)["ev_len"].astype(np.int64)
+
+        def group(w):
+            f = int(caps["flags"][w])
+            return (0 if f & abi.CAP_FAST else 1 if f & abi.CAP_REG0 else 2 if f & abi.CAP_REG else
+                    3 if f & abi.CAP_REG2 else 4)
+
+        def key(w):
+            g = group(w)
+            counts = 1 <= g <= 3
+            ext = int(caps["child_cap"][w] + caps["cancel_cap"][w] + caps["signal_cap"][w])
+            slots = int(caps["act_live"][w]) * 12 + int(caps["timer_live"][w]) * 4  # CDR_ACT/TIM_PLANES
+            return (g, -int(math.log2(lens[w] + 1.0) * 16.0), -int(caps["act_cap"][w]) if counts else 0,
+                    -int(caps["timer_cap"][w]) if counts else 0, -ext if counts else 0, -slots, -int(lens[w]))
+        order = sorted(range(b.n_wfs), key=key)  # Python's sort is stable
+        expect = []
+        for i, w in enumerate(order):
+            if i and group(w) != group(order[i - 1]):
+                expect += [-1] * (-len(expect) % 64)
+            expect.append(w)
+        expect += [-1] * (-len(expect) % 64)
+        assert lane.ravel().tolist() == expect, cfg
+        exp_len = [max([int(lens[w]) for w in expect[s:s + 64] if w >= 0], default=0)
+                   for s in range(0, len(expect), 64)]
+        assert slen.tolist() == exp_len
