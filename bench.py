@@ -352,11 +352,19 @@ def ndc_forks_line(args):
     state, vhs, pool, decs, rounds = rep.run()  # warm-up (and the decisions the events count from)
     ev_base = rep.events[0]
     lens_rb = np.array([rebuild.wfs[w].ev_len for w in range(n)], np.int64)
-    ev_rounds = []
+    # events a round replays: the rebuilt branch of every workflow whose rebuild ran and
+    # succeeded, and the task's events of every workflow whose apply ran and succeeded (a
+    # SKIP / BACKFILL decision, a failed branch step or rebuild leaves the apply record
+    # CDR_NOT_RUN or failed: none of its events is counted)
+    def codes(out):
+        return np.frombuffer(out.result, dtype=np.int32).reshape(-1, C.sizeof(abi.CdrWfResult) // 4)[:n, 0]
+    ev_rounds, acts = [], {}
     for k, (fb, _, _) in enumerate(forks):
-        act = np.array([decs[k][w].action for w in range(n)], np.int32)
+        rb_out, ap_out = rounds[k]
         lens_fb = np.array([fb.wfs[w].ev_len for w in range(n)], np.int64)
-        ev_rounds.append(int(lens_fb[act != 0].sum() + lens_rb[act == 2].sum()))
+        ev_rounds.append(int(lens_fb[codes(ap_out) == abi.OK].sum() + lens_rb[codes(rb_out) == abi.OK].sum()))
+        acts[f"round{k}"] = {abi.NDC_ACTIONS[a]: int(c) for a, c in
+                             zip(*np.unique([decs[k][w].action for w in range(n)], return_counts=True))}
     events = ev_base + sum(ev_rounds)
     for _ in range(args.warmup):
         rep.reset()
@@ -394,8 +402,6 @@ def ndc_forks_line(args):
                             "branch's VersionHistory, GPU vs oracle.ndc_replicate"}
         log(f"NDC parity: {parity['mismatched_entries']} states, {bad_dec} decisions, {vb} VHs differ "
             f"({parity['seconds']:.1f}s)")
-    acts = {abi.NDC_ACTIONS[a]: int(c) for k in range(len(forks))
-            for a, c in zip(*np.unique([decs[k][w].action for w in range(n)], return_counts=True))}
     # algorithmic bytes per step: every replayed event's slab element (60 B, cdr.h row layout)
     # + the per-workflow records each replay writes (264 B), base + 2 rounds x
     # (rebuild + apply)
@@ -448,6 +454,10 @@ def main():
                     help="configs[4]'s conflict-resolution line: the forked config-5 population replicated on "
                          "the device (base branch + 2 fork rounds per step); --wfs workflows")
     args = ap.parse_args()
+    import torch  # before libcdr.so: torch's HIP runtime must be the process's one (tests/conftest.py)
+    L = abi.lib()
+    if L.cdr_build_flags():  # a profiling / tuning variant never reaches a reported line
+        raise SystemExit(f"libcdr.so is a variant build (cdr_build_flags = {L.cdr_build_flags():#x}); rebuild it")
     if args.ndc_forks:
         return ndc_forks_line(args)
 
@@ -460,9 +470,6 @@ def main():
     else:
         dist = None
         torch.cuda.set_device(0)
-    L = abi.lib()
-    if L.cdr_build_flags():  # a profiling / tuning variant never reaches a reported line
-        raise SystemExit(f"libcdr.so is a variant build (cdr_build_flags = {L.cdr_build_flags():#x}); rebuild it")
     ctx = L.cdr_create(torch.cuda.current_device(), None)
     if not ctx:
         raise SystemExit("cdr_create failed (no GPU?) — the engine has no CPU fallback")

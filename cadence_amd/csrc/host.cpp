@@ -66,7 +66,7 @@ namespace cdr_internal {
 uint32_t arena_words_for(uint32_t type) { return cdr_arena_words_for(type); }
 
 void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* out, const cdr_kv* kvs,
-              const cdr_reset_point* rps) {
+              const cdr_reset_point* rps, const uint32_t* loaded) {
   cdr_wf_caps c{};
   bool fast = builder != CDR_BUILDER_2DC && n > 0 && ev[0].type == CDR_EV_WF_STARTED;
   bool have_ver = false;
@@ -92,6 +92,13 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
     auto it = std::find(lv[t].begin(), lv[t].end(), key);
     if (it != lv[t].end()) lv[t].erase(it);
   };
+  if (loaded) {  // a loaded state's rows: keys no event of the history names (never removed)
+    live = live_max = loaded[0];
+    for (int t = 0; t < 4; t++)
+      for (uint32_t i = 0; i < loaded[1 + t]; i++) lv_add(t, INT64_MIN + i, false);
+    for (uint32_t i = 0; i < loaded[5]; i++) rp_cks.push_back(0xFFFFFFFFu - i);
+    for (uint32_t i = 0; i < loaded[6]; i++) sa_keys.push_back(0xFFFFFFFFu - i);
+  }
   for (uint64_t k = 0; k < n; k++) {
     const cdr_event& e = ev[k];
     if (k == 0 || (e.flags & CDR_EVF_BATCH_FIRST)) call_start = k;
@@ -326,15 +333,19 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
       }
     }
     cdr_wf_caps c{};
-    cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c, b->kvs, b->rps);
-    if (b->carry && b->carry->src && b->carry->src[w] >= 0) {
-      // a loaded state (cdr_carry): its rows are live from the start; only the
-      // general kernel replays onto a loaded state
+    const bool carried = b->carry && b->carry->src && b->carry->src[w] >= 0;
+    if (carried) {
+      // a loaded state (cdr_carry): its rows are live from the start (the peak live sets
+      // and the register-table envelope count them); the fast and wave kernels take no
+      // loaded state, the register-table kernels' carry-in instantiations do
       const cdr_carry& cy = *b->carry;
       const uint32_t src = (uint32_t)cy.src[w];
       if (src >= cy.n_src || d.parent >= 0 || !cy.state.result) return CDR_API_EINVAL;
       const cdr_wf_result& r = cy.state.result[src];
       if (r.code != CDR_OK) return CDR_API_EINVAL;
+      const uint32_t loaded[7] = {r.n_activity, r.n_timer, r.n_child, r.n_cancel, r.n_signal, r.n_reset_points,
+                                  r.n_search_attr};
+      cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c, b->kvs, b->rps, loaded);
       c.act_cap += r.n_activity;
       c.timer_cap += r.n_timer;
       c.child_cap += r.n_child;
@@ -343,9 +354,9 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
       c.vh_cap += r.n_vh;
       c.rp_cap += r.n_reset_points;
       c.sa_cap += r.n_search_attr;
-      c.act_live += r.n_activity;
-      c.timer_live += r.n_timer;
-      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_REG | CDR_CAP_REG2 | CDR_CAP_REG0);
+      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_LANE);
+    } else {
+      cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c, b->kvs, b->rps);
     }
     if (bound) {  // the loaded rows' bound: the state's capacities
       if (d.parent >= 0 || d.newrun >= 0) return CDR_API_EINVAL;  // one run per entry
@@ -363,7 +374,18 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
       // ever added): the general kernel sizes its working slots by these
       c.act_live += s.act_live;
       c.timer_live += s.timer_live;
-      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_REG | CDR_CAP_REG2 | CDR_CAP_REG0);
+      // the loaded rows are not known here: the register-table envelope is the history's
+      // own, and an entry goes to the 12-activity variant (a loaded state plus the history's
+      // own rows outgrow the 6-activity tables for ~1 entry in 4 on the forked C5 population,
+      // and a slice runs as its largest lane needs); an entry whose loaded state outgrows even
+      // that is handed on to the general kernel (replay_reg.inc).  CDR_CARRY_REG2=0 keeps the
+      // history's own variant and relies on the hand-on chain (C5 forks 1M: 53.6 vs 48.5 ms)
+      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_LANE | CDR_CAP_REG0);
+      static const int all12 = [] {
+        const char* e = std::getenv("CDR_CARRY_REG2");
+        return e ? std::atoi(e) : 1;
+      }();
+      if (all12 && (c.flags & CDR_CAP_REG)) c.flags = (c.flags & ~CDR_CAP_REG) | CDR_CAP_REG2;
     }
     cdr_internal::task_caps(b->events + d.ev_off, d.ev_len, &c.xfer_cap, &c.ttask_cap);
     c.xfer_off = t.xfer;

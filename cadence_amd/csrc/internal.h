@@ -11,8 +11,12 @@ uint32_t arena_words_for(uint32_t type);
 
 // Output capacities of one history (cdr_plan_caps restricted to one workflow);
 // offsets are left zero.
+// `loaded` (nullable): the live rows a loaded state (cdr_carry) starts with — activities,
+// user timers, children, request-cancels, signals, reset points, search-attribute keys —
+// counted into the peak live sets and the register-table envelope as rows the history never
+// removes (an upper bound).
 void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* c, const cdr_kv* kvs = nullptr,
-              const cdr_reset_point* rps = nullptr);
+              const cdr_reset_point* rps = nullptr, const uint32_t* loaded = nullptr);
 
 // Pack one workflow's events into lane `lane` of a slice whose first row is row0 and
 // whose length is len (rows beyond n are padding).  `apos` is the workflow's arena

@@ -376,6 +376,9 @@ int cdr_ndc_replicate_async(cdr_ctx* ctx, uint32_t n, const cdr_ndc_round* R, cd
   if (n > R->rebuild.n_wfs || n > R->apply.n_wfs || R->apply.carry || !R->rebuild_out.transfer ||
       !R->rebuild_out.timer_tasks || !R->rebuild_out.n_tasks)
     return CDR_API_EINVAL;
+  // every apply entry replays onto a loaded state: only the general and the register-table
+  // kernels take one (cdr_plan_ndc_apply never plans fast or wave slices)
+  if (R->apply.n_fast_slices || R->apply.n_wave_slices) return CDR_API_EINVAL;
   if (n == 0) return CDR_API_OK;
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipSetDevice(cdr_ctx_device(ctx)));
@@ -392,11 +395,8 @@ int cdr_ndc_replicate_async(cdr_ctx* ctx, uint32_t n, const cdr_ndc_round* R, cd
   hipLaunchKernelGGL(k_ndc_round_begin, g, b, 0, st, n, R->dec, *state, R->rebuild_out, R->apply_out, skip_rb, src);
   HIPCHK(hipGetLastError());
   // 2. nDCStateRebuilder.rebuild of the REBUILD workflows, refreshTasks, verification
-  cdr_dev_batch rb = R->rebuild;
+  cdr_dev_batch rb = R->rebuild;  // its class-sorted blocks, if any, go to k_replay_cls (skip-aware)
   rb.skip = skip_rb;
-  rb.cls_slab = nullptr;
-  rb.cls_row0 = nullptr;
-  rb.cls_rows = nullptr;
   cdr_out rbo = R->rebuild_out;
   rbo.transfer = rbo.timer_tasks = nullptr;  // the replay emits no stateBuilder tasks here
   rbo.n_tasks = nullptr;

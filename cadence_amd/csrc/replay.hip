@@ -497,9 +497,17 @@ struct cdr_launch {
   // retry pass of k_replay_reg walks that list (null: every slice of its range)
   uint32_t* rlist;
   uint32_t* rcount;
+  // carry-in launches: the list k_replay_reg appends the slices it hands on to (the next
+  // tier's rlist)
+  uint32_t* olist;
+  uint32_t* ocount;
 };
-// result code k_replay_cls leaves on an entry it hands to k_replay_reg (never returned)
+// result code k_replay_cls (or a carry-in k_replay_reg below the 12-activity variant) leaves
+// on an entry it hands to k_replay_reg (never returned)
 #define CLS_RETRY 0x7FFF
+// result code the carry-in 12-activity k_replay_reg leaves on an entry it hands to the
+// general kernel's retry pass (never returned)
+#define CLS_RETRY2 0x7FFE
 // result flag k_replay_cls sets when its pending rows are already dense and in key
 // order (k_tables skips their sort and clears it; never returned)
 #define RF_ROWS_SORTED 0x80000000u
@@ -529,7 +537,11 @@ template <bool LDS, bool TASKS>
 __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu(CDR_WPE, 8))) void k_replay(
     cdr_launch L) {
   (void)L;  // read through KA()
-  const uint32_t s = blockIdx.x + KA()->s0;
+  // retry: the slices a carry-in k_replay_reg listed (block b: list entry b), their
+  // CLS_RETRY2 entries only
+  const bool retry = KA()->retry != 0u;
+  if (retry && blockIdx.x >= __builtin_amdgcn_readfirstlane(*KA()->rcount)) return;
+  const uint32_t s = retry ? __builtin_amdgcn_readfirstlane(KA()->rlist[blockIdx.x]) : blockIdx.x + KA()->s0;
   const uint32_t lane = threadIdx.x;
   if (s >= KA()->B.ev.n_slices) return;
   // slice scalars (readfirstlane makes their uniformity visible, so the descriptor
@@ -538,7 +550,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   const uint32_t tim_cap = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_tim_slots[s]);
   const uint32_t la = KA()->la, lt = KA()->lt;
   if ((act_cap <= la && tim_cap <= lt) != LDS) return;
-  {
+  if (!retry) {
     const uint32_t sf = __builtin_amdgcn_readfirstlane(KA()->B.ev.slice_flags[s]);
     if (sf & CDR_SLICE_WAVE) return;  // k_replay_wave
     if (KA()->fast && (sf & CDR_SLICE_FAST)) return;
@@ -554,6 +566,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   S.l4 = lane * 4u;
   const int32_t w = KA()->B.ev.lane_wf[(uint64_t)s * CDR_SLICE_WIDTH + lane];
   if (w < 0 || (KA()->B.skip && KA()->B.skip[w])) return;  // empty lane / masked entry
+  if (retry && gp(KA()->O.result)[w].code != CLS_RETRY2) return;
 
   // per-workflow descriptor, capacities and output records, re-read where used
 #define B_ (KA()->B)
@@ -1959,8 +1972,11 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const bool reg = c->fast && c->reg &&
                    in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices + in->n_par_slices > 0 && !tasks &&
                    in->cluster.n_clusters <= (int)CDR_REG_NCL;
+  // carry-in batches (cdr_dev_batch.carry): the register-table slices replay in the carry-in
+  // instantiations of k_replay_reg, each class followed by its hand-on chain (below)
+  const bool carry = in->carry != nullptr;
   // class-decomposed replay of the register-table slices (their class-sorted blocks)
-  const bool cls = reg && c->cls && in->cls_slab && in->cls_row0 && in->cls_rows && !in->skip;
+  const bool cls = reg && !carry && c->cls && in->cls_slab && in->cls_row0 && in->cls_rows;
   const bool cls_fb = c->cls != 2;  // 2 (tests): no k_replay_reg pass for the CLS_RETRY entries
   auto retry_of = [](cdr_launch x) {
     x.retry = 1u;
@@ -1978,9 +1994,11 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
   cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u, 0u, 0u, nullptr, nullptr};
   // retry lists (k_replay_cls -> k_replay_reg): counters zeroed on the launch stream
+  // (carry-in: a second level of lists, k_replay_reg<12-activity> -> the general kernel,
+  // counters 8 + class)
   uint32_t* rws = nullptr;
-  if (cls && cls_fb) {
-    rws = (uint32_t*)cdr_ws_get(c, WS_RETRY, (16ull + (uint64_t)cdr_ctx::N_SIDE * blocks) * 4ull);
+  if ((cls && cls_fb) || (carry && reg)) {
+    rws = (uint32_t*)cdr_ws_get(c, WS_RETRY, (16ull + 2ull * cdr_ctx::N_SIDE * blocks) * 4ull);
     if (!rws) return CDR_API_ENOMEM;
     HIPCHK(hipMemsetAsync(rws, 0, 16 * 4, st));
   }
@@ -1990,6 +2008,34 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       x.rlist = rws + 16 + (uint64_t)cls_id * blocks;
     }
     return x;
+  };
+  // carry-in hand-on lists of class cls_id: level 1 (-> the 12-activity variant), level 2
+  // (-> the general kernel)
+  auto out_list = [&](cdr_launch x, int cls_id, int level) {
+    x.ocount = rws + (level == 1 ? 0 : 8) + cls_id;
+    x.olist = rws + 16 + (uint64_t)((level == 1 ? 0 : cdr_ctx::N_SIDE) + cls_id) * blocks;
+    return x;
+  };
+  auto in_list = [&](int cls_id, int level) {
+    cdr_launch x = L;
+    x.retry = 1u;
+    x.rcount = rws + (level == 1 ? 0 : 8) + cls_id;
+    x.rlist = rws + 16 + (uint64_t)((level == 1 ? 0 : cdr_ctx::N_SIDE) + cls_id) * blocks;
+    return x;
+  };
+  // after a carry-in register-table launch of class cls_id over grid g on stream sq: the
+  // 12-activity variant over its level-1 list (below12: the class's tables are smaller),
+  // then the general kernel over the level-2 list
+  auto carry_tail = [&](int cls_id, dim3 g, hipStream_t sq, bool below12) {
+    if (below12) {
+      typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
+      // a whole grid: unlike k_replay_cls's few leftovers, a loaded state outgrowing the
+      // smaller tables is common, and this variant runs one wave per SIMD
+      hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_CLS_SLICES, CDR_WPE_REG, true>), g,
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sq, out_list(in_list(cls_id, 1), cls_id, 2));
+    }
+    hipLaunchKernelGGL((k_replay<true, false>), g, dim3(CDR_SLICE_WIDTH), lds, sq, in_list(cls_id, 2));
+    if (spill) hipLaunchKernelGGL((k_replay<false, false>), g, dim3(CDR_SLICE_WIDTH), 0, sq, in_list(cls_id, 2));
   };
   // each kernel over its class's slice range (cdr_plan_class_ranges), or every slice
   bool ranged = false;
@@ -2056,7 +2102,14 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   auto launch_class = [&](int i) {
     switch (i) {
       case 6:
-    if (par) {  // first: the longest critical paths of the batch
+    if (par && carry) {
+      cdr_launch Lp = L;
+      Lp.s0 = 0;
+      typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
+      hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_REG, true>), dim3(npar),
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6), out_list(Lp, 6, 2));
+      carry_tail(6, dim3(npar), sx(6), false);
+    } else if (par) {  // first: the longest critical paths of the batch
       cdr_launch Lp = L;
       Lp.s0 = 0;
       typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
@@ -2075,7 +2128,12 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
     if (wv) hipLaunchKernelGGL(k_replay_wave, gw, dim3(CDR_SLICE_WIDTH), 0, sx(0), Lw);
         break;
       case 1:
-    if (reg2) {
+    if (reg2 && carry) {
+      typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
+      hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_REG, true>), gr2,
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), out_list(Lr2, 1, 2));
+      carry_tail(1, gr2, sx(1), false);
+    } else if (reg2) {
       typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
       if (cls) {
         typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LC;
@@ -2102,7 +2160,12 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
     }
         break;
       case 3:
-    if (reg0) {  // the small-table variant, at 3 waves per SIMD
+    if (reg0 && carry) {
+      typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
+      hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3, true>), gr0,
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), out_list(Lr0, 3, 1));
+      carry_tail(3, gr0, sx(3), true);
+    } else if (reg0) {  // the small-table variant, at 3 waves per SIMD
       typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
       if (cls) {
         typedef ClsLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LC;
@@ -2118,7 +2181,12 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
     if (fst) hipLaunchKernelGGL(k_replay_fast, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), Lf);
         break;
       case 5:
-    if (reg1) {
+    if (reg1 && carry) {
+      typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
+      hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_REG, true>), gr1,
+                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), out_list(Lr1, 5, 1));
+      carry_tail(5, gr1, sx(5), true);
+    } else if (reg1) {
       typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
       if (cls) {
         typedef ClsLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LC;

@@ -136,10 +136,12 @@ def offsets_from_caps(caps, n):
     return tot
 
 
-def upload_batch(dev: _Dev, batch: engine.Batch, caps, mode: int = abi.PLAN_WAVE | abi.PLAN_PAR) -> abi.CdrDevBatch:
+def upload_batch(dev: _Dev, batch: engine.Batch, caps, mode: int = abi.PLAN_WAVE | abi.PLAN_PAR,
+                 cls: bool = False) -> abi.CdrDevBatch:
     """Host planning + packing (cdr_plan_slices_ex / cdr_pack_slices / cdr_plan_scratch)
-    of `batch` with capacities `caps`, uploaded: a device-resident cdr_dev_batch (no
-    class-sorted blocks)."""
+    of `batch` with capacities `caps`, uploaded: a device-resident cdr_dev_batch; `cls`:
+    with the register-table slices' class-sorted blocks from the host packer (cdr_plan_cls /
+    cdr_pack_cls), which k_replay_cls replays."""
     L = abi.lib()
     n = batch.n_wfs
     ns, rows, nw = C.c_uint32(), C.c_uint64(), C.c_uint32()
@@ -172,6 +174,18 @@ def upload_batch(dev: _Dev, batch: engine.Batch, caps, mode: int = abi.PLAN_WAVE
     if rc:
         raise RuntimeError(f"cdr_plan_scratch rc={rc}")
     db = abi.CdrDevBatch()
+    if cls and int(((flags[:ns.value] & abi.CLS_SLICES) != 0).sum()):
+        crows = np.zeros(max(1, ns.value * 4), np.uint32)
+        crow0 = np.zeros(ns.value + 1, np.uint64)
+        rc = L.cdr_plan_cls(C.byref(s), C.cast(batch.wfs, C.c_void_p), crows.ctypes.data, crow0.ctypes.data)
+        if rc:
+            raise RuntimeError(f"cdr_plan_cls rc={rc}")
+        cslab = np.empty(max(8, int(crow0[-1]) * abi.ROW_BYTES), np.uint8)
+        rc = L.cdr_pack_cls(C.byref(s), C.cast(batch.wfs, C.c_void_p), crows.ctypes.data, crow0.ctypes.data,
+                            cslab.ctypes.data, 0)
+        if rc:
+            raise RuntimeError(f"cdr_pack_cls rc={rc}")
+        db.cls_slab, db.cls_row0, db.cls_rows = dev.up(cslab), dev.up(crow0), dev.up(crows)
     db.ev.n_slices, db.ev.n_rows, db.ev.arena_words = ns.value, rows.value, aw
     db.ev.slice_row0, db.ev.slice_len, db.ev.lane_wf = dev.up(row0), dev.up(slen), dev.up(lane)
     db.ev.slab, db.ev.arena = dev.up(slab), dev.up(arena)
@@ -259,11 +273,13 @@ class DeviceReplicator:
         dev = self.dev
         self.state_plan = state_caps_for(base, rebuild, forks)
         live_bound = state_caps_for(base, rebuild, forks, live_sum=True).caps
-        self.base_db = upload_batch(dev, base, self.state_plan.caps)
+        # the base and rebuild replays run the class-decomposed kernel (their class-sorted
+        # blocks come from the host packer, like the rest of the setup)
+        self.base_db = upload_batch(dev, base, self.state_plan.caps, cls=True)
         self.state = alloc_out(dev, n, self.state_plan.totals)
         self.state_caps_d = self.base_db.caps  # the state's capacities (the base batch was planned with them)
         self.rebuild_plan = engine.plan(rebuild)
-        self.rebuild_db = upload_batch(dev, rebuild, self.rebuild_plan.caps)
+        self.rebuild_db = upload_batch(dev, rebuild, self.rebuild_plan.caps, cls=True)
         self.rebuild_out = alloc_out(dev, n, self.rebuild_plan.totals, tasks=True)
         self.rounds = []
         for fb, tasks, items in forks:

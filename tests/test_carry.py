@@ -58,8 +58,10 @@ def test_oracle_split_builders_faults(builder):
 
 
 def test_carry_plan_caps():
-    """Loaded rows count toward the entry's capacities; loaded entries leave the
-    fast/wave kernels (the general kernel replays onto loaded state)."""
+    """Loaded rows count toward the entry's capacities and peak live sets; loaded entries
+    leave the fast / wave kernels (the register-table kernels' carry-in instantiations and
+    the general kernel replay onto a loaded state), and a register-table variant is chosen
+    only when the loaded rows plus the history's own fit its tables."""
     import oracle
     b = engine.synth_batch(3, 64, seed=5)
     pre, cut = engine.split_batch(b, 1)
@@ -76,6 +78,12 @@ def test_carry_plan_caps():
         assert c.vh_cap >= r.n_vh and c.rp_cap >= r.n_reset_points and c.sa_cap >= r.n_search_attr
         assert c.child_cap >= r.n_child and c.signal_cap >= r.n_signal and c.cancel_cap >= r.n_cancel
         assert c.act_cap <= pl0.caps[w].act_cap + r.n_activity
+        if c.flags & abi.CAP_REG0:
+            assert r.n_activity <= 3 and r.n_timer <= 5 and max(r.n_child, r.n_cancel, r.n_signal) <= 3
+        if c.flags & abi.CAP_REG:
+            assert r.n_activity <= 6 and r.n_timer <= 10 and max(r.n_child, r.n_cancel, r.n_signal) <= 4
+            assert r.n_reset_points <= 6 and r.n_search_attr <= 8
+    assert any(pl.caps[w].flags & (abi.CAP_REG | abi.CAP_REG2) for w in range(b.n_wfs) if sb.carry.src[w] >= 0)
 
 
 def test_carry_rejects_failed_state():
@@ -123,5 +131,68 @@ def test_gpu_carry_builders(engine_gpu, builder):
     pre_gpu = engine_gpu.replay(pre)
     sb = engine.suffix_batch(b, cut, pre, pre_gpu)
     got, ref = engine_gpu.replay(sb), oracle.replay(sb)
+    bad = engine.compare(sb, got, ref)
+    assert not bad, "\n".join(bad[:10])
+
+
+def _force_small_tables(sb, pl):
+    """Every carried register-table entry planned onto the 3-activity variant whatever its
+    loaded state: the carry-in kernel hands those that outgrow it on to the 12-activity
+    variant and the general kernel (replay_reg.inc) — the chain the NDC apply relies on."""
+    n = 0
+    for w in range(sb.n_wfs):
+        if sb.carry.src[w] >= 0 and pl.caps[w].flags & (abi.CAP_REG | abi.CAP_REG2):
+            pl.caps[w].flags |= abi.CAP_REG | abi.CAP_REG0
+            n += 1
+    return n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 2, 3, 4, 5])
+def test_gpu_carry_kernel_tiers(engine_gpu, cfg):
+    """Carry-in on each tier, bit-exact against the oracle: the register-table kernels'
+    carry-in instantiations (the default route), the hand-on chain from an undersized
+    variant (3 activity slots) through the 12-activity variant to the general kernel, and
+    the general kernel alone (register kernels off)."""
+    import oracle
+    b = engine.synth_batch(cfg, 400, seed=0x5EED0400 + cfg, error_rate=0.1 if cfg in (0, 3) else 0.0)
+    pre, cut = engine.split_batch(b, cfg + 11)
+    pre_gpu = engine_gpu.replay(pre)
+    sb = engine.suffix_batch(b, cut, pre, pre_gpu)
+    ref = oracle.replay(sb)
+    pl = engine.plan(sb)
+    n_reg = sum(1 for w in range(sb.n_wfs) if sb.carry.src[w] >= 0 and pl.caps[w].flags & (abi.CAP_REG | abi.CAP_REG2))
+    assert n_reg > 0
+    got = engine_gpu.replay(sb, pl)
+    bad = engine.compare(sb, got, ref)
+    assert not bad, "default route:\n" + "\n".join(bad[:10])
+    pl2 = engine.plan(sb)
+    assert _force_small_tables(sb, pl2) > 0
+    got2 = engine_gpu.replay(sb, pl2)
+    bad = engine.compare(sb, got2, ref)
+    assert not bad, "hand-on chain:\n" + "\n".join(bad[:10])
+    old = abi.lib().cdr_set_reg_path(engine_gpu.ctx, 0)
+    try:
+        got3 = engine_gpu.replay(sb)
+    finally:
+        abi.lib().cdr_set_reg_path(engine_gpu.ctx, old)
+    bad = engine.compare(sb, got3, ref)
+    assert not bad, "general kernel:\n" + "\n".join(bad[:10])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("builder", [abi.BUILDER_LOCAL, abi.BUILDER_2DC, abi.BUILDER_NDC])
+def test_gpu_carry_chain_builders(engine_gpu, builder):
+    """The hand-on chain with every builder (2DC: the loaded LastReplicationInfo in the
+    register kernel's LDS planes), faults injected."""
+    import oracle
+    b = engine.synth_batch(3, 300, seed=71 + builder, builder=builder, error_rate=0.15)
+    pre, cut = engine.split_batch(b, builder + 5)
+    pre_gpu = engine_gpu.replay(pre)
+    sb = engine.suffix_batch(b, cut, pre, pre_gpu)
+    ref = oracle.replay(sb)
+    pl = engine.plan(sb)
+    _force_small_tables(sb, pl)
+    got = engine_gpu.replay(sb, pl)
     bad = engine.compare(sb, got, ref)
     assert not bad, "\n".join(bad[:10])
