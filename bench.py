@@ -406,19 +406,24 @@ def ndc_forks_line(args):
     # + the per-workflow records each replay writes (264 B), base + 2 rounds x
     # (rebuild + apply)
     alg = events * 60 + n * 264 * (1 + 2 * len(forks))
+    workload = f"C5-forked-{n}wf-ndc-replicate"
+    traffic, tnote = load_traffic(workload)
     line = {
         "metric": "history events replayed/sec + workflows rebuilt/sec (node), % of HBM roofline",
         "value": events / (ms / 1e3), "unit": "events/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms, "wall_ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int64",
         "data": "synthetic forked config 5 (cadence_amd.ndc.synth_forked)",
-        "config": {"workload": f"C5-forked-{n}wf-ndc-replicate", "workflows_per_gpu": n, "rounds": len(forks),
+        "config": {"workload": workload, "workflows_per_gpu": n, "rounds": len(forks),
                    "events_per_step": events, "events_base": ev_base, "events_rounds": ev_rounds,
                    "decisions": acts, "parallelism": "shard1"},
         "workflows_per_s": n / (ms / 1e3),
         "roofline": {"bound": "hbm", "achieved": alg / (ms / 1e3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": alg / (ms / 1e3) / 1e9 / PEAK_HBM_GBS, "traffic": None,
-                     "traffic_note": "no PMC pass of this line", "algorithmic_bytes_per_step": alg,
+                     "frac": alg / (ms / 1e3) / 1e9 / PEAK_HBM_GBS,
+                     "traffic": traffic["bytes_per_launch"] if traffic else None,
+                     "traffic_note": tnote or (traffic.get("source") + "; per step: every k_* kernel of the "
+                                               "step (the VersionHistories reset copy excluded)"),
+                     "algorithmic_bytes_per_step": alg,
                      "kernel": "k_ndc_branch + k_replay* + k_refresh + k_ndc_verify/apply (one step)"},
         "host": {"setup_s": setup_s},
         "parity": parity, "parity_checked": parity is not None,
@@ -426,6 +431,167 @@ def ndc_forks_line(args):
     beat.set()
     print(json.dumps(line), flush=True)
     rep.close()
+
+
+def carry_line(args):
+    """Carry-in replay at full size (the north star's drop-in for every
+    applyEvents caller, not just rebuild): every history of the config's population is cut at
+    the call boundary nearest after its middle; the first half replays into a state buffer
+    (k_replay_cls, untimed), then a step = the second half replayed onto those LOADED states
+    (cdr_dev_batch.carry: mutableStateBuilder.Load mutableStateBuilder.go:272-295, then
+    applyEvents, nDCHistoryReplicator.go:330-398) through the register-table kernels'
+    carry-in instantiations.  value = suffix events per second.  Parity, entry by entry: the
+    GPU's carried replay against the oracle's carried replay of the oracle's own prefix
+    states, and against the oracle's WHOLE-history replay (split equals whole)."""
+    import torch
+    from cadence_amd import engine, ndc
+    torch.cuda.set_device(0)
+    eng = engine.Engine(0)
+    L = abi.lib()
+    n, cfg = args.wfs, args.config
+    seed = args.seed if args.seed != 0x5EED0002 else 0x5EED0000 + cfg
+    t0 = time.perf_counter()
+    b = engine.synth_batch(cfg, n, seed)
+    n_wf, n = n, b.n_wfs  # entries: a continue-as-new run is an entry of its own (never split)
+    cut = engine.split_half(b)
+    pre, suf = engine.cut_batches(b, cut)
+    log(f"carry: {n} C{cfg} workflows, {int((cut > 0).sum())} split ({time.perf_counter() - t0:.0f}s)")
+    dev = ndc._Dev()
+    stream = torch.cuda.current_stream().cuda_stream
+    # the first halves: replayed once into the state buffer the steps load from
+    pre_pl = engine.plan(pre)
+    pre_db = ndc.upload_batch(dev, pre, pre_pl.caps, cls=True)
+    pre_out = ndc.alloc_out(dev, n, pre_pl.totals)
+    rc = L.cdr_replay_sliced_async(eng.ctx, C.byref(pre_db), C.byref(pre_out), C.c_void_p(stream))
+    if rc:
+        raise RuntimeError(f"prefix replay rc={rc}")
+    torch.cuda.synchronize()
+    # planning reads the loaded states (a host copy: row counts and keys)
+    pre_host = ndc.download_out(dev, pre_out, n, pre_pl)
+    pre_res = pre_host.result
+    codes = np.frombuffer(pre_res, dtype=np.int32).reshape(n, -1)[:, 0]
+    src = np.where((cut > 0) & (codes == abi.OK), np.arange(n), -1).astype(np.int32)
+    suf.carry = engine.Carry(src=src, state=pre_host)
+    spl = engine.plan(suf)
+    caps, tot = spl.caps, spl.totals
+    suf.carry = None
+    suf_db = ndc.upload_batch(dev, suf, caps)
+    dc = abi.CdrCarry()  # the device copy: the loaded states in HBM
+    dc.src, dc.caps, dc.n_src, dc.totals, dc.state = dev.up(src), pre_db.caps, n, pre_pl.totals, pre_out
+    suf_db.carry = dev.up(dc)
+    suf_out = ndc.alloc_out(dev, n, tot)
+    setup_s = time.perf_counter() - t0
+    flags = np.frombuffer(caps, dtype=np.uint32).reshape(n, -1)[:, abi.CdrWfCaps.flags.offset // 4]
+    route = {k: int(((flags & m) != 0)[src >= 0].sum()) for k, m in
+             (("reg0", abi.CAP_REG0), ("reg", abi.CAP_REG), ("reg2", abi.CAP_REG2))}
+    log(f"carry: setup {setup_s:.1f}s, carried entries by variant {route}")
+
+    def step():
+        rc = L.cdr_replay_sliced_async(eng.ctx, C.byref(suf_db), C.byref(suf_out), C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"carry replay rc={rc}")
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    L.cdr_timing_begin(eng.ctx, args.steps)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.steps):
+        step()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    kms = (C.c_float * args.steps)()
+    nk = C.c_uint32(args.steps)
+    L.cdr_timing_read(eng.ctx, kms, C.byref(nk))
+    kern_ms = float(np.mean(kms[:nk.value])) if nk.value else ms
+    # events and algorithmic bytes of a step: the suffix events (48 B + A[type] each), the
+    # loaded records read (ExecutionInfo + rows, the per-row bytes of SURVEY 8(d)) and the
+    # records written
+    from cadence_amd.synth import A_TYPE
+    words = C.sizeof(abi.CdrEvent) // 4
+    ev = np.frombuffer(b.events, dtype=np.uint32).reshape(-1, words)
+    wfa = np.frombuffer(suf.wfs, dtype=np.uint8).reshape(n, -1)
+    o_off, o_len = abi.CdrWfDesc.ev_off.offset, abi.CdrWfDesc.ev_len.offset
+    s_off = wfa[:, o_off:o_off + 8].copy().view(np.int64).ravel()
+    s_len = wfa[:, o_len:o_len + 8].copy().view(np.int64).ravel()
+    mask = np.zeros(len(ev) + 1, np.int64)
+    np.add.at(mask, s_off, 1)
+    np.add.at(mask, s_off + s_len, -1)
+    in_suf = np.cumsum(mask)[:len(ev)] > 0
+    types = ev[in_suf, abi.CdrEvent.type.offset // 4]
+    events = int(in_suf.sum())
+    ev_bytes = int((48 + A_TYPE[np.minimum(types, 41)]).sum())
+    out_res = (abi.CdrWfResult * n)()
+    dev.down(out_res, suf_out.result)
+    row_b = {"n_activity": 128, "n_timer": 32, "n_child": 48, "n_cancel": 24, "n_signal": 40}
+    res_np = np.frombuffer(out_res, dtype=np.uint32).reshape(n, -1)
+    pre_np = np.frombuffer(pre_res, dtype=np.uint32).reshape(n, -1)
+
+    def rows(rn, sel):
+        tot_ = 0
+        for f, bb in row_b.items():
+            tot_ += int(rn[sel, getattr(abi.CdrWfResult, f).offset // 4].astype(np.int64).sum()) * bb
+        return tot_ + 16 * int(rn[sel, abi.CdrWfResult.n_vh.offset // 4].astype(np.int64).sum())
+    carried = src >= 0
+    loaded_b = int(carried.sum()) * 256 + rows(pre_np, carried)
+    out_b = n * 264 + rows(res_np, np.ones(n, bool))
+    alg = ev_bytes + loaded_b + out_b
+    out_codes = res_np[:, 0].view(np.int32)
+    parity = None
+    if not args.no_parity:
+        import oracle
+        t1 = time.perf_counter()
+        per = torch.zeros(max(1, n), dtype=torch.int64, device="cuda")
+        tsum = torch.zeros(1, dtype=torch.int64, device="cuda")
+        rc = L.cdr_entry_digests_async(eng.ctx, C.byref(suf_db), C.byref(suf_out), C.c_void_p(per.data_ptr()),
+                                       C.c_void_p(tsum.data_ptr()), C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"cdr_entry_digests_async rc={rc}")
+        torch.cuda.synchronize()
+        got = per[:n].cpu().numpy().view(np.uint64).copy()
+        th = host_cores()[0]
+        ref_pre = oracle.replay(pre, pre_pl, threads=th)
+        sb = engine.Batch(events=b.events, wfs=suf.wfs, kvs=b.kvs, rps=b.rps, cluster=b.cluster, now_ns=b.now_ns,
+                          uuid_seed=b.uuid_seed, empty_uuid=b.empty_uuid, carry=engine.Carry(src=src, state=ref_pre))
+        rpl = engine.plan(sb)
+        ref = oracle.replay(sb, rpl, threads=th)
+        want, _ = oracle.entry_digests(sb, rpl, ref, th)
+        whole, _, _ = oracle.synth_digests(cfg, np.arange(n_wf, dtype=np.uint32), seed, threads=th)
+        bad = np.nonzero(got != want)[0]
+        bad_whole = np.nonzero(got != whole)[0]
+        parity = {"checked": True, "entries": n, "mismatched_entries": int(len(bad)),
+                  "first_mismatches": bad[:8].tolist(), "split_vs_whole_mismatched_entries": int(len(bad_whole)),
+                  "seconds": time.perf_counter() - t1,
+                  "method": "per-entry digest (cdr_entry_digests_async vs oracle/digest_ref.cpp) of the carried "
+                            "replay against the oracle's carried replay of its own prefix states, and against the "
+                            "oracle's whole-history replay"}
+        log(f"carry parity: {len(bad)} of {n} entries differ from the oracle's carried replay, "
+            f"{len(bad_whole)} from the whole-history replay ({parity['seconds']:.1f}s)")
+    achieved = alg / (kern_ms / 1e3) / 1e9
+    workload = f"C{cfg}-{n_wf}wf-carry-half"
+    traffic, tnote = load_traffic(workload)
+    line = {
+        "metric": "history events replayed/sec + workflows rebuilt/sec (node), % of HBM roofline",
+        "value": events / (ms / 1e3), "unit": "events/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": f"synthetic config {cfg}, each history's second half applied onto its first half's loaded state",
+        "config": {"workload": workload, "workflows_per_gpu": n_wf, "entries": n, "carried_entries": int(carried.sum()),
+                   "events_per_step": events, "routing": route,
+                   "status": {abi.STATUS.get(int(v), str(int(v))): int(c) for v, c in
+                              zip(*np.unique(out_codes, return_counts=True))},
+                   "parallelism": "shard1"},
+        "workflows_per_s": n_wf / (ms / 1e3),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS,
+                     "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_note": tnote or traffic.get("source"),
+                     "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": alg,
+                     "bytes_breakdown": {"events": ev_bytes, "loaded_state": loaded_b, "written": out_b}},
+        "host": {"setup_s": setup_s},
+        "parity": parity, "parity_checked": parity is not None,
+    }
+    print(json.dumps(line), flush=True)
+    dev.close()
 
 
 def main():
@@ -453,6 +619,9 @@ def main():
     ap.add_argument("--ndc-forks", action="store_true",
                     help="configs[4]'s conflict-resolution line: the forked config-5 population replicated on "
                          "the device (base branch + 2 fork rounds per step); --wfs workflows")
+    ap.add_argument("--carry", action="store_true",
+                    help="carry-in line: each history's second half replayed onto its first half's loaded state "
+                         "(--config, --wfs)")
     args = ap.parse_args()
     import torch  # before libcdr.so: torch's HIP runtime must be the process's one (tests/conftest.py)
     L = abi.lib()
@@ -460,6 +629,8 @@ def main():
         raise SystemExit(f"libcdr.so is a variant build (cdr_build_flags = {L.cdr_build_flags():#x}); rebuild it")
     if args.ndc_forks:
         return ndc_forks_line(args)
+    if args.carry:
+        return carry_line(args)
 
     import torch
     world, rank, local = dist_env()

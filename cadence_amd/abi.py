@@ -248,6 +248,7 @@ CAP_LANE = 0x4
 CAP_REG = 0x8
 CAP_REG2 = 0x10
 CAP_REG0 = 0x20
+CAP_LOADED = 0x40
 
 # variable-size row blobs (cdr.h cdr_encode_blobs_async)
 CdrStrtab = _S("cdr_strtab", [("bytes", C.c_void_p), ("off", C.c_void_p), ("n", u32), ("_pad", u32)])

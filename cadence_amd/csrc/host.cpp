@@ -66,7 +66,7 @@ namespace cdr_internal {
 uint32_t arena_words_for(uint32_t type) { return cdr_arena_words_for(type); }
 
 void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* out, const cdr_kv* kvs,
-              const cdr_reset_point* rps, const uint32_t* loaded) {
+              const cdr_reset_point* rps, const loaded_rows* loaded) {
   cdr_wf_caps c{};
   bool fast = builder != CDR_BUILDER_2DC && n > 0 && ev[0].type == CDR_EV_WF_STARTED;
   bool have_ver = false;
@@ -92,12 +92,16 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
     auto it = std::find(lv[t].begin(), lv[t].end(), key);
     if (it != lv[t].end()) lv[t].erase(it);
   };
-  if (loaded) {  // a loaded state's rows: keys no event of the history names (never removed)
-    live = live_max = loaded[0];
-    for (int t = 0; t < 4; t++)
-      for (uint32_t i = 0; i < loaded[1 + t]; i++) lv_add(t, INT64_MIN + i, false);
-    for (uint32_t i = 0; i < loaded[5]; i++) rp_cks.push_back(0xFFFFFFFFu - i);
-    for (uint32_t i = 0; i < loaded[6]; i++) sa_keys.push_back(0xFFFFFFFFu - i);
+  if (loaded) {  // a loaded state's rows (by key when known; else keys no event names)
+    const loaded_rows& L = *loaded;
+    live = live_max = L.n[0];
+    for (uint32_t i = 0; i < L.n[1]; i++) lv_add(0, L.timer ? (int64_t)L.timer[i].timer_id : INT64_MIN + i, false);
+    for (uint32_t i = 0; i < L.n[2]; i++) lv_add(1, L.child ? L.child[i].initiated_id : INT64_MIN + i, false);
+    for (uint32_t i = 0; i < L.n[3]; i++) lv_add(2, L.cancel ? L.cancel[i].initiated_id : INT64_MIN + i, false);
+    for (uint32_t i = 0; i < L.n[4]; i++) lv_add(3, L.signal ? L.signal[i].initiated_id : INT64_MIN + i, false);
+    for (uint32_t i = 0; i < L.n[5]; i++)
+      rp_cks.push_back(L.rp ? ((L.rp[i].flags & CDR_RP_HAS_CHECKSUM) ? L.rp[i].binary_checksum : 0u) : 0xFFFFFFFFu - i);
+    for (uint32_t i = 0; i < L.n[6]; i++) sa_keys.push_back(L.sa ? L.sa[i].key : 0xFFFFFFFFu - i);
   }
   for (uint64_t k = 0; k < n; k++) {
     const cdr_event& e = ev[k];
@@ -343,9 +347,19 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
       if (src >= cy.n_src || d.parent >= 0 || !cy.state.result) return CDR_API_EINVAL;
       const cdr_wf_result& r = cy.state.result[src];
       if (r.code != CDR_OK) return CDR_API_EINVAL;
-      const uint32_t loaded[7] = {r.n_activity, r.n_timer, r.n_child, r.n_cancel, r.n_signal, r.n_reset_points,
-                                  r.n_search_attr};
-      cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c, b->kvs, b->rps, loaded);
+      cdr_internal::loaded_rows ld{{r.n_activity, r.n_timer, r.n_child, r.n_cancel, r.n_signal, r.n_reset_points,
+                                    r.n_search_attr},
+                                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+      if (cy.caps) {  // host-visible rows: the simulation follows their keys
+        const cdr_wf_caps& sc = cy.caps[src];
+        ld.timer = cy.state.timer ? cy.state.timer + sc.timer_off : nullptr;
+        ld.child = cy.state.child ? cy.state.child + sc.child_off : nullptr;
+        ld.cancel = cy.state.cancel ? cy.state.cancel + sc.cancel_off : nullptr;
+        ld.signal = cy.state.signal ? cy.state.signal + sc.signal_off : nullptr;
+        ld.rp = cy.state.rp ? cy.state.rp + sc.rp_off : nullptr;
+        ld.sa = cy.state.sa ? cy.state.sa + sc.sa_off : nullptr;
+      }
+      cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c, b->kvs, b->rps, &ld);
       c.act_cap += r.n_activity;
       c.timer_cap += r.n_timer;
       c.child_cap += r.n_child;
@@ -354,7 +368,7 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
       c.vh_cap += r.n_vh;
       c.rp_cap += r.n_reset_points;
       c.sa_cap += r.n_search_attr;
-      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_LANE);
+      c.flags = (c.flags & ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_LANE)) | CDR_CAP_LOADED;
     } else {
       cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c, b->kvs, b->rps);
     }
@@ -380,7 +394,7 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
       // and a slice runs as its largest lane needs); an entry whose loaded state outgrows even
       // that is handed on to the general kernel (replay_reg.inc).  CDR_CARRY_REG2=0 keeps the
       // history's own variant and relies on the hand-on chain (C5 forks 1M: 53.6 vs 48.5 ms)
-      c.flags &= ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_LANE | CDR_CAP_REG0);
+      c.flags = (c.flags & ~(CDR_CAP_FAST | CDR_CAP_WAVE | CDR_CAP_LANE | CDR_CAP_REG0)) | CDR_CAP_LOADED;
       static const int all12 = [] {
         const char* e = std::getenv("CDR_CARRY_REG2");
         return e ? std::atoi(e) : 1;
@@ -455,7 +469,7 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     const uint32_t f = caps ? caps[w].flags : 0u;
     const uint64_t thr = (f & CDR_CAP_REG) ? long_thr : long_thr2;
     if ((mode & CDR_PLAN_WAVE) && (mode & CDR_PLAN_PAR) && !(mode & CDR_PLAN_WAVE_ALL) &&
-        (f & (CDR_CAP_REG | CDR_CAP_REG2)) && (uint64_t)wfs[w].ev_len > ((f & CDR_CAP_REG) ? par_thr : par_thr2)) {
+        (f & (CDR_CAP_REG | CDR_CAP_REG2)) && !(f & CDR_CAP_LOADED) && (uint64_t)wfs[w].ev_len > ((f & CDR_CAP_REG) ? par_thr : par_thr2)) {
       pars.push_back(w);
       continue;
     }

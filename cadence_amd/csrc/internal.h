@@ -11,12 +11,24 @@ uint32_t arena_words_for(uint32_t type);
 
 // Output capacities of one history (cdr_plan_caps restricted to one workflow);
 // offsets are left zero.
-// `loaded` (nullable): the live rows a loaded state (cdr_carry) starts with — activities,
-// user timers, children, request-cancels, signals, reset points, search-attribute keys —
-// counted into the peak live sets and the register-table envelope as rows the history never
-// removes (an upper bound).
+// The live rows a loaded state (cdr_carry) starts with: counts (activities, user timers,
+// children, request-cancels, signals, reset points, search-attribute keys) and, when the
+// state is host-visible, the rows themselves (their keys: a history event that removes a
+// loaded row removes it from the simulation too; without rows, the loaded rows count as
+// rows no event removes — an upper bound).
+struct loaded_rows {
+  uint32_t n[7];
+  const cdr_timer_info* timer;
+  const cdr_child_info* child;
+  const cdr_cancel_info* cancel;
+  const cdr_signal_info* signal;
+  const cdr_reset_point* rp;
+  const cdr_kv* sa;
+};
+// `loaded` (nullable): the entry replays onto that state; its rows count into the peak
+// live sets and the register-table envelope.
 void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* c, const cdr_kv* kvs = nullptr,
-              const cdr_reset_point* rps = nullptr, const uint32_t* loaded = nullptr);
+              const cdr_reset_point* rps = nullptr, const loaded_rows* loaded = nullptr);
 
 // Pack one workflow's events into lane `lane` of a slice whose first row is row0 and
 // whose length is len (rows beyond n are padding).  `apos` is the workflow's arena

@@ -248,6 +248,8 @@ __global__ __launch_bounds__(256) void k_ndc_rebuild_verify(uint32_t n, const cd
   s.current = d.branch_index;  // SetCurrentVersionHistoryIndex (:172-174)
 }
 
+__device__ void zero_result(cdr_wf_result& r, int32_t code);
+
 __global__ __launch_bounds__(256) void k_vhs_sync(uint32_t n, cdr_vhs* vhs, cdr_vh_item* pool,
                                                   const cdr_wf_caps* caps, cdr_out O) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
@@ -255,7 +257,10 @@ __global__ __launch_bounds__(256) void k_vhs_sync(uint32_t n, cdr_vhs* vhs, cdr_
   const cdr_wf_result& r = O.result[w];
   if (r.code != CDR_OK) return;
   cdr_vhs& s = vhs[w];
-  if (r.n_vh > s.items_cap) return;
+  if (r.n_vh > s.items_cap) {  // the caller's item slots are too few: the workflow fails visibly
+    zero_result(O.result[w], CDR_E_VHS_CAPACITY);
+    return;
+  }
   if (s.n_branches == 0) {  // NewVersionHistories (versionHistory.go:350-363)
     s.n_branches = 1;
     s.current = 0;

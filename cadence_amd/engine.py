@@ -123,6 +123,47 @@ def split_batch(batch: Batch, seed: int = 1):
     return _entry_batch(batch, wfs), cut
 
 
+def split_half(batch: Batch) -> np.ndarray:
+    """The call boundary nearest after the middle of every top-level entry without a
+    continue-as-new (vectorised over the events' flag words, for full-size batches):
+    cut[w] = event offset of that call's first event within entry w, 0 = not split (one
+    call, or a new-run link).  The prefix [0, cut) and the suffix [cut, len) are the two
+    applyEvents sequences a loaded-state replay splits the history into."""
+    n = batch.n_wfs
+    words = C.sizeof(abi.CdrEvent) // 4
+    ev = np.frombuffer(batch.events, dtype=np.uint32).reshape(-1, words) if len(batch.events) else \
+        np.zeros((0, words), np.uint32)
+    bf = np.nonzero(ev[:, abi.CdrEvent.flags.offset // 4] & abi.EVF_BATCH_FIRST)[0].astype(np.int64)
+    wf = np.frombuffer(batch.wfs, dtype=np.uint8).reshape(n, C.sizeof(abi.CdrWfDesc))
+
+    def col(name, dt):
+        o = getattr(abi.CdrWfDesc, name).offset
+        return wf[:, o:o + np.dtype(dt).itemsize].copy().view(dt).ravel()
+    off, ln = col("ev_off", np.uint64).astype(np.int64), col("ev_len", np.uint64).astype(np.int64)
+    top = (col("parent", np.int32) < 0) & (col("newrun", np.int32) < 0)
+    i = np.searchsorted(bf, off + ln // 2)
+    pos = np.where(i < len(bf), bf[np.minimum(i, max(0, len(bf) - 1))] if len(bf) else 0, -1)
+    ok = top & (pos > off) & (pos < off + ln)
+    return np.where(ok, pos - off, 0)
+
+
+def cut_batches(batch: Batch, cut) -> tuple:
+    """(prefix wfs, suffix wfs) descriptor arrays of a split: entry w's events [0, cut[w])
+    and [cut[w], len) (cut 0: the prefix is the whole entry and the suffix replays it again
+    on a fresh builder — its carry src is -1)."""
+    n = batch.n_wfs
+    pre = (abi.CdrWfDesc * n)()
+    suf = (abi.CdrWfDesc * n)()
+    C.memmove(pre, batch.wfs, C.sizeof(pre))
+    C.memmove(suf, batch.wfs, C.sizeof(suf))
+    for w in np.nonzero(np.asarray(cut) > 0)[0]:
+        c = int(cut[w])
+        pre[w].ev_len = c
+        suf[w].ev_off += c
+        suf[w].ev_len -= c
+    return _entry_batch(batch, pre), _entry_batch(batch, suf)
+
+
 def suffix_batch(batch: Batch, cut, prefix: Batch, prefix_out: "Outputs") -> Batch:
     """The remainder of split_batch's cut as a batch replaying onto the prefix's
     persisted states; entries whose prefix failed (or were not cut) replay whole on a

@@ -32,14 +32,31 @@ from . import abi, engine
 ITEMS_CAP = 64  # version-history item slots per branch
 
 
-def new_vhs(n: int, items_cap: int = ITEMS_CAP):
-    """Empty VersionHistories for n workflows (items pool: MAX_BRANCHES x items_cap each)."""
+def new_vhs(n: int, items_cap=ITEMS_CAP):
+    """Empty VersionHistories for n workflows; items pool: MAX_BRANCHES x items_cap[w] slots
+    for workflow w (items_cap: one capacity for all, or one per workflow)."""
+    caps = np.broadcast_to(np.asarray(items_cap, dtype=np.int64), (n,)).astype(np.int64)
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(caps * abi.VHS_MAX_BRANCHES, out=offs[1:])
     vhs = (abi.CdrVHS * max(1, n))()
-    for w in range(n):
-        vhs[w].items_cap = items_cap
-        vhs[w].items_off = w * items_cap * abi.VHS_MAX_BRANCHES
-    pool = (abi.CdrVHItem * max(1, n * items_cap * abi.VHS_MAX_BRANCHES))()
+    raw = np.frombuffer(vhs, dtype=np.uint8).reshape(max(1, n), C.sizeof(abi.CdrVHS))[:n]
+    o_cap, o_off = abi.CdrVHS.items_cap.offset, abi.CdrVHS.items_off.offset
+    raw[:, o_cap:o_cap + 4] = caps.astype(np.uint32).view(np.uint8).reshape(n, 4)
+    raw[:, o_off:o_off + 8] = offs[:n].astype(np.uint64).view(np.uint8).reshape(n, 8)
+    pool = (abi.CdrVHItem * max(1, int(offs[n])))()
     return vhs, pool
+
+
+def items_cap_for(base: engine.Batch, rebuild: engine.Batch, forks) -> np.ndarray:
+    """Per-workflow version-history item slots a replication run needs per branch: every
+    branch holds at most the items of the state's whole history (the base's, the rebuilt
+    branch's and every fork's version runs: state_caps_for's vh_cap), floor ITEMS_CAP."""
+    sp = state_caps_for(base, rebuild, forks)
+    n = base.n_wfs
+    vh = np.frombuffer(sp.caps, dtype=np.uint8).reshape(max(1, n), C.sizeof(abi.CdrWfCaps))[:n]
+    o = abi.CdrWfCaps.vh_cap.offset
+    need = vh[:, o:o + 4].copy().view(np.uint32).ravel().astype(np.int64)
+    return np.maximum(need, ITEMS_CAP)
 
 
 def branch_items(vhs, pool, w: int, b: int):
@@ -265,7 +282,7 @@ class DeviceReplicator:
     branch, rebuild + refresh + verify, apply onto the in-memory rebuilt or the loaded
     state, VH sync, adopt — with every buffer allocated up front."""
 
-    def __init__(self, eng: engine.Engine, base: engine.Batch, rebuild: engine.Batch, forks, items_cap=ITEMS_CAP,
+    def __init__(self, eng: engine.Engine, base: engine.Batch, rebuild: engine.Batch, forks, items_cap=None,
                  refresh_flags: int = abi.REFRESH_ADVANCED_VISIBILITY):
         n = base.n_wfs
         L = abi.lib()
@@ -298,7 +315,7 @@ class DeviceReplicator:
             r.refresh_now = rebuild.now_ns
             r.refresh_flags = refresh_flags
             self.rounds.append((r, pl))
-        self.vhs_h, self.pool_h = new_vhs(n, items_cap)
+        self.vhs_h, self.pool_h = new_vhs(n, items_cap_for(base, rebuild, forks) if items_cap is None else items_cap)
         self.vhs, self.pool = dev.up(self.vhs_h), dev.up(self.pool_h)
         self.vhs_fresh = dev.up(self.vhs_h)  # NewVersionHistories for every workflow (reset())
         self.events = [int(sum(base.wfs[w].ev_len for w in range(n)))] + [

@@ -620,6 +620,10 @@ typedef struct cdr_wf_caps {
 #define CDR_REG0_NA 3u
 #define CDR_REG0_NT 5u
 #define CDR_REG0_NX 3u
+/* the entry replays onto a loaded state (cdr_carry; cdr_plan_caps / cdr_plan_ndc_apply set
+ * it): never planned onto a PAR slice — only the register-table kernels' lane form and the
+ * general kernel take a loaded state */
+#define CDR_CAP_LOADED 0x40u
 #define CDR_LANE_MAX_ACT 6u
 #define CDR_LANE_MAX_TIMERS 10u
 #define CDR_LANE_MAX_EXT 8u

@@ -141,7 +141,7 @@ class NdcBackend:
         return dec
 
 
-def ndc_replicate(base, rebuild, forks, items_cap: int = 64, refresh_flags: int = 1, threads: int = 1):
+def ndc_replicate(base, rebuild, forks, items_cap=None, refresh_flags: int = 1, threads: int = 1):
     """The NDC replication run restated on the CPU (replay_ref.cpp cdro_ndc_replicate_round:
     per workflow, the rebuilt MutableState kept in memory between nDCStateRebuilder.rebuild
     and applyEvents, nDCConflictResolver.go:117-184, nDCHistoryReplicator.go:330-398): the
@@ -164,7 +164,7 @@ def ndc_replicate(base, rebuild, forks, items_cap: int = 64, refresh_flags: int 
     rc = L.cdro_replay_batch(C.byref(base.cstruct()), sp.caps, C.byref(state.cstruct()), threads)
     if rc:
         raise RuntimeError(f"cdro_replay_batch rc={rc}")
-    vhs, pool = ndc.new_vhs(n, items_cap)
+    vhs, pool = ndc.new_vhs(n, ndc.items_cap_for(base, rebuild, forks) if items_cap is None else items_cap)
     L.cdro_vhs_sync(n, vhs, pool, sp.caps, C.byref(state.cstruct()))
     rp = engine.plan(rebuild)
     decs, per_round = [], []

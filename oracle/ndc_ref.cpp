@@ -373,8 +373,10 @@ int cdro_vhs_sync(uint32_t n, cdr_vhs* vhs, cdr_vh_item* pool, const cdr_wf_caps
     const cdr_wf_result& r = out->result[w];
     if (r.code != CDR_OK) continue;
     cdr_vhs& s = vhs[w];
-    if (r.n_vh > s.items_cap) {
-      continue;  // capacity is the caller's: left unsynchronised (the GPU path reports it)
+    if (r.n_vh > s.items_cap) {  // the caller's item slots are too few: the workflow fails visibly
+      out->result[w] = cdr_wf_result{};
+      out->result[w].code = CDR_E_VHS_CAPACITY;
+      continue;
     }
     if (s.n_branches == 0) {
       s.n_branches = 1;

@@ -1533,7 +1533,11 @@ static bool finish(const GoErr& e, const MutableState& ms, const cdr_batch* b, u
 // the current branch's VersionHistory := the applied state's (cdr_vhs_sync's restatement)
 static void sync_vhs(cdr_vhs& s, cdr_vh_item* pool, const cdr_out& o, const cdr_wf_caps& c, uint32_t w) {
   const cdr_wf_result& r = o.result[w];
-  if (r.code != CDR_OK || r.n_vh > s.items_cap) return;
+  if (r.code != CDR_OK) return;
+  if (r.n_vh > s.items_cap) {  // the caller's item slots are too few: the workflow fails visibly
+    fail_result(o.result[w], CDR_E_VHS_CAPACITY);
+    return;
+  }
   if (s.n_branches == 0) {
     s.n_branches = 1;
     s.current = 0;
@@ -1630,7 +1634,10 @@ int cdro_ndc_replicate_round(uint32_t n, const cdr_ndc_task* tasks, const cdr_vh
       state->result[w] = apply_out->result[w];
     } else {
       sync_vhs(vhs[w], pool, *apply_out, apply_caps[w], w);
-      copy_state(*apply_out, apply_caps[w], *state, state_caps[w], w);
+      if (apply_out->result[w].code != CDR_OK)
+        state->result[w] = apply_out->result[w];
+      else
+        copy_state(*apply_out, apply_caps[w], *state, state_caps[w], w);
     }
     delete ms;
   };

@@ -129,3 +129,20 @@ def test_apply_working_slots_bounded_by_live_rows():
         assert caps[w].act_cap == own[w].act_cap + caps_tab[w].act_cap
         tighter += caps[w].act_live < own[w].act_live + caps_tab[w].act_cap
     assert tighter > 0
+
+
+def test_vh_item_capacity_is_reported():
+    """The VersionHistories item slots are the caller's (cdr_vhs.items_cap): a state whose
+    version history outgrows them fails with CDR_E_VHS_CAPACITY (it is not silently left
+    without a branch — which surfaced as E_VH_NO_LCA at the next task); the default slots
+    come from the run's own histories (ndc.items_cap_for) and never overflow."""
+    import oracle
+    base, rebuild, forks = ndc.synth_forked(5, 64, 0x5EED0C07)
+    need = ndc.items_cap_for(base, rebuild, forks)
+    assert (need >= ndc.ITEMS_CAP).all()
+    small = 4
+    st, _, _, _, _ = oracle.ndc_replicate(base, rebuild, forks, items_cap=small)
+    hist = engine.status_histogram(st)
+    assert hist.get("E_VHS_CAPACITY", 0) > 0, hist
+    st, _, _, _, _ = oracle.ndc_replicate(base, rebuild, forks)
+    assert engine.status_histogram(st) == {"OK": 64}

@@ -107,9 +107,11 @@ def test_vh_add_or_update_failed_event_id_not_increasing():  # :218-231
     assert _vh([(3, 0), (6, 4)], 6, 4)[0] == 6
 
 
-def test_vh_add_or_update_failed_version_not_increasing():  # :233-292
-    assert _vh([(3, 0), (6, 4)], 7, 3)[0] == 5
-    assert _vh([(3, 0), (6, 4)], 5, 5)[0] == 6
+def test_vh_add_or_update_failed_version_not_increasing():  # :233-249
+    # the reference's three items, each an error; the version check comes first
+    # (versionHistory.go:213-218), so each is the lower-version one
+    for event_id in (6, 2, 7):
+        assert _vh([(3, 0), (6, 4)], event_id, 3)[0] == 5, event_id
 
 
 def test_vh_item_panics():  # NewVersionHistoryItem versionHistory.go:31-42

@@ -9,7 +9,7 @@ WRITE_SIZE is taken as is.  Counters are averaged over the profiled dispatches â
 an anchor kernel (a multi-kernel step: C3-C5 run several replay kernels per step), summed
 over every matching dispatch and divided by the anchor's dispatch count (one per step).
 Writes profiles/traffic_<workload>.json (and traffic_latest.json).
-usage: tools/traffic.py <tag> <workload> <profile-name> [kernel-substring] [anchor-kernel]"""
+usage: tools/traffic.py <tag> <workload> <profile-name> [kernel-substring] [anchor-kernel] [anchors per step]"""
 import collections
 import csv
 import glob
@@ -24,6 +24,7 @@ def main():
     tag, workload, name = sys.argv[1:4]
     kern = sys.argv[4] if len(sys.argv) > 4 else "k_replay"
     anchor = sys.argv[5] if len(sys.argv) > 5 else None
+    per_step = float(sys.argv[6]) if len(sys.argv) > 6 else 1.0  # anchor dispatches per step
     agg = collections.defaultdict(float)
     nd = collections.defaultdict(set)
     steps = collections.defaultdict(set)  # per counter pass: the anchor's dispatches
@@ -38,7 +39,7 @@ def main():
             nd[r["Counter_Name"]].add(r["Dispatch_Id"])
             kernels[r["Kernel_Name"].split("(")[0]].add(r["Dispatch_Id"])
     if anchor:
-        avg = {c: v / max(1, len(steps[c])) for c, v in agg.items()}
+        avg = {c: v / max(1, len(steps[c])) * per_step for c, v in agg.items()}
     else:
         avg = {c: v / len(nd[c]) for c, v in agg.items()}
     lines = [f"{c:24s} {v:.6g}" for c, v in sorted(avg.items())]
