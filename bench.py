@@ -7,7 +7,9 @@ workflows x 203 events, synthetic, NDC builder, on each GPU
 (weak scaling: N GPUs replay N x 1M workflows, sharded by historyShardID =
 Fingerprint32(workflowID) % 16384 and assigned shard->GPU greedily).
 
-One "step" = one replay of the whole device-resident batch (k_replay + k_finalize).
+One "step" = one replay of the whole device-resident batch: the replay kernels of the
+batch's slice classes (C2: k_replay_fast; C3-C5: k_replay_cls and its k_replay_reg retry
+passes, the PAR slices, the general kernel for what fits no other) + k_tables + k_finalize.
 Inputs are uploaded before the timed region; host SoA packing and H2D time are
 reported separately.  The CPU baseline is the CPU restatement (oracle/) run with one
 task per workflow on the host's cores over a bounded sample.
@@ -48,11 +50,11 @@ def dist_env():
     return ws, rank, local
 
 
-def workflow_weights(config: int, total_wfs: int, seed: int) -> np.ndarray:
+def workflow_weights(config: int, total_wfs: int, seed: int, long_stride: int = 0) -> np.ndarray:
     """Planned event count of every workflow of the population (synth.cpp plan_one),
     drawn without generating the histories: the shard->GPU assignment's weights."""
     L = abi.lib()
-    p = abi.CdrSynthParams(config=config, n_wfs=0, seed=seed)
+    p = abi.CdrSynthParams(config=config, n_wfs=0, seed=seed, long_stride=long_stride)
     w = np.zeros(total_wfs, np.uint32)
     rc = L.cdr_synth_weights(C.byref(p), total_wfs, w.ctypes.data)
     if rc:
@@ -304,7 +306,7 @@ def load_traffic(workload):
     return d, None
 
 
-def parity_check(db, ctx, stream, config, mine, seed):
+def parity_check(db, ctx, stream, config, mine, seed, long_stride=0):
     """Full-size parity: every entry's output digest on the GPU (k_digest) against the
     CPU restatement's (oracle/, restated hash in digest_ref.cpp) over the same
     population, entry by entry.  Runs after the timed region."""
@@ -312,7 +314,7 @@ def parity_check(db, ctx, stream, config, mine, seed):
     t0 = time.perf_counter()
     got, got_sum = db.digests(ctx, stream)
     threads = host_cores()[0]
-    want, want_sum, hist = oracle.synth_digests(config, mine, seed, threads=threads)
+    want, want_sum, hist = oracle.synth_digests(config, mine, seed, threads=threads, long_stride=long_stride)
     bad = np.nonzero(got != want)[0] if len(got) == len(want) else np.arange(max(len(got), len(want)))
     return {"checked": True, "entries": int(len(want)), "mismatched_entries": int(len(bad)),
             "first_mismatches": bad[:8].tolist(), "gpu_checksum": got_sum, "oracle_checksum": want_sum,
@@ -619,6 +621,9 @@ def main():
     ap.add_argument("--ndc-forks", action="store_true",
                     help="configs[4]'s conflict-resolution line: the forked config-5 population replicated on "
                          "the device (base branch + 2 fork rounds per step); --wfs workflows")
+    ap.add_argument("--long-stride", type=int, default=0,
+                    help="configs[3] load balance: every workflow at index long_stride/2 mod long_stride is generated "
+                         "at the history count limit (204,800 events); 125000 mixes 8 into 1M")
     ap.add_argument("--carry", action="store_true",
                     help="carry-in line: each history's second half replayed onto its first half's loaded state "
                          "(--config, --wfs)")
@@ -648,7 +653,7 @@ def main():
         L.cdr_set_fast_path(ctx, 0)
 
     total = args.wfs * world
-    mine, load = assign_shards(total, world, rank, workflow_weights(args.config, total, args.seed))
+    mine, load = assign_shards(total, world, rank, workflow_weights(args.config, total, args.seed, args.long_stride))
     log(f"[rank {rank}] {len(mine)} of {total} workflows (shard->GPU greedy over {NUM_SHARDS} shards)")
     # the register-table slices' class-sorted blocks: emitted by the host packer beside the
     # slab (default; host packing time cls_pack_s), built on the device in every step
@@ -657,7 +662,7 @@ def main():
     db = DeviceBatch(torch, args.config, mine, args.seed,
                      plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0)
                      | (0 if args.no_par else abi.PLAN_PAR),
-                     ctx_for_cls=ctx, cls=cls_src)
+                     ctx_for_cls=ctx, cls=cls_src, long_stride=args.long_stride)
     if args.no_cls:
         L.cdr_set_cls_path(ctx, abi.CLS_OFF)
     log(f"[rank {rank}] {db.n_fast} of {db.info.n_slices} slices on the fast-path kernel, {db.n_wave} wave slices")
@@ -708,7 +713,7 @@ def main():
     if tot_ok != tot_wfs:
         log(f"WARNING: {tot_wfs - tot_ok} workflows did not replay OK")
 
-    parity = None if args.no_parity else parity_check(db, ctx, stream, args.config, mine, args.seed)
+    parity = None if args.no_parity else parity_check(db, ctx, stream, args.config, mine, args.seed, args.long_stride)
     if parity:
         log(f"[rank {rank}] parity: {parity['mismatched_entries']} of {parity['entries']} entries differ from the "
             f"oracle ({parity['seconds']:.1f}s)")
@@ -727,7 +732,7 @@ def main():
     ev_per_s = tot_events * args.steps / elapsed
     wf_per_s = tot_wfs * args.steps / elapsed
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-    workload = f"C{args.config}-{args.wfs}wf-sliced"
+    workload = f"C{args.config}-{args.wfs}wf-sliced" + (f"-long{args.long_stride}" if args.long_stride else "")
     traffic, traffic_note = load_traffic(workload)
     bld = db.builders()
     names = {abi.BUILDER_LOCAL: "local", abi.BUILDER_2DC: "2DC", abi.BUILDER_NDC: "NDC"}

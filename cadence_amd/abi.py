@@ -296,7 +296,7 @@ CdrNdcRound = _S("cdr_ndc_round", [("tasks", C.c_void_p), ("task_items", C.c_voi
 CdrSynthParams = _S("cdr_synth_params", [
     ("config", i32), ("n_wfs", u32), ("seed", u64), ("target_len", u32), ("max_len", u32), ("error_rate", f64),
     ("builder", i32), ("rebuild", i32), ("fault_kinds", u32), ("plan_mode", u32), ("index_map", C.c_void_p),
-    ("ndc_part", u32), ("_pad2", u32)])
+    ("ndc_part", u32), ("long_stride", u32)])
 SYNTH_PART_BASE, SYNTH_PART_REBUILD, SYNTH_PART_FORK_A, SYNTH_PART_FORK_B = range(4)
 # synth fault kinds that keep a sequential-activity history on the fast path (synth.cpp inject_fault)
 FAULTS_FAST = (1 << 1) | (1 << 2) | (1 << 3) | (1 << 5) | (1 << 6)

@@ -588,6 +588,8 @@ WfPlan plan_one(const cdr_synth_params& P, uint32_t w, Rng& r2) {
       q.target = lognormal_len(r2, P.target_len ? P.target_len : 60, cap);
       break;
   }
+  if (P.long_stride && w % P.long_stride == P.long_stride / 2 && P.config != 1 && P.config != 2)
+    q.target = cap;  // at the history count limit (the draws above are kept: the stream stays aligned)
   return q;
 }
 

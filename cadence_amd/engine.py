@@ -213,7 +213,7 @@ class SynthBuffers:
 
 def synth_batch(config: int, n_wfs: int, seed: int, target_len: int = 0, max_len: int = 0,
                 error_rate: float = 0.0, builder: int = -1, rebuild: bool = False, fault_kinds: int = 0,
-                index_map=None, buffers: "SynthBuffers | None" = None, part: int = 0) -> Batch:
+                index_map=None, buffers: "SynthBuffers | None" = None, part: int = 0, long_stride: int = 0) -> Batch:
     """Deterministic synthetic batch (cadence_amd/csrc/synth.cpp) in natural order.
     `index_map` (uint32 array of n_wfs global workflow indices) generates a shard's
     share of a larger population: workflow i of the batch is global workflow
@@ -224,7 +224,7 @@ def synth_batch(config: int, n_wfs: int, seed: int, target_len: int = 0, max_len
     L = abi.lib()
     p = abi.CdrSynthParams(config=config, n_wfs=n_wfs, seed=seed, target_len=target_len, max_len=max_len,
                            error_rate=error_rate, builder=builder, rebuild=1 if rebuild else 0,
-                           fault_kinds=fault_kinds, ndc_part=part)
+                           fault_kinds=fault_kinds, ndc_part=part, long_stride=long_stride)
     if index_map is not None:
         index_map = np.ascontiguousarray(index_map, dtype=np.uint32)
         assert len(index_map) == n_wfs

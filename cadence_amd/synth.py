@@ -35,7 +35,7 @@ class DeviceBatch:
     """Synthetic batch generated straight into the sliced layout, uploaded to HBM."""
 
     def __init__(self, torch, config, index_map, seed, target_len=0, plan_mode=abi.PLAN_WAVE | abi.PLAN_PAR, ctx_for_cls=None,
-                 cls="host"):
+                 cls="host", long_stride=0):
         """cls: where the register-table slices' class-sorted blocks (replay_cls.inc) come
         from — "host": the packer emits them beside the slab (cdr_plan_cls / cdr_pack_cls,
         host packing time `cls_pack_s`, uploaded with the slab); "device": built on the
@@ -50,7 +50,7 @@ class DeviceBatch:
         self.index_map = index_map
         p = abi.CdrSynthParams(config=config, n_wfs=len(index_map), seed=seed, target_len=target_len, max_len=0,
                                error_rate=0.0, builder=-1, rebuild=0, index_map=index_map.ctypes.data,
-                               plan_mode=plan_mode)
+                               plan_mode=plan_mode, long_stride=long_stride)
         self.params = p
         t0 = time.perf_counter()
         info = abi.CdrSynthPlanInfo()

@@ -25,7 +25,10 @@ typedef struct cdr_synth_params {
    * F (a DeepCopy of the generator with a version bump, nDC_integration_test.go:224-308)
    * into two continuations.  Which part a batch holds: */
   uint32_t ndc_part;  /* CDR_SYNTH_PART_* */
-  uint32_t _pad2;
+  /* load-balance stress (configs[3]: "skewed lengths up to the history count limit"): if
+   * nonzero, every workflow whose global index is long_stride / 2 modulo long_stride is
+   * generated at the history count limit (max_len) instead of its drawn length */
+  uint32_t long_stride;
 } cdr_synth_params;
 #define CDR_SYNTH_PART_BASE 0    /* the base branch, whole (default) */
 #define CDR_SYNTH_PART_REBUILD 1 /* the base branch's events 1..F (the rebuild path; expected next = F+1) */

@@ -51,7 +51,16 @@ def handcrafted():
 
 
 def check_reference_outcome(final, vhs, pool, decs, doc):
-    """The outcome the reference's flow implies for TestHandcraftedMultipleBranches."""
+    """The outcome for TestHandcraftedMultipleBranches (nDC_integration_test.go:323-613).
+
+    Pinned by the reference: every replication task applies without an error (the test's
+    s.applyEvents asserts NoError), and the two branches' VersionHistories are the ones the
+    test itself builds from the event batches (versionHistory2 / versionHistory3 via
+    DuplicateUntilLCAItem((14, 21)) + eventBatchesToVersionHistory, :571-584).
+    DERIVED, not asserted by the reference (restating nDCBranchMgr / nDCConflictResolver /
+    nDCStateRebuilder on these events — the builder's reading of the flow): the decision's
+    action, branch index and rebuild point, the branch token, and the final
+    ExecutionInfo / pending-row values below the marker."""
     from cadence_amd import ndc
     d = decs[0][0]
     assert (abi.STATUS[d.code], abi.NDC_ACTIONS[d.action], d.branch_index, d.created) == ("OK", "REBUILD", 1, 1)
@@ -61,7 +70,8 @@ def check_reference_outcome(final, vhs, pool, decs, doc):
     assert ndc.branch_items(vhs, pool, 0, 1) == [tuple(x) for x in doc["versionHistory2"]]
     assert (vhs[0].branch[1].token.branch_lo, vhs[0].branch[1].token.branch_hi) == FORK_TOKEN
     r, x = final.result[0], final.exec[0]
-    assert abi.STATUS[r.code] == "OK"
+    assert abi.STATUS[r.code] == "OK"  # pinned: the applies succeed
+    # ---- derived from the restated flow (not asserted by the reference test)
     assert (x.state, x.close_status) == (abi.STATE_COMPLETED, abi.CLOSE_TIMED_OUT)
     assert (x.next_event_id, x.last_first_event_id, x.completion_event_batch_id) == (16, 15, 15)
     assert x.signal_count == 2
