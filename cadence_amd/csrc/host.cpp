@@ -564,7 +564,12 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     const char* e = std::getenv("CDR_PAR_SOLO");
     return e ? (uint32_t)std::strtoul(e, nullptr, 0) : (uint32_t)CDR_PAR_SOLO;
   }();
-  const uint32_t solo = std::min<uint32_t>(solo_max, (uint32_t)pars.size());
+  // ... and every history of at least CDR_PAR_SOLO_LEN events (up to the history count
+  // limit): alone in its slice, k_replay_cls replays its activity / timer / external classes
+  // in wave form (one event per step, the tables spread over the lanes) instead of one lane
+  uint32_t n_solo_len = 0;
+  while (n_solo_len < pars.size() && wfs[pars[n_solo_len]].ev_len >= CDR_PAR_SOLO_LEN) n_solo_len++;
+  const uint32_t solo = std::min<uint32_t>(std::max(solo_max, n_solo_len), (uint32_t)pars.size());
   // balanced PAR slices: a PAR slice's roles each walk its histories one at a time, so the
   // slice's time follows the summed lengths of its histories, and the kernel ends with its
   // heaviest slice (longest-first runs of 16 put the 16 longest histories in slice 0).

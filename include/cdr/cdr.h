@@ -340,6 +340,8 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
 #define CDR_PLAN_PAR 0x8u
 #define CDR_PAR_LANES 16u /* histories per CDR_SLICE_PAR slice (lanes 0 .. 15; the rest empty) */
 #define CDR_PAR_SOLO 0u   /* ... except the longest CDR_PAR_SOLO, one per slice */
+#define CDR_PAR_SOLO_LEN 16384u /* ... and every PAR history at least this long, one per slice
+                                   (k_replay_cls: its class loops in wave form) */
 #define CDR_PAR_MAX_SLICES 128u /* at most this many PAR slices (the longest histories); the rest stay lane slices */
 #define CDR_LONG_MIN 1024u
 #define CDR_LONG_FACTOR 2u

@@ -19,13 +19,14 @@ ap.add_argument("--config", type=int, default=4)
 ap.add_argument("--wfs", type=int, default=1_000_000)
 ap.add_argument("--top", type=int, default=8)
 ap.add_argument("--alone", action="store_true", help="replay only the PAR slices' histories")
+ap.add_argument("--long-stride", type=int, default=0, help="bench.py --long-stride (histories at the count limit)")
 args = ap.parse_args()
 import torch  # noqa: E402
 from cadence_amd.synth import DeviceBatch, RESULT_DTYPE  # noqa: E402
 torch.cuda.init()
 idx = np.arange(args.wfs, dtype=np.uint32)
 bctx = abi.lib().cdr_create(0, None)
-db = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config, ctx_for_cls=bctx)
+db = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config, ctx_for_cls=bctx, long_stride=args.long_stride)
 Lv = abi.load(args.lib)
 ctx = Lv.cdr_create(0, None)
 stream = torch.cuda.current_stream().cuda_stream
