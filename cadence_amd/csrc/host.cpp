@@ -567,8 +567,13 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   // ... and every history of at least CDR_PAR_SOLO_LEN events (up to the history count
   // limit): alone in its slice, k_replay_cls replays its activity / timer / external classes
   // in wave form (one event per step, the tables spread over the lanes) instead of one lane
+  static const uint64_t solo_len = [] {
+    const char* e = std::getenv("CDR_PAR_SOLO_LEN");  // A/B knob (events; 0 = none)
+    const uint64_t v = e ? std::strtoull(e, nullptr, 0) : (uint64_t)CDR_PAR_SOLO_LEN;
+    return v ? v : UINT64_MAX;
+  }();
   uint32_t n_solo_len = 0;
-  while (n_solo_len < pars.size() && wfs[pars[n_solo_len]].ev_len >= CDR_PAR_SOLO_LEN) n_solo_len++;
+  while (n_solo_len < pars.size() && wfs[pars[n_solo_len]].ev_len >= solo_len) n_solo_len++;
   const uint32_t solo = std::min<uint32_t>(std::max(solo_max, n_solo_len), (uint32_t)pars.size());
   // balanced PAR slices: a PAR slice's roles each walk its histories one at a time, so the
   // slice's time follows the summed lengths of its histories, and the kernel ends with its

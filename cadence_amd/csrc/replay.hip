@@ -764,6 +764,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
       t.target_run_id = trun;
       t.flags = fl;
       t._pad = 0;
+      t.version = 0;  // stateBuilder's tasks leave Version to the caller (schema.h cdr_task)
       gput(gp(O_.transfer) + CP.xfer_off + n_xt, t);
     }
     n_xt += c ? 1u : 0u;
@@ -778,6 +779,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
       t.visibility_ts = vis;
       t.attempt = att;
       t.domain_id = t.task_list = t.target_workflow_id = t.target_run_id = t.flags = t._pad = 0;
+      t.version = 0;
       gput(gp(O_.timer_tasks) + CP.ttask_off + n_tt, t);
     }
     n_tt += c ? 1u : 0u;
@@ -1967,7 +1969,8 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   // without wave slices is required, cdr_plan_slices_ex mode 0)
   const bool tasks = out->transfer != nullptr;
   if (tasks && (in->n_wave_slices > 0 || !out->timer_tasks || !out->n_tasks)) return CDR_API_EINVAL;
-  const bool fast = c->fast && in->n_fast_slices > 0 && !tasks;
+  // (the fast kernel's TASKS instantiation emits them for its slices)
+  const bool fast = c->fast && in->n_fast_slices > 0;
   // register-table kernel: LastReplicationInfo kept for clusters < CDR_REG_NCL only
   const bool reg = c->fast && c->reg &&
                    in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices + in->n_par_slices > 0 && !tasks &&
@@ -2178,7 +2181,8 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
     }
         break;
       case 4:
-    if (fst) hipLaunchKernelGGL(k_replay_fast, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), Lf);
+    if (fst && tasks) hipLaunchKernelGGL(k_replay_fast<true>, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), Lf);
+    else if (fst) hipLaunchKernelGGL(k_replay_fast<false>, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), Lf);
         break;
       case 5:
     if (reg1 && carry) {

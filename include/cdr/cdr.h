@@ -452,7 +452,16 @@ int cdr_set_plan_mode(cdr_ctx* ctx, uint32_t mode);
 
 /* Replay a device-resident sliced batch into device-resident outputs on `stream`
  * (a hipStream_t; NULL = default stream).  Asynchronous: enqueues the replay
- * kernel and the continue-as-new finalize kernel and returns. */
+ * kernel and the continue-as-new finalize kernel and returns.
+ * A context's asynchronous calls all go on ONE stream, in order: the retry lists and the
+ * side streams the kernel classes fork onto are the context's (per-context workspace), so
+ * two calls in flight on one context from different streams would share them.  Use one
+ * context per stream (per goroutine in the cgo shim).
+ * Carry-in (in->carry): loaded entries replay in the register-table kernels' carry-in
+ * instantiations (their slices) or the general kernel; an entry whose loaded state
+ * outgrows its variant is handed on, on the device, to the 12-activity variant and then to
+ * the general kernel (replay_reg.inc).  Never plan a loaded entry onto a fast or wave slice
+ * (cdr_plan_caps / cdr_plan_ndc_apply never do: CDR_CAP_LOADED). */
 int cdr_replay_sliced_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, void* stream);
 
 /* Whole pipeline for host-resident data: plan + pack + H2D + replay + D2H on `stream`

@@ -216,3 +216,20 @@ def test_gpu_tasks_fixture_histories(engine_gpu):
     got = engine_gpu.replay(b, tasks=True)
     assert not engine.compare_tasks(b, got, ref)
     assert _types(got.task_rows(0, "xfer")) == ["RecordWorkflowStarted", "DecisionTask", "DecisionTask"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_gpu_tasks_fast_kernel(engine_gpu, cfg):
+    """C1 / C2 with tasks stay on k_replay_fast (its TASKS instantiation, replay_fast.inc):
+    the task lists equal the oracle's and the general kernel's (fast path off)."""
+    b = engine.synth_batch(cfg, 1500, seed=0x5EED0310 + cfg)
+    nf, ns = engine.fast_slices(b)
+    assert nf == ns > 0  # every slice of the task plan is a fast-path slice
+    ref = _check_tasks(engine_gpu, b)
+    old = engine_gpu.set_fast_path(False)
+    try:
+        gen = engine_gpu.replay(b, tasks=True)
+    finally:
+        engine_gpu.set_fast_path(old)
+    assert not engine.compare_tasks(b, gen, ref)
