@@ -84,6 +84,7 @@ struct cdr_ctx {
   // caller's stream — so that with HIP's default 4 queues each stream has a queue of its own
   int side_of[N_SIDE] = {0, 1, 2, 3, 4, 5, 6};
   int concurrent = 1;
+  int wait_value = -1;  // hipStreamWaitValue32 usable on the device (-1: not asked yet)
   // grow-only device workspace of the host-buffer calls
   void* ws[WS_NUM] = {};
   uint64_t ws_bytes[WS_NUM] = {};

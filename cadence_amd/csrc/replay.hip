@@ -501,6 +501,9 @@ struct cdr_launch {
   // tier's rlist)
   uint32_t* olist;
   uint32_t* ocount;
+  // PAR k_replay_cls: workgroups started (the other classes' streams wait until every PAR
+  // workgroup holds its CU, so that the bulk classes' small workgroups cannot starve them)
+  uint32_t* pstart;
 };
 // result code k_replay_cls (or a carry-in k_replay_reg below the 12-activity variant) leaves
 // on an entry it hands to k_replay_reg (never returned)
@@ -1995,7 +1998,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
                        in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
-  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u, 0u, 0u, nullptr, nullptr};
+  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u, 0u, 0u, nullptr, nullptr, nullptr, nullptr, nullptr};
   // retry lists (k_replay_cls -> k_replay_reg): counters zeroed on the launch stream
   // (carry-in: a second level of lists, k_replay_reg<12-activity> -> the general kernel,
   // counters 8 + class)
@@ -2118,8 +2121,10 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
       if (cls) {
         typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, true> LC;
+        cdr_launch Lpg = with_list(Lp, 6);
+        if (rws) Lpg.pstart = rws + 15;
         hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_CLS2, true>),
-                           dim3(npar), dim3(4 * CDR_SLICE_WIDTH), LC::bytes, sx(6), with_list(Lp, 6));
+                           dim3(npar), dim3(4 * CDR_SLICE_WIDTH), LC::bytes, sx(6), Lpg);
       }
       if (!cls || cls_fb)
         hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR>),
@@ -2211,9 +2216,30 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       if (e[j] >= '0' && e[j] < '0' + cdr_ctx::N_SIDE) seen |= 1u << (e[j] - '0');
     return (e && std::strlen(e) == (size_t)cdr_ctx::N_SIDE && seen == (1u << cdr_ctx::N_SIDE) - 1u) ? e : "6012345";
   }();
+  // PAR first: a PAR workgroup takes a whole CU (four 256-VGPR waves), and once the bulk
+  // classes' one-wave workgroups hold the CUs it finds none free until they drain (measured:
+  // C4 + long histories, the PAR kernel started ~7 ms late).  Its workgroups count
+  // themselves in (rws word 15, zeroed above); every other stream waits for all of them
+  if (c->wait_value < 0) {
+    int v = 0;
+    c->wait_value = hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, c->device) == hipSuccess && v;
+  }
+  const bool gate = par && cls && !carry && rws && c->wait_value && order[0] == '6' && !std::getenv("CDR_NO_PAR_GATE");
   for (int j = 0; j < cdr_ctx::N_SIDE; j++) {
     launch_class(order[j] - '0');
     HIPCHK(hipGetLastError());
+    if (j == 0 && gate) {
+      hipStream_t waited[cdr_ctx::N_SIDE + 1];
+      int nw = 0;
+      for (int i = 0; i < 6; i++) {
+        if (!on[i] || sx(i) == sx(6)) continue;
+        bool dup = false;
+        for (int q = 0; q < nw; q++) dup |= waited[q] == sx(i);
+        if (dup) continue;
+        waited[nw++] = sx(i);
+        HIPCHK(hipStreamWaitValue32(sx(i), rws + 15, npar < 256u ? npar : 256u, hipStreamWaitValueGte, 0xFFFFFFFFu));
+      }
+    }
   }
   for (int j = 0; j < cdr_ctx::N_SIDE; j++)
     if (used[j]) {
