@@ -2101,6 +2101,39 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   for (int j = 0; j < cdr_ctx::N_SIDE; j++)
     if (used[j]) HIPCHK(hipStreamWaitEvent(c->side[j], c->fork, 0));
   auto sx = [&](int i) { return fk[i] ? c->side[so[i]] : st; };
+  static const char* order = [] {
+    const char* e = std::getenv("CDR_LAUNCH_ORDER");
+    uint32_t seen = 0;  // a permutation of the side-stream indices, or the default
+    for (size_t j = 0; e && j < std::strlen(e); j++)
+      if (e[j] >= '0' && e[j] < '0' + cdr_ctx::N_SIDE) seen |= 1u << (e[j] - '0');
+    return (e && std::strlen(e) == (size_t)cdr_ctx::N_SIDE && seen == (1u << cdr_ctx::N_SIDE) - 1u) ? e : "6012345";
+  }();
+  // big workgroups first: a PAR workgroup takes a whole CU (four 256-VGPR waves), a 12-activity
+  // class workgroup one 193-VGPR wave, and once the bulk classes' small workgroups hold the
+  // CUs they find no room until those drain (measured: C4 + long histories, the PAR kernel
+  // started ~7 ms late).  Their workgroups count themselves in (rws word 15, zeroed above);
+  // the other classes' streams wait until the PAR workgroups (or, without them, up to
+  // CDR_GATE_REG2 of the 12-activity ones) have started (CDR_NO_PAR_GATE: no gate;
+  // CDR_GATE_REG2=0: PAR only)
+  if (c->wait_value < 0) {
+    int v = 0;
+    c->wait_value = hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, c->device) == hipSuccess && v;
+  }
+  static const uint32_t gate_reg2_max = [] {
+    const char* e = std::getenv("CDR_GATE_REG2");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 1024u;
+  }();
+  const bool gate_ok = cls && !carry && rws && c->wait_value && c->concurrent && !std::getenv("CDR_NO_PAR_GATE") &&
+                       order[0] == '6' && std::strchr(order, '1') < std::strchr(order, '2') &&
+                       std::strchr(order, '1') < std::strchr(order, '3') && std::strchr(order, '1') < std::strchr(order, '4') &&
+                       std::strchr(order, '1') < std::strchr(order, '5');
+  const bool gate = gate_ok && par && fk[6];
+  // (the 12-activity class only in a batch without PAR slices: with them, holding the other
+  // classes back for it too cost C4 / C5 0.2-0.4 ms; without, it is C3's longest class and
+  // gains 5%: 5.07 -> 4.84 ms)
+  const bool gate2 = gate_ok && !par && reg2 && gate_reg2_max > 0 && fk[1] && so[1] != so[6] && !(wv && so[0] == so[1]);
+  const uint32_t gate_n = (gate ? (npar < 256u ? npar : 256u) : 0u) + (gate2 ? (gr2.x < gate_reg2_max ? gr2.x : gate_reg2_max) : 0u);
+  bool gating = gate || gate2;
   // each class's launches (its stream sx(i)); the order they are issued in decides which
   // class's workgroups take the CUs first (CDR_LAUNCH_ORDER overrides: a digit string of
   // side-stream indices, default \"6012345\": PAR, wave, 12-activity, general, small-table,
@@ -2122,7 +2155,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       if (cls) {
         typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, true> LC;
         cdr_launch Lpg = with_list(Lp, 6);
-        if (rws) Lpg.pstart = rws + 15;
+        if (rws && gate) Lpg.pstart = rws + 15;
         hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_CLS2, true>),
                            dim3(npar), dim3(4 * CDR_SLICE_WIDTH), LC::bytes, sx(6), Lpg);
       }
@@ -2145,8 +2178,10 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
       if (cls) {
         typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LC;
+        cdr_launch Lg2 = with_list(Lr2, 1);
+        if (rws && gate2) Lg2.pstart = rws + 15;
         hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_CLS2>), gr2,
-                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(1), with_list(Lr2, 1));
+                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(1), Lg2);
       }
       if (!cls || cls_fb)
         hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), cls ? retry_grid(gr2) : gr2,
@@ -2209,37 +2244,24 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
         break;
     }
   };
-  static const char* order = [] {
-    const char* e = std::getenv("CDR_LAUNCH_ORDER");
-    uint32_t seen = 0;  // a permutation of the side-stream indices, or the default
-    for (size_t j = 0; e && j < std::strlen(e); j++)
-      if (e[j] >= '0' && e[j] < '0' + cdr_ctx::N_SIDE) seen |= 1u << (e[j] - '0');
-    return (e && std::strlen(e) == (size_t)cdr_ctx::N_SIDE && seen == (1u << cdr_ctx::N_SIDE) - 1u) ? e : "6012345";
-  }();
-  // PAR first: a PAR workgroup takes a whole CU (four 256-VGPR waves), and once the bulk
-  // classes' one-wave workgroups hold the CUs it finds none free until they drain (measured:
-  // C4 + long histories, the PAR kernel started ~7 ms late).  Its workgroups count
-  // themselves in (rws word 15, zeroed above); every other stream waits for all of them
-  if (c->wait_value < 0) {
-    int v = 0;
-    c->wait_value = hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, c->device) == hipSuccess && v;
-  }
-  const bool gate = par && cls && !carry && rws && c->wait_value && order[0] == '6' && !std::getenv("CDR_NO_PAR_GATE");
   for (int j = 0; j < cdr_ctx::N_SIDE; j++) {
-    launch_class(order[j] - '0');
-    HIPCHK(hipGetLastError());
-    if (j == 0 && gate) {
+    const int i = order[j] - '0';
+    if (gating && i != 6 && i != 1 && !(i == 0 && so[0] == so[1])) {
+      // before the first ungated class: every ungated stream waits for the gated workgroups
+      gating = false;
       hipStream_t waited[cdr_ctx::N_SIDE + 1];
       int nw = 0;
-      for (int i = 0; i < 6; i++) {
-        if (!on[i] || sx(i) == sx(6)) continue;
+      for (int q = 0; q < 6; q++) {
+        if (!on[q] || q == 1 || (gate && sx(q) == sx(6)) || (gate2 && sx(q) == sx(1))) continue;
         bool dup = false;
-        for (int q = 0; q < nw; q++) dup |= waited[q] == sx(i);
+        for (int r = 0; r < nw; r++) dup |= waited[r] == sx(q);
         if (dup) continue;
-        waited[nw++] = sx(i);
-        HIPCHK(hipStreamWaitValue32(sx(i), rws + 15, npar < 256u ? npar : 256u, hipStreamWaitValueGte, 0xFFFFFFFFu));
+        waited[nw++] = sx(q);
+        HIPCHK(hipStreamWaitValue32(sx(q), rws + 15, gate_n, hipStreamWaitValueGte, 0xFFFFFFFFu));
       }
     }
+    launch_class(i);
+    HIPCHK(hipGetLastError());
   }
   for (int j = 0; j < cdr_ctx::N_SIDE; j++)
     if (used[j]) {
