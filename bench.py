@@ -624,6 +624,9 @@ def main():
     ap.add_argument("--long-stride", type=int, default=0,
                     help="configs[3] load balance: every workflow at index long_stride/2 mod long_stride is generated "
                          "at the history count limit (204,800 events); 125000 mixes 8 into 1M")
+    ap.add_argument("--tasks", action="store_true",
+                    help="also emit the stateBuilder's transfer / timer task lists (cdr_out.transfer / timer_tasks; "
+                         "the fast kernel's TASKS instantiation for C1/C2, the general kernel otherwise)")
     ap.add_argument("--carry", action="store_true",
                     help="carry-in line: each history's second half replayed onto its first half's loaded state "
                          "(--config, --wfs)")
@@ -658,11 +661,13 @@ def main():
     # the register-table slices' class-sorted blocks: emitted by the host packer beside the
     # slab (default; host packing time cls_pack_s), built on the device in every step
     # (--cls-in-step), or none (--no-cls)
-    cls_src = None if args.no_cls else "device" if args.cls_in_step else "host"
+    # (with task lists: no class blocks — the register-table kernels emit no tasks — and no
+    # wave / PAR slices, cdr_replay_sliced_async's contract for task emission)
+    cls_src = None if args.no_cls or args.tasks else "device" if args.cls_in_step else "host"
     db = DeviceBatch(torch, args.config, mine, args.seed,
-                     plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0)
-                     | (0 if args.no_par else abi.PLAN_PAR),
-                     ctx_for_cls=ctx, cls=cls_src, long_stride=args.long_stride)
+                     plan_mode=0 if args.no_wave or args.tasks else abi.PLAN_WAVE
+                     | (abi.PLAN_WAVE_ALL if args.wave_all else 0) | (0 if args.no_par else abi.PLAN_PAR),
+                     ctx_for_cls=ctx, cls=cls_src, long_stride=args.long_stride, tasks=args.tasks)
     if args.no_cls:
         L.cdr_set_cls_path(ctx, abi.CLS_OFF)
     log(f"[rank {rank}] {db.n_fast} of {db.info.n_slices} slices on the fast-path kernel, {db.n_wave} wave slices")
@@ -705,6 +710,9 @@ def main():
     # verification + the only collective: RCCL allreduce of counters and checksums
     res = db.results()
     alg_bytes, n_ok, ev_b, wf_b, row_b = db.algorithmic_bytes(res)
+    n_xfer, n_ttask = db.task_counts()
+    task_b = (n_xfer + n_ttask) * C.sizeof(abi.CdrTask)  # the task rows written (cdr_task)
+    alg_bytes += task_b
     csum = torch.zeros(1, dtype=torch.int64, device="cuda")
     L.cdr_checksum_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(csum.data_ptr()), C.c_void_p(stream))
     stats = torch.tensor([db.n_events, db.info.n_entries, n_ok, 0], dtype=torch.int64, device="cuda")
@@ -732,7 +740,8 @@ def main():
     ev_per_s = tot_events * args.steps / elapsed
     wf_per_s = tot_wfs * args.steps / elapsed
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-    workload = f"C{args.config}-{args.wfs}wf-sliced" + (f"-long{args.long_stride}" if args.long_stride else "")
+    workload = (f"C{args.config}-{args.wfs}wf-sliced" + (f"-long{args.long_stride}" if args.long_stride else "")
+                + ("-tasks" if args.tasks else ""))
     traffic, traffic_note = load_traffic(workload)
     bld = db.builders()
     names = {abi.BUILDER_LOCAL: "local", abi.BUILDER_2DC: "2DC", abi.BUILDER_NDC: "NDC"}
@@ -756,9 +765,11 @@ def main():
                      "traffic_note": traffic_note or traffic.get("source"),
                      # HBM bytes actually moved per launch (PMC) / the live kernel time
                      "traffic_gbs": traffic["bytes_per_launch"] / (kern_ms / 1e3) / 1e9 if traffic else None,
-                     "kernel": "k_replay_fast" if args.config in (1, 2) and not args.no_fast_path else "k_replay*",
+                     "kernel": ("k_replay_fast" if args.config in (1, 2) and not args.no_fast_path else "k_replay*")
+                     + ("<TASKS>" if args.tasks else ""),
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": alg_bytes,
-                     "bytes_breakdown": {"events": ev_b, "per_workflow": wf_b, "pending_rows": row_b},
+                     "bytes_breakdown": {"events": ev_b, "per_workflow": wf_b, "pending_rows": row_b,
+                                         "tasks": task_b},
                      "stream_copy_peak_gbs": peak_meas},
         "cpu_baseline": cpu,
         "refresh": refresh,
@@ -775,6 +786,7 @@ def main():
                  # one replay step
                  "per_batch_s": db.pack_s + db.cls_pack_s + db.h2d_s + ms_per_step / 1e3,
                  "per_batch_events_per_s": db.n_events / (db.pack_s + db.cls_pack_s + db.h2d_s + ms_per_step / 1e3)},
+        "tasks": {"transfer": n_xfer, "timer": n_ttask, "bytes": task_b} if args.tasks else None,
         "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_workflows": tot_ok,
         "parity_checked": bool(parity) and parity["mismatched_entries_all_ranks"] == 0,
         "parity": parity,

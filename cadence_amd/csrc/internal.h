@@ -27,6 +27,8 @@ struct loaded_rows {
 };
 // `loaded` (nullable): the entry replays onto that state; its rows count into the peak
 // live sets and the register-table envelope.
+// upper bounds of the transfer / timer tasks an entry's events append (host.cpp)
+void task_caps(const cdr_event* ev, uint64_t n, uint32_t* xfer, uint32_t* ttask);
 void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* c, const cdr_kv* kvs = nullptr,
               const cdr_reset_point* rps = nullptr, const loaded_rows* loaded = nullptr);
 

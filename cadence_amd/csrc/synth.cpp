@@ -754,6 +754,10 @@ void size_pass(const cdr_synth_params& P, Sizes& S, int threads, bool want_caps 
       cdr_internal::caps_one(o.newrun.data(), o.newrun.size(),
                              o.newrun_ndc ? (uint32_t)CDR_BUILDER_NDC : (uint32_t)CDR_BUILDER_2DC, &S.cap_nr[w],
                              o.kvs.data(), o.rps.data());
+      // task-list capacities too (cdr_out.transfer / timer_tasks: bench.py --tasks)
+      cdr_internal::task_caps(o.ev.data(), o.ev.size(), &S.cap_ev[w].xfer_cap, &S.cap_ev[w].ttask_cap);
+      if (!o.newrun.empty())
+        cdr_internal::task_caps(o.newrun.data(), o.newrun.size(), &S.cap_nr[w].xfer_cap, &S.cap_nr[w].ttask_cap);
       S.aw_ev[w] = arena_of(o.ev);
       S.aw_nr[w] = arena_of(o.newrun);
     }
@@ -901,6 +905,8 @@ int cdr_synth_sliced_plan(const cdr_synth_params* p, cdr_synth_plan_info* info) 
       z.totals.vh += cs[j]->vh_cap;
       z.totals.rp += cs[j]->rp_cap;
       z.totals.sa += cs[j]->sa_cap;
+      z.totals.xfer += cs[j]->xfer_cap;
+      z.totals.ttask += cs[j]->ttask_cap;
       cdr_wf_desc d{};
       d.ev_len = j == 0 ? S.n_ev[w] : S.n_nr[w];
       lens.push_back(d);
@@ -960,6 +966,10 @@ int cdr_synth_sliced_fill(const cdr_synth_params* p, cdr_slices* o, cdr_wf_desc*
       t.rp += c.rp_cap;
       c.sa_off = t.sa;
       t.sa += c.sa_cap;
+      c.xfer_off = t.xfer;
+      t.xfer += c.xfer_cap;
+      c.ttask_off = t.ttask;
+      t.ttask += c.ttask_cap;
       caps[ent + j] = c;
       cdr_wf_desc d{};
       d.ev_len = j == 0 ? S.n_ev[w] : S.n_nr[w];

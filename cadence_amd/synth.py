@@ -35,12 +35,14 @@ class DeviceBatch:
     """Synthetic batch generated straight into the sliced layout, uploaded to HBM."""
 
     def __init__(self, torch, config, index_map, seed, target_len=0, plan_mode=abi.PLAN_WAVE | abi.PLAN_PAR, ctx_for_cls=None,
-                 cls="host", long_stride=0):
+                 cls="host", long_stride=0, tasks=False):
         """cls: where the register-table slices' class-sorted blocks (replay_cls.inc) come
         from — "host": the packer emits them beside the slab (cdr_plan_cls / cdr_pack_cls,
         host packing time `cls_pack_s`, uploaded with the slab); "device": built on the
         device after the upload (cdr_cls_plan_async / cdr_cls_pack_async on ctx_for_cls,
-        `cls_s`); None: no blocks (k_replay_reg alone)."""
+        `cls_s`); None: no blocks (k_replay_reg alone).  tasks: also the stateBuilder's
+        transfer / timer task lists (cdr_out.transfer / timer_tasks / n_tasks, sized by the
+        synthetic plan's task capacities)."""
         if cls not in ("host", "device", None):
             raise ValueError(f"cls={cls!r}")
         if cls == "device" and not ctx_for_cls:
@@ -174,6 +176,9 @@ class DeviceBatch:
                  "cancel": tot.cancel * C.sizeof(abi.CdrCancelInfo),
                  "signal": tot.signal * C.sizeof(abi.CdrSignalInfo),
                  "rp": tot.rp * C.sizeof(abi.CdrResetPoint), "sa": tot.sa * C.sizeof(abi.CdrKV)}
+        if tasks:
+            sizes.update({"transfer": tot.xfer * C.sizeof(abi.CdrTask), "timer_tasks": tot.ttask * C.sizeof(abi.CdrTask),
+                          "n_tasks": 2 * info.n_entries * 4})
         self.out_bytes = sum(sizes.values())
         self.out_t = {}
         for k, nb in sizes.items():
@@ -239,6 +244,14 @@ class DeviceBatch:
         n = self.info.n_entries
         raw = self.out_t["result"][: n * C.sizeof(abi.CdrWfResult)].cpu().numpy().copy()
         return (abi.CdrWfResult * n).from_buffer(raw)
+
+    def task_counts(self):
+        """(transfer, timer) tasks emitted by the last replay (cdr_out.n_tasks, 2 per entry)."""
+        if "n_tasks" not in self.out_t:
+            return 0, 0
+        n = self.out_t["n_tasks"][: 2 * self.info.n_entries * 4].view(self.torch.int32).view(-1, 2).to(self.torch.int64)
+        t = n.sum(0).tolist()
+        return int(t[0]), int(t[1])
 
     def algorithmic_bytes(self, res):
         ev_bytes = int((self.type_counts[:42] * (48 + A_TYPE[:42])).sum())
