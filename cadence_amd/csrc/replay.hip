@@ -2123,7 +2123,10 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
     const char* e = std::getenv("CDR_GATE_REG2");
     return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 1024u;
   }();
-  const bool gate_ok = cls && !carry && rws && c->wait_value && c->concurrent && !std::getenv("CDR_NO_PAR_GATE") &&
+  // (not under a counter-collecting profiler, which serializes dispatches: a stream waiting
+  // on a value another queue's kernel writes would wait on a kernel it holds back)
+  static const bool gate_env = !std::getenv("CDR_NO_PAR_GATE") && !std::getenv("ROCPROF_COUNTER_COLLECTION");
+  const bool gate_ok = cls && !carry && rws && c->wait_value && c->concurrent && gate_env &&
                        order[0] == '6' && std::strchr(order, '1') < std::strchr(order, '2') &&
                        std::strchr(order, '1') < std::strchr(order, '3') && std::strchr(order, '1') < std::strchr(order, '4') &&
                        std::strchr(order, '1') < std::strchr(order, '5');

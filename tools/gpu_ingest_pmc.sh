@@ -3,6 +3,9 @@
 set -o pipefail
 out=gpurun_out/${1:-igp}; mkdir -p $out
 export TMPDIR=/tmp
+# counter collection serializes the dispatches: the launch gate (a stream waiting on a
+# value another queue's kernel writes) would wait on a kernel the profiler holds back
+export CDR_NO_PAR_GATE=1
 run() { local name=$1; shift
   timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d "$out/$name" -o run -- \
     python3 tools/ingest_bench.py --config 2 --wfs 100000 --reps 1 > "$out/$name.log" 2>&1; }

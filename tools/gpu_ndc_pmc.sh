@@ -8,6 +8,9 @@ tag=${1:-ndc}; n=${2:-1000000}
 out=gpurun_out/${tag}_pmc; mkdir -p $out
 sha1sum cadence_amd/libcdr.so | cut -d' ' -f1 > $out/lib_sha1
 export TMPDIR=/tmp
+# counter collection serializes the dispatches: the launch gate (a stream waiting on a
+# value another queue's kernel writes) would wait on a kernel the profiler holds back
+export CDR_NO_PAR_GATE=1
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 400 rocprofv3 --pmc "$@" --output-format csv -d "$out/$name" -o run -- \

@@ -12,6 +12,9 @@ out=gpurun_out/${tag}_pmc
 mkdir -p "$out"
 sha1sum "$lib" | cut -d' ' -f1 > "$out/lib_sha1"  # bench.py uses the summary only for this build
 export TMPDIR=/tmp
+# counter collection serializes the dispatches: the launch gate (a stream waiting on a
+# value another queue's kernel writes) would wait on a kernel the profiler holds back
+export CDR_NO_PAR_GATE=1
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$out/$name" -o run -- \
