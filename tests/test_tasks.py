@@ -233,3 +233,47 @@ def test_gpu_tasks_fast_kernel(engine_gpu, cfg):
     finally:
         engine_gpu.set_fast_path(old)
     assert not engine.compare_tasks(b, gen, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [2, 3])
+def test_gpu_tasks_device_batch(engine_gpu, cfg):
+    """The `bench.py --tasks` path: a synthetic sliced batch carrying task capacities
+    (DeviceBatch(tasks=True), a plan without wave / PAR slices, no class blocks) replayed by
+    cdr_replay_sliced_async — C2 on k_replay_fast<TASKS>, C3 on the general kernel — equals
+    the oracle's task lists for the same workflows, entry by entry and byte for byte."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    import oracle
+    from cadence_amd.synth import DeviceBatch
+    n, seed = 1500, 0x5EED0410 + cfg
+    db = DeviceBatch(torch, cfg, np.arange(n, dtype=np.uint32), seed, plan_mode=0, cls=None, tasks=True)
+    L = abi.lib()
+    ctx = L.cdr_create(torch.cuda.current_device(), None)
+    try:
+        stream = torch.cuda.current_stream().cuda_stream
+        assert L.cdr_replay_sliced_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(stream)) == 0
+        torch.cuda.synchronize()
+    finally:
+        L.cdr_destroy(ctx)
+    ref = oracle.replay(engine.synth_batch(cfg, n, seed), tasks=True)
+    ne = db.info.n_entries
+    assert ne == ref.n_wfs
+    nt = db.out_t["n_tasks"][: 8 * ne].view(torch.int32).cpu().numpy().reshape(-1, 2)
+    bufs = {"xfer": db.out_t["transfer"].cpu().numpy().tobytes(), "ttask": db.out_t["timer_tasks"].cpu().numpy().tobytes()}
+    sz = C.sizeof(abi.CdrTask)
+    bad, total = [], 0
+    for w in range(ne):
+        assert ref.result[w].code == abi.OK
+        cap = db.h_caps[w]
+        for kind, off, k in (("xfer", cap.xfer_off, 0), ("ttask", cap.ttask_off, 1)):
+            want = [bytes(r) for r in ref.task_rows(w, kind)]
+            got = [bufs[kind][(off + j) * sz:(off + j + 1) * sz] for j in range(int(nt[w, k]))]
+            total += len(want)
+            if got != want:
+                bad.append((w, kind, len(got), len(want)))
+    assert not bad, bad[:5]
+    assert total > n
