@@ -1968,21 +1968,22 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const size_t lds = (size_t)(la * CDR_ACT_PLANES + lt * CDR_TIM_PLANES) * CDR_SLICE_WIDTH * sizeof(uint64_t);
   const bool spill = in->max_act_slots > la || in->max_tim_slots > lt;
   const uint32_t blocks = in->ev.n_slices;
-  // task emission lives in the general kernel only: every slice goes there (a plan
-  // without wave slices is required, cdr_plan_slices_ex mode 0)
+  // task emission: the general kernel, the fast kernel's and the register-table kernels'
+  // TASKS instantiations (a plan without wave slices is required; no class blocks, no
+  // loaded state on the register-table kernels)
   const bool tasks = out->transfer != nullptr;
   if (tasks && (in->n_wave_slices > 0 || !out->timer_tasks || !out->n_tasks)) return CDR_API_EINVAL;
   // (the fast kernel's TASKS instantiation emits them for its slices)
   const bool fast = c->fast && in->n_fast_slices > 0;
   // register-table kernel: LastReplicationInfo kept for clusters < CDR_REG_NCL only
   const bool reg = c->fast && c->reg &&
-                   in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices + in->n_par_slices > 0 && !tasks &&
-                   in->cluster.n_clusters <= (int)CDR_REG_NCL;
+                   in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices + in->n_par_slices > 0 &&
+                   !(tasks && in->carry) && in->cluster.n_clusters <= (int)CDR_REG_NCL;
   // carry-in batches (cdr_dev_batch.carry): the register-table slices replay in the carry-in
   // instantiations of k_replay_reg, each class followed by its hand-on chain (below)
   const bool carry = in->carry != nullptr;
   // class-decomposed replay of the register-table slices (their class-sorted blocks)
-  const bool cls = reg && !carry && c->cls && in->cls_slab && in->cls_row0 && in->cls_rows;
+  const bool cls = reg && !carry && !tasks && c->cls && in->cls_slab && in->cls_row0 && in->cls_rows;
   const bool cls_fb = c->cls != 2;  // 2 (tests): no k_replay_reg pass for the CLS_RETRY entries
   auto retry_of = [](cdr_launch x) {
     x.retry = 1u;
@@ -2162,7 +2163,10 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
         hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_CLS2, true>),
                            dim3(npar), dim3(4 * CDR_SLICE_WIDTH), LC::bytes, sx(6), Lpg);
       }
-      if (!cls || cls_fb)
+      if (tasks)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_REG, false, true>),
+                           dim3(npar), dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6), Lp);
+      else if (!cls || cls_fb)
         hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR>),
                            cls ? retry_grid(dim3(npar)) : dim3(npar), dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6),
                            cls ? retry_of(with_list(Lp, 6)) : Lp);
@@ -2186,7 +2190,10 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
         hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_CLS2>), gr2,
                            dim3(CDR_SLICE_WIDTH), LC::bytes, sx(1), Lg2);
       }
-      if (!cls || cls_fb)
+      if (tasks)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_REG, false, true>), gr2,
+                           dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), Lr2);
+      else if (!cls || cls_fb)
         hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), cls ? retry_grid(gr2) : gr2,
                          dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), cls ? retry_of(with_list(Lr2, 1)) : Lr2);
     }
@@ -2218,7 +2225,10 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
         hipLaunchKernelGGL((k_replay_cls<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_CLS0>), gr0,
                            dim3(CDR_SLICE_WIDTH), LC::bytes, sx(3), with_list(Lr0, 3));
       }
-      if (!cls || cls_fb)
+      if (tasks)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_REG, false, true>), gr0,
+                           dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), Lr0);
+      else if (!cls || cls_fb)
         hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), cls ? retry_grid(gr0) : gr0,
                          dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), cls ? retry_of(with_list(Lr0, 3)) : Lr0);
     }
@@ -2240,7 +2250,10 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
         hipLaunchKernelGGL((k_replay_cls<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_CLS>), gr1,
                            dim3(CDR_SLICE_WIDTH), LC::bytes, sx(5), with_list(Lr1, 5));
       }
-      if (!cls || cls_fb)
+      if (tasks)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_REG, false, true>), gr1,
+                           dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), Lr1);
+      else if (!cls || cls_fb)
         hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), cls ? retry_grid(gr1) : gr1,
                          dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), cls ? retry_of(with_list(Lr1, 5)) : Lr1);
     }
