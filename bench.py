@@ -644,8 +644,15 @@ def main():
     world, rank, local = dist_env()
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL (backend "nccl") between the GPUs of the node; CDR_BENCH_BACKEND=gloo rehearses
+        # the multi-rank path on a box with fewer GPUs than ranks (ranks share a device, the
+        # counters reduce on the host; the timings then mean nothing)
+        backend = os.environ.get("CDR_BENCH_BACKEND", "nccl")
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()) if backend == "gloo" else local)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         dist = None
         torch.cuda.set_device(0)
@@ -715,8 +722,10 @@ def main():
     alg_bytes += task_b
     csum = torch.zeros(1, dtype=torch.int64, device="cuda")
     L.cdr_checksum_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(csum.data_ptr()), C.c_void_p(stream))
+    coll_dev = "cpu" if dist and os.environ.get("CDR_BENCH_BACKEND", "nccl") == "gloo" else "cuda"
     stats = torch.tensor([db.n_events, db.info.n_entries, n_ok, 0], dtype=torch.int64, device="cuda")
     stats[3] = csum[0]
+    stats = stats.to(coll_dev)
     (tot_events, tot_wfs, tot_ok, checksum), elapsed = reduce_step(dist, torch, stats, elapsed)
     if tot_ok != tot_wfs:
         log(f"WARNING: {tot_wfs - tot_ok} workflows did not replay OK")
@@ -725,7 +734,7 @@ def main():
     if parity:
         log(f"[rank {rank}] parity: {parity['mismatched_entries']} of {parity['entries']} entries differ from the "
             f"oracle ({parity['seconds']:.1f}s)")
-        flag = torch.tensor([parity["mismatched_entries"], parity["entries"]], dtype=torch.int64, device="cuda")
+        flag = torch.tensor([parity["mismatched_entries"], parity["entries"]], dtype=torch.int64, device=coll_dev)
         if dist:
             dist.all_reduce(flag)
         parity["mismatched_entries_all_ranks"], parity["entries_all_ranks"] = [int(x) for x in flag.tolist()]
