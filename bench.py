@@ -16,6 +16,9 @@ task per workflow on the host's cores over a bounded sample.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--wfs M] [--config C]
        (N>1: torchrun --nproc-per-node N bench.py --gpus N ...)
+Other lines: --long-stride 125000 (configs[3]: histories at the 204,800-event count limit
+mixed in), --tasks (with the stateBuilder task lists), --carry (replay onto a loaded
+state), --ndc-forks (configs[4]'s conflict-resolution rounds).
 """
 from __future__ import annotations
 
