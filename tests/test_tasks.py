@@ -277,3 +277,37 @@ def test_gpu_tasks_device_batch(engine_gpu, cfg):
                 bad.append((w, kind, len(got), len(want)))
     assert not bad, bad[:5]
     assert total > n
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+def test_synth_sliced_task_caps(cfg):
+    """The synthetic sliced plan's task capacities (bench.py --tasks) are cdr_plan_caps's for
+    the same workflows, entry by entry, with prefix offsets in entry order."""
+    import ctypes as C
+
+    import numpy as np
+    L = abi.lib()
+    n, seed = 700, 0x5EED0420 + cfg
+    idx = np.arange(n, dtype=np.uint32)
+    p = abi.CdrSynthParams(config=cfg, n_wfs=n, seed=seed, target_len=0, max_len=0, error_rate=0.0, builder=-1,
+                           rebuild=0, index_map=idx.ctypes.data, plan_mode=0, long_stride=0)
+    info = abi.CdrSynthPlanInfo()
+    assert L.cdr_synth_sliced_plan(C.byref(p), C.byref(info)) == 0
+    slab = np.empty(info.n_rows * 64 * abi.EL_BYTES, np.uint8)
+    lane = np.empty(info.n_slices * 64, np.int32)
+    slen, row0 = np.empty(info.n_slices, np.uint32), np.empty(info.n_slices, np.uint64)
+    z = [np.zeros(info.n_slices, t) for t in (np.uint64, np.uint32, np.uint32, np.uint32)]
+    arena = np.empty(max(1, info.arena_words), np.uint64)
+    wfs, caps = (abi.CdrWfDesc * info.n_entries)(), (abi.CdrWfCaps * info.n_entries)()
+    kvs, rps = np.zeros(max(1, info.n_kvs) * 2, np.uint32), (abi.CdrResetPoint * max(1, info.n_rps))()
+    s = abi.CdrSlices(n_slices=info.n_slices, n_rows=info.n_rows, arena_words=info.arena_words)
+    s.slice_row0, s.slice_len, s.lane_wf, s.slab, s.arena = (row0.ctypes.data, slen.ctypes.data, lane.ctypes.data,
+                                                             slab.ctypes.data, arena.ctypes.data)
+    s.slice_scratch_off, s.slice_act_slots, s.slice_tim_slots, s.slice_flags = [a.ctypes.data for a in z]
+    meta = abi.CdrBatch()
+    assert L.cdr_synth_sliced_fill(C.byref(p), C.byref(s), wfs, caps, kvs.ctypes.data, rps, C.byref(meta), 4) == 0
+    ref = engine.plan(engine.synth_batch(cfg, n, seed))
+    assert info.totals.xfer == ref.totals.xfer and info.totals.ttask == ref.totals.ttask
+    for w in range(info.n_entries):
+        a, b = caps[w], ref.caps[w]
+        assert (a.xfer_cap, a.ttask_cap, a.xfer_off, a.ttask_off) == (b.xfer_cap, b.ttask_cap, b.xfer_off, b.ttask_off), w
