@@ -2234,7 +2234,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
     }
         break;
       case 4:
-    if (fst && tasks) hipLaunchKernelGGL(k_replay_fast<true>, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), Lf);
+    if (fst && tasks) hipLaunchKernelGGL(k_replay_fast<true>, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES + FAST_TBUF_BYTES, sx(4), Lf);
     else if (fst) hipLaunchKernelGGL(k_replay_fast<false>, gf, dim3(CDR_SLICE_WIDTH), FAST_LDS_BYTES, sx(4), Lf);
         break;
       case 5:
@@ -2309,7 +2309,7 @@ uint32_t cdr_build_flags(void) {
   if (CDR_PAR_PRIO != 0 || CDR_FDEPTH != 2 || CDR_DEPTH != 1 || CDR_TYPED != 1 || CDR_FAST_DELTA != 1 ||
       CDR_VHBF != 1 || CDR_CLS_DEPTH != 1 || CDR_CLS_PDEPTH != 4 || CDR_CLS_DEPTH_PAR != 4 ||
       CDR_CLS_PDEPTH_PAR != 16 || CDR_WPE_FAST != 3 || CDR_WPE != 3 || CDR_WPE_CLS != 4 || CDR_WPE_CLS0 != 4 ||
-      CDR_WPE_CLS2 != 2 || FAST_CK != 8u)
+      CDR_WPE_CLS2 != 2 || FAST_CK != 8u || CDR_FAST_TBUF != 8 || CDR_WPE_FAST_TBUF != 2)
     f |= 2u;
   return f;
 }
