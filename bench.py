@@ -270,6 +270,32 @@ def cpu_baseline(config, n_wfs, seed, min_seconds=10.0):
             "single_thread_events_per_s": res[1], "workflows_per_s": res[threads] / (n_ev / max(1, n_wfs))}
 
 
+def init_dist(torch):
+    """One process per GPU (torch.distributed.run's env): (dist or None, world, rank, local
+    rank, the device the counters reduce on).  RCCL (backend "nccl") between the GPUs of the
+    node; CDR_BENCH_BACKEND=gloo rehearses the multi-rank path on a box with fewer GPUs than
+    ranks (ranks share a device, the counters reduce on the host; the timings then mean
+    nothing)."""
+    world, rank, local = dist_env()
+    if world > 1:
+        import torch.distributed as dist
+        backend = os.environ.get("CDR_BENCH_BACKEND", "nccl")
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()) if backend == "gloo" else local)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, world, rank, local, "cpu" if backend == "gloo" else "cuda"
+    torch.cuda.set_device(0)
+    return None, 1, 0, 0, "cuda"
+
+
+def finish_dist(dist):
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def reduce_step(dist, torch, stats, elapsed: float):
     """The multi-GPU step's only collective: the sum over ranks of the
     int64 counters [events, entries, OK entries, cdr_checksum_async digest sum] (the
@@ -292,18 +318,12 @@ def load_traffic(workload):
     """PMC HBM bytes per launch (tools/pmc.sh + tools/traffic.py) for this workload, used
     only when they were collected on this very build of libcdr.so (same SHA-1); else
     (None, reason)."""
-    d = None
-    for name in (f"traffic_{workload}.json", "traffic_latest.json"):
-        try:
-            d = json.load(open(os.path.join(HERE, "profiles", name)))
-        except Exception:
-            continue
-        if d.get("workload") == workload:
-            break
-    if d is None:
-        return None, "no PMC summary"
+    try:
+        d = json.load(open(os.path.join(HERE, "profiles", f"traffic_{workload}.json")))
+    except (OSError, ValueError):
+        return None, "no PMC summary for this workload"
     if d.get("workload") != workload:
-        return None, f"PMC summary is for {d.get('workload')}"
+        return None, "no PMC summary for this workload"
     if d.get("lib_sha1") != lib_sha1():
         return None, "stale: PMC summary from another build of libcdr.so"
     return d, None
@@ -326,6 +346,125 @@ def parity_check(db, ctx, stream, config, mine, seed, long_stride=0):
                       "oracle/digest_ref.cpp), CopyToPersistence mutableStateBuilder.go:257-270"}
 
 
+def compare_task_lists(got, nt, caps_g, ref, caps_r, ne):
+    """Entries (of the first ne) whose transfer / timer task lists differ, byte for byte:
+    got = {"xfer", "ttask"} device buffers as bytes, nt = their [n_xfer, n_timer] per entry,
+    caps_g / caps_r the two plans' task offsets, ref the oracle's Outputs(tasks=True).
+    Returns (mismatched entries, the oracle's task count)."""
+    sz = C.sizeof(abi.CdrTask)
+    want = {k: bytes(ref.tasks[k]) for k in ("xfer", "ttask")}
+    bad, n_tasks = [], 0
+    for w in range(ne):
+        for k, kind, off_g, off_r in ((0, "xfer", caps_g[w].xfer_off, caps_r[w].xfer_off),
+                                      (1, "ttask", caps_g[w].ttask_off, caps_r[w].ttask_off)):
+            n_r = int(ref.tasks["n"][2 * w + k])
+            n_tasks += n_r
+            g = got[kind][int(off_g) * sz:(int(off_g) + int(nt[w, k])) * sz]
+            r = want[kind][int(off_r) * sz:(int(off_r) + n_r) * sz]
+            if g != r:
+                bad.append(w)
+                break
+    return bad, n_tasks
+
+
+def task_parity(db, config, mine, seed, long_stride=0, sample=20000):
+    """The --tasks line's task lists (cdr_out.transfer / timer_tasks) against the oracle's
+    (oracle.replay(tasks=True), stateBuilder.go:613-804) for the entries of the first
+    `sample` workflows of this rank's population, entry by entry and byte for byte (the
+    per-entry state digests of parity_check do not cover the task lists).  Runs after the
+    timed region."""
+    import oracle
+    from cadence_amd import engine
+    t0 = time.perf_counter()
+    m = min(len(mine), sample)
+    sb = engine.synth_batch(config, m, seed, index_map=np.asarray(mine[:m], np.uint32), long_stride=long_stride)
+    pl = engine.plan(sb)
+    ref = oracle.replay(sb, pl, threads=host_cores()[0], tasks=True)
+    ne = sb.n_wfs  # the DeviceBatch's first ne entries are these workflows' (natural order)
+    sz = C.sizeof(abi.CdrTask)
+    nt = db.out_t["n_tasks"][: 8 * ne].view(db.torch.int32).cpu().numpy().reshape(-1, 2)
+    caps = db.h_caps
+    hi_x = int(caps[ne - 1].xfer_off) + int(nt[ne - 1, 0]) if ne else 0
+    hi_t = int(caps[ne - 1].ttask_off) + int(nt[ne - 1, 1]) if ne else 0
+    got = {"xfer": db.out_t["transfer"][: hi_x * sz].cpu().numpy().tobytes(),
+           "ttask": db.out_t["timer_tasks"][: hi_t * sz].cpu().numpy().tobytes()}
+    bad, n_tasks = compare_task_lists(got, nt, caps, ref, pl.caps, ne)
+    return {"checked": True, "sample_workflows": m, "entries": ne, "tasks": n_tasks,
+            "mismatched_entries": len(bad), "first_mismatches": bad[:8], "seconds": time.perf_counter() - t0,
+            "method": "byte-for-byte task lists (transfer + timer) of the first sample workflows' entries, GPU vs "
+                      "oracle.replay(tasks=True)"}
+
+
+def canonical_event_bytes(batch) -> np.ndarray:
+    """SURVEY 8(d) canonical input bytes of every entry of a host batch: sum over its events
+    of 48 B core + A[type]."""
+    from cadence_amd.synth import A_TYPE
+    words = C.sizeof(abi.CdrEvent) // 4
+    n = batch.n_wfs
+    if not len(batch.events):
+        return np.zeros(n, np.int64)
+    ty = np.frombuffer(batch.events, dtype=np.uint32).reshape(-1, words)[:, abi.CdrEvent.type.offset // 4]
+    cum = np.concatenate([[0], np.cumsum(48 + A_TYPE[np.minimum(ty, 255)])])
+    wf = np.frombuffer(batch.wfs, dtype=np.uint8).reshape(n, C.sizeof(abi.CdrWfDesc))
+
+    def col(name):
+        o = getattr(abi.CdrWfDesc, name).offset
+        return wf[:, o:o + 8].copy().view(np.uint64).ravel().astype(np.int64)
+    off, ln = col("ev_off"), col("ev_len")
+    return cum[off + ln] - cum[off]
+
+
+def ndc_cpu_baseline(n_sample, seed, min_seconds=10.0):
+    """configs[4]'s CPU leg: oracle.ndc_replicate (the restated stateRebuilder /
+    conflict-resolution rounds, nDCConflictResolver.go:117-184, nDCStateRebuilder.go:92-160)
+    on the box's host cores over a sample of the same forked population; events counted as
+    the GPU line counts them (base + every rebuilt branch + every applied task)."""
+    import oracle
+    from cadence_amd import ndc
+    base, rebuild, forks = ndc.synth_forked(5, n_sample, seed)
+    threads, how = host_cores()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        _, _, _, decs, rounds = oracle.ndc_replicate(base, rebuild, forks, threads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds or reps >= 50:
+            break
+    ev = ndc_counts(base, rebuild, forks, rounds, decs)[0]
+    return {"value": ev * reps / el, "unit": "events/s", "cores": threads, "cores_source": how, "kind": "port",
+            "sample": f"forked config 5: {n_sample} workflows (base + 2 fork rounds), oracle.ndc_replicate repeated "
+                      f"for >= {min_seconds:.0f} s; the Go stateRebuilder cannot run here (no Go toolchain)",
+            "workflows_per_s": n_sample * reps / el}
+
+
+def ndc_counts(base, rebuild, forks, rounds, decs):
+    """What one replication run of a (shard of the) forked population replays: (events,
+    base events, events per round, decision counts per round, SURVEY 8(d) canonical event
+    bytes).  A round replays the rebuilt branch of every workflow whose rebuild ran and
+    succeeded and the task's events of every workflow whose apply ran and succeeded (a SKIP /
+    BACKFILL decision, a failed branch step or rebuild leaves the apply record CDR_NOT_RUN or
+    failed: none of its events is counted).  `rounds` / `decs` as DeviceReplicator.run (or
+    oracle.ndc_replicate) return them."""
+    n = base.n_wfs
+
+    def codes(out):
+        return np.frombuffer(out.result, dtype=np.int32).reshape(-1, C.sizeof(abi.CdrWfResult) // 4)[:n, 0]
+    ev_base = int(sum(base.wfs[w].ev_len for w in range(n)))
+    lens_rb = np.array([rebuild.wfs[w].ev_len for w in range(n)], np.int64)
+    cb_rb = canonical_event_bytes(rebuild)
+    ev_bytes = int(canonical_event_bytes(base).sum())
+    ev_rounds, acts = [], {}
+    for k, (fb, _, _) in enumerate(forks):
+        rb_out, ap_out = rounds[k]
+        ok_ap, ok_rb = codes(ap_out) == abi.OK, codes(rb_out) == abi.OK
+        lens_fb = np.array([fb.wfs[w].ev_len for w in range(n)], np.int64)
+        ev_rounds.append(int(lens_fb[ok_ap].sum() + lens_rb[ok_rb].sum()))
+        ev_bytes += int(canonical_event_bytes(fb)[ok_ap].sum() + cb_rb[ok_rb].sum())
+        acts[f"round{k}"] = {abi.NDC_ACTIONS[a]: int(c) for a, c in
+                             zip(*np.unique([decs[k][w].action for w in range(n)], return_counts=True))}
+    return ev_base + sum(ev_rounds), ev_base, ev_rounds, acts, ev_bytes
+
+
 def ndc_forks_line(args):
     """configs[4]'s conflict-resolution path at scale: the forked config-5 population
     (cadence_amd.ndc.synth_forked: a base branch and two fork rounds per workflow,
@@ -334,61 +473,71 @@ def ndc_forks_line(args):
     92-160).  A step = the base branch replayed into the state buffer + both rounds (branch,
     rebuild replay + refreshTasks + verify, apply onto the rebuilt state in memory or the loaded
     one, VersionHistories sync).  value = events replayed per second (base + rebuilt + applied
-    events); parity: the final state, the VersionHistories and each round's decisions against
-    oracle.ndc_replicate, entry by entry."""
+    events) over all ranks; parity: the final state, the VersionHistories and each round's
+    decisions against oracle.ndc_replicate, entry by entry, on every rank.
+    N > 1 (torch.distributed.run): each rank replicates the workflows of its historyShardIDs
+    (Fingerprint32(workflowID) % 16384, greedy on events, as the headline line) — no
+    data-path collective; one all-reduce of [events, workflows, OK states, state digest sum],
+    the max of the timed region and the parity counts closes the run."""
     import torch
     from cadence_amd import engine, ndc
-    torch.cuda.set_device(0)
-    eng = engine.Engine(0)
-    n = args.wfs
+    dist, world, rank, local, coll_dev = init_dist(torch)
+    eng = engine.Engine(torch.cuda.current_device())
+    total = args.wfs * world
+    mine, load = assign_shards(total, world, rank, workflow_weights(5, total, args.seed))
+    n = len(mine)
     t0 = time.perf_counter()
     import threading
     beat = threading.Event()
 
     def heartbeat():  # long host phases at 1M workflows: a progress line every minute
         while not beat.wait(60):
-            log(f"NDC forks: {time.perf_counter() - t0:.0f}s")
+            log(f"[rank {rank}] NDC forks: {time.perf_counter() - t0:.0f}s")
     threading.Thread(target=heartbeat, daemon=True).start()
-    base, rebuild, forks = ndc.synth_forked(5, n, args.seed)
-    log(f"NDC forks: synthesized {n} forked workflows ({time.perf_counter() - t0:.0f}s)")
+    base, rebuild, forks = ndc.synth_forked(5, n, args.seed, index_map=mine)
+    log(f"[rank {rank}] NDC forks: synthesized {n} of {total} forked workflows ({time.perf_counter() - t0:.0f}s)")
     rep = ndc.DeviceReplicator(eng, base, rebuild, forks)
     setup_s = time.perf_counter() - t0
-    log(f"NDC forks: {n} workflows, host synth + plan + upload {setup_s:.1f}s")
+    log(f"[rank {rank}] NDC forks: {n} workflows, host synth + plan + upload {setup_s:.1f}s")
     state, vhs, pool, decs, rounds = rep.run()  # warm-up (and the decisions the events count from)
-    ev_base = rep.events[0]
-    lens_rb = np.array([rebuild.wfs[w].ev_len for w in range(n)], np.int64)
-    # events a round replays: the rebuilt branch of every workflow whose rebuild ran and
-    # succeeded, and the task's events of every workflow whose apply ran and succeeded (a
-    # SKIP / BACKFILL decision, a failed branch step or rebuild leaves the apply record
-    # CDR_NOT_RUN or failed: none of its events is counted)
-    def codes(out):
-        return np.frombuffer(out.result, dtype=np.int32).reshape(-1, C.sizeof(abi.CdrWfResult) // 4)[:n, 0]
-    ev_rounds, acts = [], {}
-    for k, (fb, _, _) in enumerate(forks):
-        rb_out, ap_out = rounds[k]
-        lens_fb = np.array([fb.wfs[w].ev_len for w in range(n)], np.int64)
-        ev_rounds.append(int(lens_fb[codes(ap_out) == abi.OK].sum() + lens_rb[codes(rb_out) == abi.OK].sum()))
-        acts[f"round{k}"] = {abi.NDC_ACTIONS[a]: int(c) for a, c in
-                             zip(*np.unique([decs[k][w].action for w in range(n)], return_counts=True))}
-    events = ev_base + sum(ev_rounds)
-    for _ in range(args.warmup):
+    events, ev_base, ev_rounds, acts, ev_bytes = ndc_counts(base, rebuild, forks, rounds, decs)
+
+    def step():
         rep.reset()
         rep.base_replay()
         for k in range(len(rep.rounds)):
             rep.round(k)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record()
     for _ in range(args.steps):
-        rep.reset()
-        rep.base_replay()
-        for k in range(len(rep.rounds)):
-            rep.round(k)
+        step()
     e1.record()
+    if dist:
+        dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ms = e0.elapsed_time(e1) / args.steps
+    dev_ms = e0.elapsed_time(e1) / args.steps
+    # the final states' per-entry digests (k_digest over the state buffer) and their sum: the
+    # product checksum the ranks reduce
+    stream = torch.cuda.current_stream().cuda_stream
+    per = torch.zeros(max(1, n), dtype=torch.int64, device="cuda")
+    dsum = torch.zeros(1, dtype=torch.int64, device="cuda")
+    rc = abi.lib().cdr_entry_digests_async(eng.ctx, C.byref(rep.base_db), C.byref(rep.state), C.c_void_p(per.data_ptr()),
+                                           C.c_void_p(dsum.data_ptr()), C.c_void_p(stream))
+    if rc:
+        raise RuntimeError(f"cdr_entry_digests_async rc={rc}")
+    torch.cuda.synchronize()
+    ok = int((np.frombuffer(state.result, dtype=np.int32).reshape(-1, C.sizeof(abi.CdrWfResult) // 4)[:n, 0]
+              == abi.OK).sum())
+    stats = torch.tensor([events, n, ok, int(dsum.item())], dtype=torch.int64, device=coll_dev)
+    (tot_events, tot_wfs, tot_ok, checksum), elapsed = reduce_step(dist, torch, stats, elapsed)
     parity = None
     if not args.no_parity:
         import oracle
@@ -400,42 +549,62 @@ def ndc_forks_line(args):
                       if bytes(g_decs[k][w]) != bytes(r_decs[k][w]))
         vb = sum(1 for w in range(n) if ndc.branch_items(g_vhs, g_pool, w, g_vhs[w].current) !=
                  ndc.branch_items(r_vhs, r_pool, w, r_vhs[w].current) or g_vhs[w].n_branches != r_vhs[w].n_branches)
-        parity = {"checked": True, "entries": n, "mismatched_entries": len({b.split(':')[0] for b in bad}),
+        bad_st = len({b.split(':')[0] for b in bad})
+        flag = torch.tensor([bad_st, bad_dec, vb, n], dtype=torch.int64, device=coll_dev)
+        if dist:
+            dist.all_reduce(flag)
+        bad_st, bad_dec, vb, n_all = [int(x) for x in flag.tolist()]
+        parity = {"checked": True, "entries": n_all, "mismatched_entries": bad_st,
                   "mismatched_decisions": bad_dec, "mismatched_version_histories": vb,
-                  "first_mismatches": bad[:4], "seconds": time.perf_counter() - t1,
+                  "first_mismatches": bad[:4], "seconds": time.perf_counter() - t1, "ranks": world,
                   "method": "engine.compare of the final persisted state + each round's decisions + the current "
-                            "branch's VersionHistory, GPU vs oracle.ndc_replicate"}
-        log(f"NDC parity: {parity['mismatched_entries']} states, {bad_dec} decisions, {vb} VHs differ "
+                            "branch's VersionHistory, GPU vs oracle.ndc_replicate, on every rank (counts summed)"}
+        log(f"[rank {rank}] NDC parity (all ranks): {bad_st} states, {bad_dec} decisions, {vb} VHs differ "
             f"({parity['seconds']:.1f}s)")
-    # algorithmic bytes per step: every replayed event's slab element (60 B, cdr.h row layout)
-    # + the per-workflow records each replay writes (264 B), base + 2 rounds x
-    # (rebuild + apply)
-    alg = events * 60 + n * 264 * (1 + 2 * len(forks))
-    workload = f"C5-forked-{n}wf-ndc-replicate"
+    if rank != 0:
+        beat.set()
+        rep.close()
+        finish_dist(dist)
+        return
+    ms = elapsed / args.steps * 1e3
+    # algorithmic bytes per step, this rank's: every replayed event's 48 B +
+    # A[type] (the base branch, each round's rebuilt branch and applied task, counted as
+    # `events` is) + the per-workflow records each replay writes (264 B), base + 2 rounds x
+    # (rebuild + apply); the roofline is one GPU's, on its own bytes and device time
+    alg = ev_bytes + n * 264 * (1 + 2 * len(forks))
+    workload = f"C5-forked-{args.wfs}wf-ndc-replicate"
     traffic, tnote = load_traffic(workload)
     line = {
         "metric": "history events replayed/sec + workflows rebuilt/sec (node), % of HBM roofline",
-        "value": events / (ms / 1e3), "unit": "events/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms, "wall_ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "value": tot_events * args.steps / elapsed, "unit": "events/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "device_ms_per_step_rank0": dev_ms, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int64",
         "data": "synthetic forked config 5 (cadence_amd.ndc.synth_forked)",
-        "config": {"workload": workload, "workflows_per_gpu": n, "rounds": len(forks),
-                   "events_per_step": events, "events_base": ev_base, "events_rounds": ev_rounds,
-                   "decisions": acts, "parallelism": "shard1"},
-        "workflows_per_s": n / (ms / 1e3),
-        "roofline": {"bound": "hbm", "achieved": alg / (ms / 1e3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": alg / (ms / 1e3) / 1e9 / PEAK_HBM_GBS,
+        "config": {"workload": workload, "workflows_per_gpu": args.wfs, "rounds": len(forks),
+                   "events_per_step": tot_events, "events_rank0": events, "events_base_rank0": ev_base,
+                   "events_rounds_rank0": ev_rounds, "decisions_rank0": acts,
+                   "sharding": f"Fingerprint32(workflowID) % {NUM_SHARDS} -> greedy shard->GPU",
+                   "parallelism": f"shard{world}"},
+        "workflows_per_s": tot_wfs * args.steps / elapsed,
+        "roofline": {"bound": "hbm", "achieved": alg / (dev_ms / 1e3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": alg / (dev_ms / 1e3) / 1e9 / PEAK_HBM_GBS,
                      "traffic": traffic["bytes_per_launch"] if traffic else None,
                      "traffic_note": tnote or (traffic.get("source") + "; per step: every k_* kernel of the "
                                                "step (the VersionHistories reset copy excluded)"),
                      "algorithmic_bytes_per_step": alg,
+                     "bytes_breakdown": {"events": ev_bytes, "records": alg - ev_bytes},
                      "kernel": "k_ndc_branch + k_replay* + k_refresh + k_ndc_verify/apply (one step)"},
         "host": {"setup_s": setup_s},
-        "parity": parity, "parity_checked": parity is not None,
+        "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_workflows": tot_ok,
+        "cpu_baseline": None if (args.no_cpu_baseline or world > 1) else ndc_cpu_baseline(min(n, 20000), args.seed),
+        "parity": parity, "parity_checked": parity is not None and parity["mismatched_entries"] == 0
+        and parity["mismatched_decisions"] == 0 and parity["mismatched_version_histories"] == 0,
+        "shard_load_events": load.tolist(),
     }
     beat.set()
     print(json.dumps(line), flush=True)
     rep.close()
+    finish_dist(dist)
 
 
 def carry_line(args):
@@ -476,6 +645,9 @@ def carry_line(args):
     pre_res = pre_host.result
     codes = np.frombuffer(pre_res, dtype=np.int32).reshape(n, -1)[:, 0]
     src = np.where((cut > 0) & (codes == abi.OK), np.arange(n), -1).astype(np.int32)
+    # an entry whose prefix failed replays WHOLE on a fresh builder (engine.suffix_batch's rule)
+    for w in np.nonzero((cut > 0) & (codes != abi.OK))[0]:
+        suf.wfs[w] = b.wfs[w]
     suf.carry = engine.Carry(src=src, state=pre_host)
     spl = engine.plan(suf)
     caps, tot = spl.caps, spl.totals
@@ -484,7 +656,7 @@ def carry_line(args):
     dc = abi.CdrCarry()  # the device copy: the loaded states in HBM
     dc.src, dc.caps, dc.n_src, dc.totals, dc.state = dev.up(src), pre_db.caps, n, pre_pl.totals, pre_out
     suf_db.carry = dev.up(dc)
-    suf_out = ndc.alloc_out(dev, n, tot)
+    suf_out = ndc.alloc_out(dev, n, tot, tasks=args.tasks)
     setup_s = time.perf_counter() - t0
     flags = np.frombuffer(caps, dtype=np.uint32).reshape(n, -1)[:, abi.CdrWfCaps.flags.offset // 4]
     route = {k: int(((flags & m) != 0)[src >= 0].sum()) for k, m in
@@ -541,8 +713,14 @@ def carry_line(args):
     carried = src >= 0
     loaded_b = int(carried.sum()) * 256 + rows(pre_np, carried)
     out_b = n * 264 + rows(res_np, np.ones(n, bool))
-    alg = ev_bytes + loaded_b + out_b
+    alg = ev_bytes + loaded_b + out_b  # SURVEY 8(d) canonical bytes: no task bytes (a17 prices none)
     out_codes = res_np[:, 0].view(np.int32)
+    n_xfer = n_ttask = 0
+    if args.tasks:
+        nt_h = (C.c_int32 * (2 * n))()
+        dev.down(nt_h, suf_out.n_tasks)
+        nt = np.frombuffer(nt_h, np.int32).reshape(n, 2).astype(np.int64)
+        n_xfer, n_ttask = int(nt[:, 0].sum()), int(nt[:, 1].sum())
     parity = None
     if not args.no_parity:
         import oracle
@@ -560,7 +738,7 @@ def carry_line(args):
         sb = engine.Batch(events=b.events, wfs=suf.wfs, kvs=b.kvs, rps=b.rps, cluster=b.cluster, now_ns=b.now_ns,
                           uuid_seed=b.uuid_seed, empty_uuid=b.empty_uuid, carry=engine.Carry(src=src, state=ref_pre))
         rpl = engine.plan(sb)
-        ref = oracle.replay(sb, rpl, threads=th)
+        ref = oracle.replay(sb, rpl, threads=th, tasks=args.tasks)
         want, _ = oracle.entry_digests(sb, rpl, ref, th)
         whole, _, _ = oracle.synth_digests(cfg, np.arange(n_wf, dtype=np.uint32), seed, threads=th)
         bad = np.nonzero(got != want)[0]
@@ -571,10 +749,21 @@ def carry_line(args):
                   "method": "per-entry digest (cdr_entry_digests_async vs oracle/digest_ref.cpp) of the carried "
                             "replay against the oracle's carried replay of its own prefix states, and against the "
                             "oracle's whole-history replay"}
+        if args.tasks:  # every entry's task lists, byte for byte (stateBuilder.go:606-608 of the carried call)
+            sz = C.sizeof(abi.CdrTask)
+            xb = (C.c_uint8 * (max(1, tot.xfer) * sz))()
+            tb = (C.c_uint8 * (max(1, tot.ttask) * sz))()
+            dev.down(xb, suf_out.transfer)
+            dev.down(tb, suf_out.timer_tasks)
+            tbad, tn = compare_task_lists({"xfer": bytes(xb), "ttask": bytes(tb)}, nt, caps, ref, rpl.caps, n)
+            parity["tasks"] = {"entries": n, "tasks": tn, "mismatched_entries": len(tbad), "first_mismatches": tbad[:8]}
+            parity["seconds"] = time.perf_counter() - t1
         log(f"carry parity: {len(bad)} of {n} entries differ from the oracle's carried replay, "
-            f"{len(bad_whole)} from the whole-history replay ({parity['seconds']:.1f}s)")
+            f"{len(bad_whole)} from the whole-history replay"
+            + (f", {parity['tasks']['mismatched_entries']} task lists" if args.tasks else "")
+            + f" ({parity['seconds']:.1f}s)")
     achieved = alg / (kern_ms / 1e3) / 1e9
-    workload = f"C{cfg}-{n_wf}wf-carry-half"
+    workload = f"C{cfg}-{n_wf}wf-carry-half" + ("-tasks" if args.tasks else "")
     traffic, tnote = load_traffic(workload)
     line = {
         "metric": "history events replayed/sec + workflows rebuilt/sec (node), % of HBM roofline",
@@ -592,8 +781,11 @@ def carry_line(args):
                      "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_note": tnote or traffic.get("source"),
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": alg,
                      "bytes_breakdown": {"events": ev_bytes, "loaded_state": loaded_b, "written": out_b}},
+        "tasks": {"transfer": n_xfer, "timer": n_ttask, "bytes": (n_xfer + n_ttask) * C.sizeof(abi.CdrTask),
+                  "note": "task rows written (cdr_task), not in the canonical bytes"} if args.tasks else None,
         "host": {"setup_s": setup_s},
-        "parity": parity, "parity_checked": parity is not None,
+        "parity": parity, "parity_checked": parity is not None and parity["mismatched_entries"] == 0
+        and (not args.tasks or parity["tasks"]["mismatched_entries"] == 0),
     }
     print(json.dumps(line), flush=True)
     dev.close()
@@ -629,7 +821,9 @@ def main():
                          "at the history count limit (204,800 events); 125000 mixes 8 into 1M")
     ap.add_argument("--tasks", action="store_true",
                     help="also emit the stateBuilder's transfer / timer task lists (cdr_out.transfer / timer_tasks; "
-                         "the fast kernel's TASKS instantiation for C1/C2, the general kernel otherwise)")
+                         "k_replay_fast<TASKS> for C1/C2, the register-table kernels' TASKS instantiations "
+                         "(k_replay_reg<..., TASKS>) for the register-table / PAR slices of C3-C5, the general "
+                         "kernel for the rest)")
     ap.add_argument("--carry", action="store_true",
                     help="carry-in line: each history's second half replayed onto its first half's loaded state "
                          "(--config, --wfs)")
@@ -644,21 +838,7 @@ def main():
         return carry_line(args)
 
     import torch
-    world, rank, local = dist_env()
-    if world > 1:
-        import torch.distributed as dist
-        # RCCL (backend "nccl") between the GPUs of the node; CDR_BENCH_BACKEND=gloo rehearses
-        # the multi-rank path on a box with fewer GPUs than ranks (ranks share a device, the
-        # counters reduce on the host; the timings then mean nothing)
-        backend = os.environ.get("CDR_BENCH_BACKEND", "nccl")
-        torch.cuda.set_device(local % max(1, torch.cuda.device_count()) if backend == "gloo" else local)
-        if backend == "gloo":
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        dist = None
-        torch.cuda.set_device(0)
+    dist, world, rank, local, coll_dev = init_dist(torch)
     ctx = L.cdr_create(torch.cuda.current_device(), None)
     if not ctx:
         raise SystemExit("cdr_create failed (no GPU?) — the engine has no CPU fallback")
@@ -725,7 +905,6 @@ def main():
     alg_bytes += task_b
     csum = torch.zeros(1, dtype=torch.int64, device="cuda")
     L.cdr_checksum_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(csum.data_ptr()), C.c_void_p(stream))
-    coll_dev = "cpu" if dist and os.environ.get("CDR_BENCH_BACKEND", "nccl") == "gloo" else "cuda"
     stats = torch.tensor([db.n_events, db.info.n_entries, n_ok, 0], dtype=torch.int64, device="cuda")
     stats[3] = csum[0]
     stats = stats.to(coll_dev)
@@ -741,6 +920,10 @@ def main():
         if dist:
             dist.all_reduce(flag)
         parity["mismatched_entries_all_ranks"], parity["entries_all_ranks"] = [int(x) for x in flag.tolist()]
+        if args.tasks:
+            parity["tasks"] = task_parity(db, args.config, mine, args.seed, args.long_stride)
+            log(f"[rank {rank}] task parity: {parity['tasks']['mismatched_entries']} of {parity['tasks']['entries']} "
+                f"entries' task lists differ ({parity['tasks']['tasks']} tasks, {parity['tasks']['seconds']:.1f}s)")
     encode = None if args.no_refresh else encode_measure(torch, L, ctx, db, stream, max(1, args.steps))
     refresh = None if args.no_refresh else refresh_measure(torch, L, ctx, db, stream, max(1, args.steps))
     if rank != 0:
@@ -800,7 +983,8 @@ def main():
                  "per_batch_events_per_s": db.n_events / (db.pack_s + db.cls_pack_s + db.h2d_s + ms_per_step / 1e3)},
         "tasks": {"transfer": n_xfer, "timer": n_ttask, "bytes": task_b} if args.tasks else None,
         "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_workflows": tot_ok,
-        "parity_checked": bool(parity) and parity["mismatched_entries_all_ranks"] == 0,
+        "parity_checked": bool(parity) and parity["mismatched_entries_all_ranks"] == 0
+        and (not parity.get("tasks") or parity["tasks"]["mismatched_entries"] == 0),
         "parity": parity,
         "shard_load_events": load.tolist(),
     }

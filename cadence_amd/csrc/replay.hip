@@ -1796,6 +1796,18 @@ void* cdr_ws_get(cdr_ctx* c, int slot, uint64_t bytes) {
   return p;
 }
 
+// a register-table launch with or without the task lists (the TASKS instantiation, compiled
+// for CDR_WPE_REG waves per SIMD: its emission code spills at the smaller variant's 3)
+template <int NA, int NT, int NX, uint32_t SF, int WPE, bool CARRY>
+static void launch_reg(bool tasks, dim3 g, hipStream_t sq, const cdr_launch& x) {
+  typedef RegLds<NA, NT, NX> LY;
+  if (tasks)
+    hipLaunchKernelGGL((k_replay_reg<NA, NT, NX, SF, CDR_WPE_REG, CARRY, true>), g, dim3(CDR_SLICE_WIDTH), LY::bytes, sq,
+                       x);
+  else
+    hipLaunchKernelGGL((k_replay_reg<NA, NT, NX, SF, WPE, CARRY, false>), g, dim3(CDR_SLICE_WIDTH), LY::bytes, sq, x);
+}
+
 extern "C" {
 
 void cdr_opts_default(cdr_opts* o) {
@@ -1975,10 +1987,12 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   if (tasks && (in->n_wave_slices > 0 || !out->timer_tasks || !out->n_tasks)) return CDR_API_EINVAL;
   // (the fast kernel's TASKS instantiation emits them for its slices)
   const bool fast = c->fast && in->n_fast_slices > 0;
-  // register-table kernel: LastReplicationInfo kept for clusters < CDR_REG_NCL only
+  // register-table kernel: LastReplicationInfo kept for clusters < CDR_REG_NCL only (a loaded
+  // state with tasks: the CARRY + TASKS instantiations, nDCHistoryReplicator.go:341-348 then
+  // stateBuilder.go:606-608)
   const bool reg = c->fast && c->reg &&
                    in->n_reg_slices + in->n_reg2_slices + in->n_reg0_slices + in->n_par_slices > 0 &&
-                   !(tasks && in->carry) && in->cluster.n_clusters <= (int)CDR_REG_NCL;
+                   in->cluster.n_clusters <= (int)CDR_REG_NCL;
   // carry-in batches (cdr_dev_batch.carry): the register-table slices replay in the carry-in
   // instantiations of k_replay_reg, each class followed by its hand-on chain (below)
   const bool carry = in->carry != nullptr;
@@ -2034,15 +2048,17 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   // 12-activity variant over its level-1 list (below12: the class's tables are smaller),
   // then the general kernel over the level-2 list
   auto carry_tail = [&](int cls_id, dim3 g, hipStream_t sq, bool below12) {
-    if (below12) {
-      typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
-      // a whole grid: unlike k_replay_cls's few leftovers, a loaded state outgrowing the
-      // smaller tables is common, and this variant runs one wave per SIMD
-      hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_CLS_SLICES, CDR_WPE_REG, true>), g,
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sq, out_list(in_list(cls_id, 1), cls_id, 2));
+    if (below12)  // a whole grid: unlike k_replay_cls's few leftovers, a loaded state outgrowing the
+                  // smaller tables is common, and this variant runs one wave per SIMD
+      launch_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_CLS_SLICES, CDR_WPE_REG, true>(
+          tasks, g, sq, out_list(in_list(cls_id, 1), cls_id, 2));
+    if (tasks) {
+      hipLaunchKernelGGL((k_replay<true, true>), g, dim3(CDR_SLICE_WIDTH), lds, sq, in_list(cls_id, 2));
+      if (spill) hipLaunchKernelGGL((k_replay<false, true>), g, dim3(CDR_SLICE_WIDTH), 0, sq, in_list(cls_id, 2));
+    } else {
+      hipLaunchKernelGGL((k_replay<true, false>), g, dim3(CDR_SLICE_WIDTH), lds, sq, in_list(cls_id, 2));
+      if (spill) hipLaunchKernelGGL((k_replay<false, false>), g, dim3(CDR_SLICE_WIDTH), 0, sq, in_list(cls_id, 2));
     }
-    hipLaunchKernelGGL((k_replay<true, false>), g, dim3(CDR_SLICE_WIDTH), lds, sq, in_list(cls_id, 2));
-    if (spill) hipLaunchKernelGGL((k_replay<false, false>), g, dim3(CDR_SLICE_WIDTH), 0, sq, in_list(cls_id, 2));
   };
   // each kernel over its class's slice range (cdr_plan_class_ranges), or every slice
   bool ranged = false;
@@ -2137,7 +2153,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   // gains 5%: 5.07 -> 4.84 ms)
   const bool gate2 = gate_ok && !par && reg2 && gate_reg2_max > 0 && fk[1] && so[1] != so[6] && !(wv && so[0] == so[1]);
   const uint32_t gate_n = (gate ? (npar < 256u ? npar : 256u) : 0u) + (gate2 ? (gr2.x < gate_reg2_max ? gr2.x : gate_reg2_max) : 0u);
-  bool gating = gate || gate2;
+  const bool gating = gate || gate2;
   // each class's launches (its stream sx(i)); the order they are issued in decides which
   // class's workgroups take the CUs first (CDR_LAUNCH_ORDER overrides: a digit string of
   // side-stream indices, default \"6012345\": PAR, wave, 12-activity, general, small-table,
@@ -2148,9 +2164,8 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
     if (par && carry) {
       cdr_launch Lp = L;
       Lp.s0 = 0;
-      typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
-      hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_REG, true>), dim3(npar),
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6), out_list(Lp, 6, 2));
+      launch_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_REG, true>(tasks, dim3(npar), sx(6),
+                                                                                        out_list(Lp, 6, 2));
       carry_tail(6, dim3(npar), sx(6), false);
     } else if (par) {  // first: the longest critical paths of the batch
       cdr_launch Lp = L;
@@ -2177,9 +2192,8 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
         break;
       case 1:
     if (reg2 && carry) {
-      typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
-      hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_REG, true>), gr2,
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), out_list(Lr2, 1, 2));
+      launch_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_REG, true>(tasks, gr2, sx(1),
+                                                                                         out_list(Lr2, 1, 2));
       carry_tail(1, gr2, sx(1), false);
     } else if (reg2) {
       typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
@@ -2214,9 +2228,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
         break;
       case 3:
     if (reg0 && carry) {
-      typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
-      hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3, true>), gr0,
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), out_list(Lr0, 3, 1));
+      launch_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3, true>(tasks, gr0, sx(3), out_list(Lr0, 3, 1));
       carry_tail(3, gr0, sx(3), true);
     } else if (reg0) {  // the small-table variant, at 3 waves per SIMD
       typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
@@ -2239,9 +2251,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
         break;
       case 5:
     if (reg1 && carry) {
-      typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
-      hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_REG, true>), gr1,
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), out_list(Lr1, 5, 1));
+      launch_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_REG, true>(tasks, gr1, sx(5), out_list(Lr1, 5, 1));
       carry_tail(5, gr1, sx(5), true);
     } else if (reg1) {
       typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
@@ -2260,22 +2270,36 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
         break;
     }
   };
-  for (int j = 0; j < cdr_ctx::N_SIDE; j++) {
-    const int i = order[j] - '0';
-    if (gating && i != 6 && i != 1 && !(i == 0 && so[0] == so[1])) {
-      // before the first ungated class: every ungated stream waits for the gated workgroups
-      gating = false;
-      hipStream_t waited[cdr_ctx::N_SIDE + 1];
-      int nw = 0;
-      for (int q = 0; q < 6; q++) {
-        if (!on[q] || q == 1 || (gate && sx(q) == sx(6)) || (gate2 && sx(q) == sx(1))) continue;
-        bool dup = false;
-        for (int r = 0; r < nw; r++) dup |= waited[r] == sx(q);
-        if (dup) continue;
-        waited[nw++] = sx(q);
-        HIPCHK(hipStreamWaitValue32(sx(q), rws + 15, gate_n, hipStreamWaitValueGte, 0xFFFFFFFFu));
+  // The gated kernels are issued before any wait: a wait-value packet blocks its whole
+  // hardware queue, so a wait issued ahead of the kernel whose workgroups it counts could
+  // block that kernel's own queue (streams share the 4 hardware queues) and never be met.
+  // Issued after it, every wait is met once the gated kernel's workgroups have started,
+  // whatever the stream -> queue mapping or a profiler's dispatch serialisation.
+  bool issued[cdr_ctx::N_SIDE] = {};
+  if (gating) {
+    for (int j = 0; j < cdr_ctx::N_SIDE; j++) {
+      const int i = order[j] - '0';
+      if ((gate && i == 6) || (gate2 && i == 1)) {
+        launch_class(i);
+        HIPCHK(hipGetLastError());
+        issued[i] = true;
       }
     }
+    // every other class's stream waits for the gated workgroups
+    hipStream_t waited[cdr_ctx::N_SIDE + 1];
+    int nw = 0;
+    for (int q = 0; q < 6; q++) {
+      if (!on[q] || q == 1 || (gate && sx(q) == sx(6)) || (gate2 && sx(q) == sx(1))) continue;
+      bool dup = false;
+      for (int r = 0; r < nw; r++) dup |= waited[r] == sx(q);
+      if (dup) continue;
+      waited[nw++] = sx(q);
+      HIPCHK(hipStreamWaitValue32(sx(q), rws + 15, gate_n, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    }
+  }
+  for (int j = 0; j < cdr_ctx::N_SIDE; j++) {
+    const int i = order[j] - '0';
+    if (issued[i]) continue;
     launch_class(i);
     HIPCHK(hipGetLastError());
   }

@@ -426,7 +426,7 @@ class Engine:
 
     def replay(self, batch: Batch, pl: Plan | None = None, tasks: bool = False) -> Outputs:
         """Replay through cdr_replay_batch; `tasks` also emits the transfer / timer
-        task lists (general kernel only)."""
+        task lists (the kernels' TASKS instantiations; no wave / PAR slices)."""
         pl = pl or plan(batch)
         out = Outputs(batch, pl, tasks)
         rc = abi.lib().cdr_replay_batch(self.ctx, C.byref(batch.cstruct()), pl.caps, C.byref(pl.totals),

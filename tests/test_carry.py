@@ -196,3 +196,39 @@ def test_gpu_carry_chain_builders(engine_gpu, builder):
     got = engine_gpu.replay(sb, pl)
     bad = engine.compare(sb, got, ref)
     assert not bad, "\n".join(bad[:10])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 3, 4, 5])
+def test_gpu_carry_tasks_tiers(engine_gpu, cfg):
+    """A loaded state AND the task lists — the NDC replication call (nDCHistoryReplicator.go:
+    341-348 applies a batch onto the loaded state, stateBuilder.go:606-608 appends its tasks):
+    the register-table kernels' CARRY + TASKS instantiations (default route), the hand-on chain
+    from an undersized variant to the 12-activity variant and the general kernel's TASKS
+    instantiation, and the general kernel alone — state and task lists bit-exact against the
+    oracle."""
+    import oracle
+    b = engine.synth_batch(cfg, 400, seed=0x5EED0500 + cfg, error_rate=0.1 if cfg in (0, 3) else 0.0)
+    pre, cut = engine.split_batch(b, cfg + 13)
+    pre_gpu = engine_gpu.replay(pre)
+    sb = engine.suffix_batch(b, cut, pre, pre_gpu)
+    ref = oracle.replay(sb, tasks=True)
+    assert sum(ref.tasks["n"][:2 * sb.n_wfs]) > 0
+    pl = engine.plan(sb)
+    n_reg = sum(1 for w in range(sb.n_wfs) if sb.carry.src[w] >= 0 and pl.caps[w].flags & (abi.CAP_REG | abi.CAP_REG2))
+    assert n_reg > 0
+    got = engine_gpu.replay(sb, pl, tasks=True)
+    bad = engine.compare(sb, got, ref) + engine.compare_tasks(sb, got, ref)
+    assert not bad, "default route:\n" + "\n".join(bad[:10])
+    pl2 = engine.plan(sb)
+    assert _force_small_tables(sb, pl2) > 0
+    got2 = engine_gpu.replay(sb, pl2, tasks=True)
+    bad = engine.compare(sb, got2, ref) + engine.compare_tasks(sb, got2, ref)
+    assert not bad, "hand-on chain:\n" + "\n".join(bad[:10])
+    old = abi.lib().cdr_set_reg_path(engine_gpu.ctx, 0)
+    try:
+        got3 = engine_gpu.replay(sb, tasks=True)
+    finally:
+        abi.lib().cdr_set_reg_path(engine_gpu.ctx, old)
+    bad = engine.compare(sb, got3, ref) + engine.compare_tasks(sb, got3, ref)
+    assert not bad, "general kernel:\n" + "\n".join(bad[:10])

@@ -236,12 +236,14 @@ def test_gpu_tasks_fast_kernel(engine_gpu, cfg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [2, 3])
-def test_gpu_tasks_device_batch(engine_gpu, cfg):
+@pytest.mark.parametrize("cfg,reg", [(2, True), (3, True), (3, False)])
+def test_gpu_tasks_device_batch(engine_gpu, cfg, reg):
     """The `bench.py --tasks` path: a synthetic sliced batch carrying task capacities
     (DeviceBatch(tasks=True), a plan without wave / PAR slices, no class blocks) replayed by
-    cdr_replay_sliced_async — C2 on k_replay_fast<TASKS>, C3 on the general kernel — equals
-    the oracle's task lists for the same workflows, entry by entry and byte for byte."""
+    cdr_replay_sliced_async — C2 on k_replay_fast<TASKS>, C3's register-table slices on
+    k_replay_reg<..., TASKS> (and, with the register-table path off, every C3 slice on the
+    general kernel's TASKS instantiation) — equals the oracle's task lists for the same
+    workflows, entry by entry and byte for byte."""
     import ctypes as C
 
     import numpy as np
@@ -254,6 +256,8 @@ def test_gpu_tasks_device_batch(engine_gpu, cfg):
     L = abi.lib()
     ctx = L.cdr_create(torch.cuda.current_device(), None)
     try:
+        if not reg:
+            L.cdr_set_reg_path(ctx, 0)
         stream = torch.cuda.current_stream().cuda_stream
         assert L.cdr_replay_sliced_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(stream)) == 0
         torch.cuda.synchronize()

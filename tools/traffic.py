@@ -5,7 +5,13 @@ profiles/<name>_pmc.txt and profiles/traffic_latest.json (read by bench.py).
 HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of
 a coalesced streaming read (128-B requests tallied at 64 B), so it is doubled;
-WRITE_SIZE is taken as is.  Counters are averaged over the profiled dispatches — or, with
+WRITE_SIZE is taken as is.  Calibrated for the replay kernels' own access widths
+(tools/calib.hip, profiles/r5_pmc_calibration.txt): FETCH_SIZE = 0.500 x the bytes for
+4-, 8- and 16-B-per-lane loads and for the slab's column-per-row pattern (one
+TCC_EA0_RDREQ per 128 B), so x2 holds for every read here; WRITE_SIZE = 1.000 x the bytes
+for 4-, 8- and 16-B streaming stores, while a record written 8 B per store from lanes 256 B
+apart costs one 64-B write request per store (WRITE_SIZE = 8.1 x the record bytes, 548 GB/s
+of records) — real write traffic, not a miscount.  Counters are averaged over the profiled dispatches — or, with
 an anchor kernel (a multi-kernel step: C3-C5 run several replay kernels per step), summed
 over every matching dispatch and divided by the anchor's dispatch count (one per step).
 Writes profiles/traffic_<workload>.json (and traffic_latest.json).
