@@ -616,20 +616,26 @@ def carry_line(args):
     applyEvents, nDCHistoryReplicator.go:330-398) through the register-table kernels'
     carry-in instantiations.  value = suffix events per second.  Parity, entry by entry: the
     GPU's carried replay against the oracle's carried replay of the oracle's own prefix
-    states, and against the oracle's WHOLE-history replay (split equals whole)."""
+    states, and against the oracle's WHOLE-history replay (split equals whole).
+    N > 1 (torch.distributed.run): each rank takes the workflows of its historyShardIDs
+    (Fingerprint32(workflowID) % 16384, greedy on events); one all-reduce of [events,
+    workflows, OK entries, digest sum], the max of the timed region and the parity counts."""
     import torch
     from cadence_amd import engine, ndc
-    torch.cuda.set_device(0)
-    eng = engine.Engine(0)
+    dist, world, rank, local, coll_dev = init_dist(torch)
+    eng = engine.Engine(torch.cuda.current_device())
     L = abi.lib()
-    n, cfg = args.wfs, args.config
+    cfg = args.config
     seed = args.seed if args.seed != 0x5EED0002 else 0x5EED0000 + cfg
+    total = args.wfs * world
+    mine, load = assign_shards(total, world, rank, workflow_weights(cfg, total, seed))
     t0 = time.perf_counter()
-    b = engine.synth_batch(cfg, n, seed)
-    n_wf, n = n, b.n_wfs  # entries: a continue-as-new run is an entry of its own (never split)
+    b = engine.synth_batch(cfg, len(mine), seed, index_map=mine)
+    n_wf, n = len(mine), b.n_wfs  # entries: a continue-as-new run is an entry of its own (never split)
     cut = engine.split_half(b)
     pre, suf = engine.cut_batches(b, cut)
-    log(f"carry: {n} C{cfg} workflows, {int((cut > 0).sum())} split ({time.perf_counter() - t0:.0f}s)")
+    log(f"[rank {rank}] carry: {n} C{cfg} entries of {n_wf} workflows, {int((cut > 0).sum())} split "
+        f"({time.perf_counter() - t0:.0f}s)")
     dev = ndc._Dev()
     stream = torch.cuda.current_stream().cuda_stream
     # the first halves: replayed once into the state buffer the steps load from
@@ -661,7 +667,7 @@ def carry_line(args):
     flags = np.frombuffer(caps, dtype=np.uint32).reshape(n, -1)[:, abi.CdrWfCaps.flags.offset // 4]
     route = {k: int(((flags & m) != 0)[src >= 0].sum()) for k, m in
              (("reg0", abi.CAP_REG0), ("reg", abi.CAP_REG), ("reg2", abi.CAP_REG2))}
-    log(f"carry: setup {setup_s:.1f}s, carried entries by variant {route}")
+    log(f"[rank {rank}] carry: setup {setup_s:.1f}s, carried entries by variant {route}")
 
     def step():
         rc = L.cdr_replay_sliced_async(eng.ctx, C.byref(suf_db), C.byref(suf_out), C.c_void_p(stream))
@@ -671,13 +677,17 @@ def carry_line(args):
         step()
     torch.cuda.synchronize()
     L.cdr_timing_begin(eng.ctx, args.steps)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    e1.record()
+    if dist:
+        dist.barrier()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / args.steps
+    elapsed = time.perf_counter() - t1
+    ms = elapsed / args.steps * 1e3
     kms = (C.c_float * args.steps)()
     nk = C.c_uint32(args.steps)
     L.cdr_timing_read(eng.ctx, kms, C.byref(nk))
@@ -721,17 +731,21 @@ def carry_line(args):
         dev.down(nt_h, suf_out.n_tasks)
         nt = np.frombuffer(nt_h, np.int32).reshape(n, 2).astype(np.int64)
         n_xfer, n_ttask = int(nt[:, 0].sum()), int(nt[:, 1].sum())
+    # per-entry digests of the carried replay (k_digest) and their sum: the product checksum
+    per = torch.zeros(max(1, n), dtype=torch.int64, device="cuda")
+    tsum = torch.zeros(1, dtype=torch.int64, device="cuda")
+    rc = L.cdr_entry_digests_async(eng.ctx, C.byref(suf_db), C.byref(suf_out), C.c_void_p(per.data_ptr()),
+                                   C.c_void_p(tsum.data_ptr()), C.c_void_p(stream))
+    if rc:
+        raise RuntimeError(f"cdr_entry_digests_async rc={rc}")
+    torch.cuda.synchronize()
+    stats = torch.tensor([events, n_wf, int((out_codes == abi.OK).sum()), int(tsum.item())], dtype=torch.int64,
+                         device=coll_dev)
+    (tot_events, tot_wfs, tot_ok, checksum), elapsed = reduce_step(dist, torch, stats, elapsed)
     parity = None
     if not args.no_parity:
         import oracle
         t1 = time.perf_counter()
-        per = torch.zeros(max(1, n), dtype=torch.int64, device="cuda")
-        tsum = torch.zeros(1, dtype=torch.int64, device="cuda")
-        rc = L.cdr_entry_digests_async(eng.ctx, C.byref(suf_db), C.byref(suf_out), C.c_void_p(per.data_ptr()),
-                                       C.c_void_p(tsum.data_ptr()), C.c_void_p(stream))
-        if rc:
-            raise RuntimeError(f"cdr_entry_digests_async rc={rc}")
-        torch.cuda.synchronize()
         got = per[:n].cpu().numpy().view(np.uint64).copy()
         th = host_cores()[0]
         ref_pre = oracle.replay(pre, pre_pl, threads=th)
@@ -740,7 +754,7 @@ def carry_line(args):
         rpl = engine.plan(sb)
         ref = oracle.replay(sb, rpl, threads=th, tasks=args.tasks)
         want, _ = oracle.entry_digests(sb, rpl, ref, th)
-        whole, _, _ = oracle.synth_digests(cfg, np.arange(n_wf, dtype=np.uint32), seed, threads=th)
+        whole, _, _ = oracle.synth_digests(cfg, mine, seed, threads=th)
         bad = np.nonzero(got != want)[0]
         bad_whole = np.nonzero(got != whole)[0]
         parity = {"checked": True, "entries": n, "mismatched_entries": int(len(bad)),
@@ -758,24 +772,38 @@ def carry_line(args):
             tbad, tn = compare_task_lists({"xfer": bytes(xb), "ttask": bytes(tb)}, nt, caps, ref, rpl.caps, n)
             parity["tasks"] = {"entries": n, "tasks": tn, "mismatched_entries": len(tbad), "first_mismatches": tbad[:8]}
             parity["seconds"] = time.perf_counter() - t1
-        log(f"carry parity: {len(bad)} of {n} entries differ from the oracle's carried replay, "
+        log(f"[rank {rank}] carry parity: {len(bad)} of {n} entries differ from the oracle's carried replay, "
             f"{len(bad_whole)} from the whole-history replay"
             + (f", {parity['tasks']['mismatched_entries']} task lists" if args.tasks else "")
             + f" ({parity['seconds']:.1f}s)")
+        flag = torch.tensor([parity["mismatched_entries"], parity["split_vs_whole_mismatched_entries"],
+                             parity["tasks"]["mismatched_entries"] if args.tasks else 0, n], dtype=torch.int64,
+                            device=coll_dev)
+        if dist:
+            dist.all_reduce(flag)
+        (parity["mismatched_entries_all_ranks"], parity["split_vs_whole_mismatched_entries_all_ranks"],
+         parity["task_mismatched_entries_all_ranks"], parity["entries_all_ranks"]) = [int(x) for x in flag.tolist()]
+    if rank != 0:
+        dev.close()
+        finish_dist(dist)
+        return
     achieved = alg / (kern_ms / 1e3) / 1e9
-    workload = f"C{cfg}-{n_wf}wf-carry-half" + ("-tasks" if args.tasks else "")
+    workload = f"C{cfg}-{args.wfs}wf-carry-half" + ("-tasks" if args.tasks else "")
     traffic, tnote = load_traffic(workload)
     line = {
         "metric": "history events replayed/sec + workflows rebuilt/sec (node), % of HBM roofline",
-        "value": events / (ms / 1e3), "unit": "events/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "value": tot_events * args.steps / elapsed, "unit": "events/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup,
         "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
         "data": f"synthetic config {cfg}, each history's second half applied onto its first half's loaded state",
-        "config": {"workload": workload, "workflows_per_gpu": n_wf, "entries": n, "carried_entries": int(carried.sum()),
-                   "events_per_step": events, "routing": route,
+        "config": {"workload": workload, "workflows_per_gpu": args.wfs, "entries_rank0": n,
+                   "carried_entries_rank0": int(carried.sum()), "events_per_step": tot_events,
+                   "events_rank0": events, "routing_rank0": route,
+                   "sharding": f"Fingerprint32(workflowID) % {NUM_SHARDS} -> greedy shard->GPU",
                    "status": {abi.STATUS.get(int(v), str(int(v))): int(c) for v, c in
                               zip(*np.unique(out_codes, return_counts=True))},
-                   "parallelism": "shard1"},
-        "workflows_per_s": n_wf / (ms / 1e3),
+                   "parallelism": f"shard{world}"},
+        "workflows_per_s": tot_wfs * args.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS,
                      "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_note": tnote or traffic.get("source"),
@@ -784,11 +812,14 @@ def carry_line(args):
         "tasks": {"transfer": n_xfer, "timer": n_ttask, "bytes": (n_xfer + n_ttask) * C.sizeof(abi.CdrTask),
                   "note": "task rows written (cdr_task), not in the canonical bytes"} if args.tasks else None,
         "host": {"setup_s": setup_s},
-        "parity": parity, "parity_checked": parity is not None and parity["mismatched_entries"] == 0
-        and (not args.tasks or parity["tasks"]["mismatched_entries"] == 0),
+        "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_entries": tot_ok,
+        "parity": parity, "parity_checked": parity is not None and parity["mismatched_entries_all_ranks"] == 0
+        and parity["task_mismatched_entries_all_ranks"] == 0,
+        "shard_load_events": load.tolist(),
     }
     print(json.dumps(line), flush=True)
     dev.close()
+    finish_dist(dist)
 
 
 def main():

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--no-par", action="store_true", help="long register-table histories on wave slices, not PAR slices")
     ap.add_argument("--par-subset", type=int, default=0,
                     help="replay only the histories of the full batch's first N PAR slices (PAR kernel alone)")
+    ap.add_argument("--tasks", action="store_true", help="with the stateBuilder task lists (bench.py --tasks's batch)")
     ap.add_argument("--ab-cls", action="store_true",
                     help="each lib twice: class-decomposed register slices (k_replay_cls) on, then off")
     args = ap.parse_args()
@@ -48,7 +49,8 @@ def main():
     db = DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config,
                      plan_mode=0 if args.no_wave else abi.PLAN_WAVE | (abi.PLAN_WAVE_ALL if args.wave_all else 0)
                      | (abi.PLAN_NO_LONG if args.no_long else 0) | (0 if args.no_par else abi.PLAN_PAR),
-                     ctx_for_cls=bctx)
+                     ctx_for_cls=bctx) if not args.tasks else \
+        DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config, plan_mode=0, cls=None, tasks=True)
     print(json.dumps({"cls_pack_s": round(db.cls_pack_s, 4), "cls_rows": db.cls_rows, "rows": db.info.n_rows}),
           flush=True)
     stream = torch.cuda.current_stream().cuda_stream
