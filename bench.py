@@ -395,6 +395,73 @@ def task_parity(db, config, mine, seed, long_stride=0, sample=20000):
                       "oracle.replay(tasks=True)"}
 
 
+def host_path_measure(config, seed, n_sample, ctx_dev, long_stride=0):
+    """What a caller holding DECODED histories (cdr_event records, the Go side's
+    []*HistoryEvent after thriftrw decode) sees through the drop-in boundary: the same
+    population's first n_sample workflows as a host batch, (a) the host planner + packer
+    stages alone (cdr_plan_caps, cdr_plan_slices_ex, cdr_pack_slices on the host's cores,
+    into a page-locked slab), and (b) the whole cdr_replay_batch call (plan + pack + H2D +
+    replay + D2H of every record), warm (the context's staging and workspace already
+    sized).  The headline's timed step excludes all of this (device-resident input)."""
+    from cadence_amd import engine
+    L = abi.lib()
+    b = engine.synth_batch(config, n_sample, seed, long_stride=long_stride)
+    n_ev = len(b.events)
+    threads = host_cores()[0]
+    import torch
+    res = {}
+    for rep in range(2):  # the second pass is the warm one
+        t0 = time.perf_counter()
+        pl = engine.plan(b)
+        t1 = time.perf_counter()
+        ns, rows, nw = C.c_uint32(), C.c_uint64(), C.c_uint32()
+        mode = abi.PLAN_WAVE | abi.PLAN_PAR
+        L.cdr_plan_slices_ex(b.wfs, pl.caps, b.n_wfs, mode, None, None, None, None, C.byref(ns), C.byref(rows),
+                             C.byref(nw))
+        lane = np.zeros(ns.value * 64, np.int32)
+        slen = np.zeros(ns.value, np.uint32)
+        row0 = np.zeros(ns.value, np.uint64)
+        fl = np.zeros(ns.value, np.uint32)
+        L.cdr_plan_slices_ex(b.wfs, pl.caps, b.n_wfs, mode, lane.ctypes.data, slen.ctypes.data, row0.ctypes.data,
+                             fl.ctypes.data, C.byref(ns), C.byref(rows), C.byref(nw))
+        t2 = time.perf_counter()
+        bs = b.cstruct()
+        aw = L.cdr_plan_arena_words(C.byref(bs))
+        if rep == 0:
+            slab_t = torch.empty(int(rows.value) * 64 * abi.EL_BYTES, dtype=torch.uint8, pin_memory=True)
+            arena_t = torch.empty(max(1, aw) * 8, dtype=torch.uint8, pin_memory=True)
+        s = abi.CdrSlices(n_slices=ns.value, n_rows=rows.value, arena_words=aw)
+        s.slice_row0, s.slice_len, s.lane_wf = row0.ctypes.data, slen.ctypes.data, lane.ctypes.data
+        s.slab, s.arena, s.slice_flags = slab_t.data_ptr(), arena_t.data_ptr(), fl.ctypes.data
+        t3 = time.perf_counter()
+        if L.cdr_pack_slices(C.byref(bs), C.byref(s), threads):
+            raise RuntimeError("cdr_pack_slices failed")
+        t4 = time.perf_counter()
+        dev = slab_t.to("cuda", non_blocking=True)
+        torch.cuda.synchronize()
+        t5 = time.perf_counter()
+        del dev
+        res = {"plan_caps_s": t1 - t0, "plan_slices_s": t2 - t1, "pack_s": t4 - t3, "h2d_s": t5 - t4,
+               "h2d_gbs": slab_t.numel() / max(t5 - t4, 1e-9) / 1e9}
+    host_s = res["plan_caps_s"] + res["plan_slices_s"] + res["pack_s"]
+    res.update({"events": n_ev, "workflows": n_sample, "threads": threads,
+                "host_planner_packer_events_per_s": n_ev / host_s,
+                "host_planner_packer_h2d_events_per_s": n_ev / (host_s + res["h2d_s"])})
+    # the whole drop-in call, warm
+    eng = engine.Engine(torch.cuda.current_device())
+    try:
+        eng.replay(b)
+        t0 = time.perf_counter()
+        eng.replay(b)
+        res["replay_batch_s"] = time.perf_counter() - t0
+    finally:
+        eng.close()
+    res["replay_batch_events_per_s"] = n_ev / res["replay_batch_s"]
+    res["method"] = ("cdr_plan_caps + cdr_plan_slices_ex + cdr_pack_slices (host threads) into a pinned slab + its H2D; "
+                     "and one warm cdr_replay_batch call (plan + pack + H2D + replay + D2H) on the same sample")
+    return res
+
+
 def canonical_event_bytes(batch) -> np.ndarray:
     """SURVEY 8(d) canonical input bytes of every entry of a host batch: sum over its events
     of 48 B core + A[type]."""
@@ -836,6 +903,10 @@ def main():
     ap.add_argument("--no-wave", action="store_true", help="no wave slices: divergent histories in lane slices")
     ap.add_argument("--wave-all", action="store_true", help="every divergent history on a wave slice")
     ap.add_argument("--no-refresh", action="store_true", help="skip the refreshTasks / row-encoder side measurements")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the drop-in host path measurement (decoded histories -> cdr_replay_batch)")
+    ap.add_argument("--host-path-wfs", type=int, default=200000,
+                    help="workflows of the host-path sample (the population's first ones)")
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size GPU == oracle digest check")
     ap.add_argument("--no-par", action="store_true",
                     help="long register-table histories on wave slices instead of CDR_SLICE_PAR slices")
@@ -974,6 +1045,8 @@ def main():
     builders = {names[int(k)]: int(c) for k, c in zip(*np.unique(bld, return_counts=True))}
     peak_meas = None if args.no_stream_peak else stream_peak_gbs(torch)
     cpu = None if (args.no_cpu_baseline or args.gpus > 1) else cpu_baseline(args.config, 20000, args.seed)
+    host_path = None if (args.no_host_path or world > 1) else \
+        host_path_measure(args.config, args.seed, args.host_path_wfs, ctx, args.long_stride)
     line = {
         "metric": "history events replayed/sec + workflows rebuilt/sec (node), % of HBM roofline",
         "value": ev_per_s, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -1013,6 +1086,7 @@ def main():
                  "per_batch_s": db.pack_s + db.cls_pack_s + db.h2d_s + ms_per_step / 1e3,
                  "per_batch_events_per_s": db.n_events / (db.pack_s + db.cls_pack_s + db.h2d_s + ms_per_step / 1e3)},
         "tasks": {"transfer": n_xfer, "timer": n_ttask, "bytes": task_b} if args.tasks else None,
+        "host_path": host_path,
         "checksum": checksum & 0xFFFFFFFFFFFFFFFF, "ok_workflows": tot_ok,
         "parity_checked": bool(parity) and parity["mismatched_entries_all_ranks"] == 0
         and (not parity.get("tasks") or parity["tasks"]["mismatched_entries"] == 0),

@@ -183,7 +183,7 @@ CdrWfCaps = _S("cdr_wf_caps", [
     ("act_off", u64), ("timer_off", u64), ("child_off", u64), ("cancel_off", u64), ("signal_off", u64),
     ("vh_off", u64), ("rp_off", u64), ("sa_off", u64), ("act_cap", u32), ("timer_cap", u32), ("child_cap", u32),
     ("cancel_cap", u32), ("signal_cap", u32), ("vh_cap", u32), ("rp_cap", u32), ("sa_cap", u32),
-    ("act_live", u32), ("timer_live", u32), ("flags", u32), ("_pad", u32), ("xfer_off", u64), ("ttask_off", u64),
+    ("act_live", u32), ("timer_live", u32), ("flags", u32), ("order_key", u32), ("xfer_off", u64), ("ttask_off", u64),
     ("xfer_cap", u32), ("ttask_cap", u32)])
 CdrTotals = _S("cdr_totals", [(n, u64) for n in ("act", "timer", "child", "cancel", "signal", "vh", "rp", "sa",
                                                  "xfer", "ttask")])

@@ -245,8 +245,11 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   if (rc) return rc;
   const uint64_t ne = rows * CDR_SLICE_WIDTH;
   const uint64_t aw = cdr_plan_arena_words(b);
-  std::vector<uint8_t> slab(ne * CDR_EL_BYTES);
-  std::vector<uint64_t> arena(aw ? aw : 1);
+  // the packer writes every cell (padding included) and every arena word it names: staging
+  // needs no zero-fill
+  uint8_t* slab = (uint8_t*)cdr_hs_get(ctx, cdr_ctx::HS_SLAB, ne * CDR_EL_BYTES);
+  uint64_t* arena = (uint64_t*)cdr_hs_get(ctx, cdr_ctx::HS_ARENA, (aw ? aw : 1) * 8ull);
+  if (!slab || !arena) return CDR_API_ENOMEM;
   cdr_slices hs{};
   hs.n_slices = ns;
   hs.n_rows = rows;
@@ -255,8 +258,8 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   hs.slice_len = slen.data();
   hs.lane_wf = lane.data();
   hs.slice_flags = sflags.data();
-  hs.slab = slab.data();
-  hs.arena = arena.data();
+  hs.slab = slab;
+  hs.arena = arena;
   rc = cdr_pack_slices(b, &hs, 0);
   if (rc) return rc;
   std::vector<uint64_t> sc_off(ns);
@@ -295,8 +298,8 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   db.ev.slice_row0 = (const uint64_t*)up(WS_ROW0, row0.data(), ns * 8ull);
   db.ev.slice_len = (const uint32_t*)up(WS_SLEN, slen.data(), ns * 4ull);
   db.ev.lane_wf = (const int32_t*)up(WS_LANE, lane.data(), lane.size() * 4ull);
-  db.ev.slab = (const uint8_t*)up(WS_SLAB, slab.data(), slab.size());
-  db.ev.arena = (const uint64_t*)up(WS_ARENA, arena.data(), arena.size() * 8);
+  db.ev.slab = (const uint8_t*)up(WS_SLAB, slab, ne * CDR_EL_BYTES);
+  db.ev.arena = (const uint64_t*)up(WS_ARENA, arena, (aw ? aw : 1) * 8ull);
   db.ev.slice_flags = (const uint32_t*)up(WS_SFLAGS, sflags.data(), ns * 4ull);
   db.n_fast_slices = n_fast;
   db.n_wave_slices = n_wave;

@@ -88,8 +88,18 @@ struct cdr_ctx {
   // grow-only device workspace of the host-buffer calls
   void* ws[WS_NUM] = {};
   uint64_t ws_bytes[WS_NUM] = {};
+  // grow-only pinned host staging of the host-buffer calls (the packed slab and arena):
+  // no page faults or zero-fill after the first call, and the H2D copy reads page-locked
+  // memory directly
+  enum { HS_SLAB, HS_ARENA, HS_NUM };
+  void* hs[HS_NUM] = {};
+  uint64_t hs_bytes[HS_NUM] = {};
   cdr_one_host one;
 };
+
+// pinned host staging `slot` of at least `bytes` (grow-only; contents undefined); nullptr
+// when page-locked memory cannot be had (defined in replay.hip)
+void* cdr_hs_get(cdr_ctx* c, int slot, uint64_t bytes);
 
 // device buffer `slot` of at least `bytes` (grow-only; contents undefined); nullptr
 // when the device is out of memory (defined in replay.hip)

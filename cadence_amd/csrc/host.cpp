@@ -189,6 +189,23 @@ void caps_one(const cdr_event* ev, uint64_t n, uint32_t builder, cdr_wf_caps* ou
   c.vh_cap = vh;
   c.act_live = (uint32_t)live_max;
   c.timer_live = (uint32_t)lv_max[0];  // peak live user timers: the kernels reuse freed slots first
+  // the lane planner's ordering key: the entity counts (cdr_wf_caps.order_key)
+  {
+    auto sat = [](uint32_t v, uint32_t bits) { return v < (1u << bits) ? v : (1u << bits) - 1u; };
+    c.order_key = sat(c.act_cap, 10) << 22 | sat(c.timer_cap, 11) << 11 |
+                  sat(c.child_cap + c.cancel_cap + c.signal_cap, 11);
+  }
+  // the pending tables' row capacities: the peak live sets (the rows still pending at the
+  // end are at most those), or the creating-event counts past the device planner's tracked
+  // bound (k_caps: CDR_WAVE_SLOTS + 1 keys per set)
+  {
+    const size_t T = CDR_WAVE_SLOTS + 1;
+    c.act_cap = (uint32_t)live_max;
+    c.timer_cap = lv_max[0] > T ? c.timer_cap : (uint32_t)lv_max[0];
+    c.child_cap = lv_max[1] > T ? c.child_cap : (uint32_t)lv_max[1];
+    c.cancel_cap = lv_max[2] > T ? c.cancel_cap : (uint32_t)lv_max[2];
+    c.signal_cap = lv_max[3] > T ? c.signal_cap : (uint32_t)lv_max[3];
+  }
   c.flags = (fast && live_max <= 1) ? CDR_CAP_FAST : 0u;
   const uint32_t W = CDR_WAVE_SLOTS;
   // the wave kernel keeps one slot per lane and reuses freed slots first, so its
@@ -314,26 +331,39 @@ int cdr_plan_ndc_apply(const cdr_batch* b, const cdr_wf_caps* state_caps, cdr_wf
 // most its state capacities (known only on the device when the launch is planned)
 static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* totals, const cdr_wf_caps* bound) {
   if (!b || !caps || !totals) return CDR_API_EINVAL;
-  cdr_totals t{};
-  for (uint32_t w = 0; w < b->n_wfs; w++) {
+  // per entry (in parallel: every entry's simulation is independent), then the offsets as a
+  // prefix over the entries
+  std::atomic<int> bad{0};
+  parallel_for(b->n_wfs, 0, [&](uint64_t wi) {
+    const uint32_t w = (uint32_t)wi;
     const cdr_wf_desc& d = b->wfs[w];
-    if (d.ev_off + d.ev_len > b->n_events) return CDR_API_EINVAL;
+    if (d.ev_off + d.ev_len > b->n_events) {
+      bad = 1;
+      return;
+    }
     // a continue-as-new entry must describe the run the parent's CAN event names
     // (stateBuilder.go:559-563): same workflow, RunId = NewExecutionRunId, builder
     // from newRunNDC
     if (d.newrun >= 0) {
-      if ((uint32_t)d.newrun >= b->n_wfs) return CDR_API_EINVAL;
+      if ((uint32_t)d.newrun >= b->n_wfs) {
+        bad = 1;
+        return;
+      }
       const cdr_wf_desc& n = b->wfs[d.newrun];
       if (n.parent != (int32_t)w || n.workflow_id != d.workflow_id ||
-          n.builder != (d.newrun_ndc ? (uint32_t)CDR_BUILDER_NDC : (uint32_t)CDR_BUILDER_2DC))
-        return CDR_API_EINVAL;
+          n.builder != (d.newrun_ndc ? (uint32_t)CDR_BUILDER_NDC : (uint32_t)CDR_BUILDER_2DC)) {
+        bad = 1;
+        return;
+      }
       uint32_t call = 0;
       for (uint64_t k = 0; k < d.ev_len; k++) {
         const cdr_event& e = b->events[d.ev_off + k];
         if (k > 0 && (e.flags & CDR_EVF_BATCH_FIRST)) call++;
         if (call == d.newrun_call && e.type == CDR_EV_WF_CONTINUED_AS_NEW &&
-            e.a.can.new_execution_run_id != n.run_id)
-          return CDR_API_EINVAL;
+            e.a.can.new_execution_run_id != n.run_id) {
+          bad = 1;
+          return;
+        }
       }
     }
     cdr_wf_caps c{};
@@ -344,9 +374,11 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
       // loaded state, the register-table kernels' carry-in instantiations do
       const cdr_carry& cy = *b->carry;
       const uint32_t src = (uint32_t)cy.src[w];
-      if (src >= cy.n_src || d.parent >= 0 || !cy.state.result) return CDR_API_EINVAL;
+      if (src >= cy.n_src || d.parent >= 0 || !cy.state.result || cy.state.result[src].code != CDR_OK) {
+        bad = 1;
+        return;
+      }
       const cdr_wf_result& r = cy.state.result[src];
-      if (r.code != CDR_OK) return CDR_API_EINVAL;
       cdr_internal::loaded_rows ld{{r.n_activity, r.n_timer, r.n_child, r.n_cancel, r.n_signal, r.n_reset_points,
                                     r.n_search_attr},
                                    nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -360,11 +392,7 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
         ld.sa = cy.state.sa ? cy.state.sa + sc.sa_off : nullptr;
       }
       cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c, b->kvs, b->rps, &ld);
-      c.act_cap += r.n_activity;
-      c.timer_cap += r.n_timer;
-      c.child_cap += r.n_child;
-      c.cancel_cap += r.n_cancel;
-      c.signal_cap += r.n_signal;
+      // (the pending tables' capacities are peak live sets that already count the loaded rows)
       c.vh_cap += r.n_vh;
       c.rp_cap += r.n_reset_points;
       c.sa_cap += r.n_search_attr;
@@ -373,7 +401,10 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
       cdr_internal::caps_one(b->events + d.ev_off, d.ev_len, d.builder, &c, b->kvs, b->rps);
     }
     if (bound) {  // the loaded rows' bound: the state's capacities
-      if (d.parent >= 0 || d.newrun >= 0) return CDR_API_EINVAL;  // one run per entry
+      if (d.parent >= 0 || d.newrun >= 0) {  // one run per entry
+        bad = 1;
+        return;
+      }
       const cdr_wf_caps& s = bound[w];
       c.act_cap += s.act_cap;
       c.timer_cap += s.timer_cap;
@@ -402,6 +433,12 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
       if (all12 && (c.flags & CDR_CAP_REG)) c.flags = (c.flags & ~CDR_CAP_REG) | CDR_CAP_REG2;
     }
     cdr_internal::task_caps(b->events + d.ev_off, d.ev_len, &c.xfer_cap, &c.ttask_cap);
+    caps[w] = c;
+  }, 64);
+  if (bad) return CDR_API_EINVAL;
+  cdr_totals t{};
+  for (uint32_t w = 0; w < b->n_wfs; w++) {
+    cdr_wf_caps& c = caps[w];
     c.xfer_off = t.xfer;
     t.xfer += c.xfer_cap;
     c.ttask_off = t.ttask;
@@ -422,7 +459,6 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
     t.rp += c.rp_cap;
     c.sa_off = t.sa;
     t.sa += c.sa_cap;
-    caps[w] = c;
   }
   *totals = t;
   return CDR_API_OK;
@@ -499,10 +535,9 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
                                              : 4u;
   };
   // register-table groups: within a length class by their entity counts (scheduled
-  // activities, started timers, initiated externals), so that a slice's lanes have similar
+  // activities, started timers, initiated externals: cdr_wf_caps.order_key), so that a slice's lanes have similar
   // class counts and the class-sorted block's aligned regions (replay_cls.inc) carry little
   // padding (C3: 13% fewer class rows than ordering by footprint)
-  auto ext = [&](uint32_t a) { return caps[a].child_cap + caps[a].cancel_cap + caps[a].signal_cap; };
   // a PAR slice holds a whole CU (four 256-VGPR waves), so beyond about one round of them the
   // PAR kernel queues behind itself: the longest CDR_PAR_MAX_SLICES slices' worth stay PAR,
   // the rest go back to the register-table lanes
@@ -521,7 +556,7 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
      // entity counts, footprint and length, all descending; the keys are computed once per
      // entry (a log2 and the caps reads per comparison dominated the planner: C3 100k 145 ms)
     struct LaneKey {
-      uint32_t group, lclass, act, timer, ext, slots;
+      uint32_t group, lclass, counts, slots;
       uint64_t len;
       uint32_t w;
     };
@@ -530,15 +565,12 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     for (size_t i = 0; i < lanes.size(); i++) {
       const uint32_t a = lanes[i], g = group(a);
       const bool counts = caps && by_counts && g >= 1 && g <= 3;
-      keys[i] = LaneKey{g, lclass(a), counts ? caps[a].act_cap : 0u, counts ? caps[a].timer_cap : 0u,
-                        counts ? ext(a) : 0u, slots(a), (uint64_t)wfs[a].ev_len, a};
+      keys[i] = LaneKey{g, lclass(a), counts ? caps[a].order_key : 0u, slots(a), (uint64_t)wfs[a].ev_len, a};
     }
     std::stable_sort(keys.begin(), keys.end(), [](const LaneKey& x, const LaneKey& y) {
       if (x.group != y.group) return x.group < y.group;
       if (x.lclass != y.lclass) return x.lclass > y.lclass;
-      if (x.act != y.act) return x.act > y.act;
-      if (x.timer != y.timer) return x.timer > y.timer;
-      if (x.ext != y.ext) return x.ext > y.ext;
+      if (x.counts != y.counts) return x.counts > y.counts;
       if (x.slots != y.slots) return x.slots > y.slots;
       return x.len > y.len;
     });
@@ -750,18 +782,34 @@ int cdr_pack_slices(const cdr_batch* b, cdr_slices* o, int threads) {
       cdr_internal::pack_chunked(b->events + b->wfs[w].ev_off, b->wfs[w].ev_len, row0, len, arena_base[w], o);
       return;
     }
+    // blocks of rows, lane by lane within a block: the block's rows (~60 KB) stay in cache
+    // while each lane's events stream in order (a lane-major walk over the whole slice
+    // revisits ~0.8 MB of rows once per lane; a row-major one interleaves 64 input streams)
+    const cdr_event* evl[CDR_SLICE_WIDTH];
+    uint32_t n_ev[CDR_SLICE_WIDTH];
+    uint64_t apos[CDR_SLICE_WIDTH];
     for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
       const int32_t w = o->lane_wf[s * CDR_SLICE_WIDTH + l];
+      evl[l] = w >= 0 ? b->events + b->wfs[w].ev_off : nullptr;
+      n_ev[l] = w >= 0 ? (uint32_t)b->wfs[w].ev_len : 0u;
+      apos[l] = w >= 0 ? arena_base[w] : 0;
       if (w >= 0 && b->wfs[w].ev_len > len) {
         bad = 1;
-        continue;
+        n_ev[l] = 0;
+        evl[l] = nullptr;
       }
-      if (w >= 0)
-        cdr_internal::pack_lane(b->events + b->wfs[w].ev_off, b->wfs[w].ev_len, row0, len, l, arena_base[w], o);
-      else
-        cdr_internal::pack_lane(nullptr, 0, row0, len, l, 0, o);
     }
-  });
+    uint8_t* const blk0 = const_cast<uint8_t*>(o->slab) + row0 * CDR_ROW_BYTES;
+    uint64_t* arena = const_cast<uint64_t*>(o->arena);
+    constexpr uint32_t KB = 16;
+    for (uint32_t k0 = 0; k0 < len; k0 += KB) {
+      const uint32_t k1 = k0 + KB < len ? k0 + KB : len;
+      for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++)
+        for (uint32_t k = k0; k < k1; k++)
+          cdr_put_event(blk0 + (uint64_t)k * CDR_ROW_BYTES, l, k < n_ev[l] ? evl[l] + k : nullptr, k == 0, &apos[l],
+                        arena);
+    }
+  }, 2, 8);  // a slice is ~0.8 MB of rows: small grains, parallel from a few slices on
   return bad ? CDR_API_EINVAL : CDR_API_OK;
 }
 

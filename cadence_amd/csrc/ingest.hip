@@ -1292,6 +1292,16 @@ __global__ __launch_bounds__(64) void k_caps(const cdr_event* events, const uint
   c.vh_cap = vh;
   c.act_live = (uint32_t)live_max;
   c.timer_live = lv0.over ? c.timer_cap : lv0.max;  // past the tracked bound: every TimerStarted
+  {  // the lane planner's ordering key and the pending tables' row capacities (host.cpp caps_one)
+    auto sat = [](uint32_t v, uint32_t bits) { return v < (1u << bits) ? v : (1u << bits) - 1u; };
+    c.order_key = sat(c.act_cap, 10) << 22 | sat(c.timer_cap, 11) << 11 |
+                  sat(c.child_cap + c.cancel_cap + c.signal_cap, 11);
+    c.act_cap = (uint32_t)live_max;
+    c.timer_cap = lv0.over ? c.timer_cap : lv0.max;
+    c.child_cap = lv1.over ? c.child_cap : lv1.max;
+    c.cancel_cap = lv2.over ? c.cancel_cap : lv2.max;
+    c.signal_cap = lv3.over ? c.signal_cap : lv3.max;
+  }
   c.flags = (fast && live_max <= 1) ? CDR_CAP_FAST : 0u;
   const uint32_t W = CDR_WAVE_SLOTS;
   if (!(c.flags & CDR_CAP_FAST) && live_max <= (int64_t)W && lv0.max <= W && lv1.max <= W && lv2.max <= W &&

@@ -1796,6 +1796,22 @@ void* cdr_ws_get(cdr_ctx* c, int slot, uint64_t bytes) {
   return p;
 }
 
+void* cdr_hs_get(cdr_ctx* c, int slot, uint64_t bytes) {
+  const uint64_t want = bytes ? bytes : 8;
+  if (c->hs[slot] && c->hs_bytes[slot] >= want) return c->hs[slot];
+  if (c->hs[slot]) (void)hipHostFree(c->hs[slot]);
+  c->hs[slot] = nullptr;
+  c->hs_bytes[slot] = 0;
+  void* p = nullptr;
+  if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  c->hs[slot] = p;
+  c->hs_bytes[slot] = want;
+  return p;
+}
+
 // a register-table launch with or without the task lists (the TASKS instantiation, compiled
 // for CDR_WPE_REG waves per SIMD: its emission code spills at the smaller variant's 3)
 template <int NA, int NT, int NX, uint32_t SF, int WPE, bool CARRY>
@@ -1966,6 +1982,8 @@ void cdr_destroy(cdr_ctx* c) {
   if (c->fork) (void)hipEventDestroy(c->fork);
   if (hipSetDevice(c->device) == hipSuccess)
     for (void* p : c->ws) (void)hipFree(p);
+  for (void* p : c->hs)
+    if (p) (void)hipHostFree(p);
   delete c;
 }
 

@@ -573,11 +573,20 @@ typedef struct cdr_wf_result {
  * cdr_plan() from the input (counts of creating events, version runs, ...). */
 typedef struct cdr_wf_caps {
   uint64_t act_off, timer_off, child_off, cancel_off, signal_off, vh_off, rp_off, sa_off;
+  /* row capacities of the entry's table slices.  The five pending tables (activities, user
+   * timers, children, request-cancels, signals) persist the rows still pending at the end,
+   * so their capacity is the simulated peak live set (cdr_plan_caps; a loaded state's rows
+   * counted in), or the number of creating events when a live set passes
+   * CDR_WAVE_SLOTS + 1 (the device planner tracks no more); version-history items, reset
+   * points and search attributes: every row the history can add */
   uint32_t act_cap, timer_cap, child_cap, cancel_cap, signal_cap, vh_cap, rp_cap, sa_cap;
   /* upper bounds of the live set (working slots): activities = max over prefixes of
-   * (#scheduled - #closed), timers = #TimerStarted */
+   * (#scheduled - #closed), timers = peak live user timers */
   uint32_t act_live, timer_live;
-  uint32_t flags, _pad; /* CDR_CAP_* */
+  /* flags: CDR_CAP_*; order_key: the lane planner's ordering of register-table entries by
+   * entity counts (cdr_plan_slices_ex), scheduled activities << 22 | started user timers << 11
+   * | initiated children + request-cancels + signals, each saturating (10 / 11 / 11 bits) */
+  uint32_t flags, order_key;
   /* task slices (bounds from the event types; used only when tasks are emitted) */
   uint64_t xfer_off, ttask_off;
   uint32_t xfer_cap, ttask_cap;

@@ -362,8 +362,8 @@ def test_register_lanes_ordered_by_entity_counts():
     reg = [w for w in order if (pl.caps[w].flags & (abi.CAP_REG | abi.CAP_REG2 | abi.CAP_REG0)) and
            not (pl.caps[w].flags & abi.CAP_FAST)]
     lcl = lambda w: int(np.log2(float(b.wfs[w].ev_len) + 1.0) * 16.0)  # noqa: E731
-    key = lambda w: (pl.caps[w].act_cap, pl.caps[w].timer_cap,  # noqa: E731
-                     pl.caps[w].child_cap + pl.caps[w].cancel_cap + pl.caps[w].signal_cap)
+    cnt = _entity_counts(b)
+    key = lambda w: tuple(cnt[w])  # noqa: E731
     pairs = 0
     for a, c in zip(reg, reg[1:]):
         grp = lambda w: (pl.caps[w].flags & abi.CAP_REG0, pl.caps[w].flags & abi.CAP_REG)  # noqa: E731
@@ -371,6 +371,51 @@ def test_register_lanes_ordered_by_entity_counts():
             assert key(a) >= key(c), (a, c, key(a), key(c))
             pairs += 1
     assert pairs > 100
+
+
+def _entity_counts(b):
+    """Per entry: (scheduled activities, started user timers, initiated children + request-
+    cancels + signals) — the lane planner's ordering counts, from the events."""
+    import ctypes as C
+    words = C.sizeof(abi.CdrEvent) // 4
+    ty = np.frombuffer(b.events, dtype=np.uint32).reshape(-1, words)[:, abi.CdrEvent.type.offset // 4]
+    wf = np.ctypeslib.as_array(b.wfs)
+    out = np.zeros((b.n_wfs, 3), np.int64)
+    E = abi.EV
+    for j, types in enumerate(([E["ActivityTaskScheduled"]], [E["TimerStarted"]],
+                               [E["StartChildWorkflowExecutionInitiated"],
+                                E["RequestCancelExternalWorkflowExecutionInitiated"],
+                                E["SignalExternalWorkflowExecutionInitiated"]])):
+        hit = np.isin(ty, types).astype(np.int64)
+        cum = np.concatenate([[0], np.cumsum(hit)])
+        off, ln = wf["ev_off"].astype(np.int64), wf["ev_len"].astype(np.int64)
+        out[:, j] = cum[off + ln] - cum[off]
+    return out
+
+
+def _order_key(cnt):
+    sat = lambda v, bits: np.minimum(v, (1 << bits) - 1)  # noqa: E731
+    return (sat(cnt[:, 0], 10) << 22) | (sat(cnt[:, 1], 11) << 11) | sat(cnt[:, 2], 11)
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+def test_caps_pending_tables_live_bound(cfg):
+    """cdr_wf_caps: order_key packs the entity counts; the five pending tables' capacities
+    are peak live sets — at most the counts, at least the rows the oracle persists."""
+    import oracle
+    b = engine.synth_batch(cfg, 1500, seed=29 + cfg, error_rate=0.0)
+    pl = engine.plan(b)
+    caps = np.ctypeslib.as_array(pl.caps)
+    cnt = _entity_counts(b)
+    assert np.array_equal(caps["order_key"].astype(np.int64), _order_key(cnt))
+    assert (caps["act_cap"] <= cnt[:, 0]).all() and (caps["timer_cap"] <= cnt[:, 1]).all()
+    assert (caps["act_cap"] == caps["act_live"]).all()
+    out = oracle.replay(b, pl)
+    res = np.ctypeslib.as_array(out.result)
+    for f, c in (("n_activity", "act_cap"), ("n_timer", "timer_cap"), ("n_child", "child_cap"),
+                 ("n_cancel", "cancel_cap"), ("n_signal", "signal_cap")):
+        assert (res[f][:b.n_wfs] <= caps[c]).all(), f
+    assert int(caps["act_cap"].sum()) < int(cnt[:, 0].sum()) or cnt[:, 0].sum() == 0
 
 
 def test_lane_order_restated():
@@ -392,13 +437,13 @@ def test_lane_order_restated():
             return (0 if f & abi.CAP_FAST else 1 if f & abi.CAP_REG0 else 2 if f & abi.CAP_REG else
                     3 if f & abi.CAP_REG2 else 4)
 
+        okey = _order_key(_entity_counts(b))
+
         def key(w):
             g = group(w)
             counts = 1 <= g <= 3
-            ext = int(caps["child_cap"][w] + caps["cancel_cap"][w] + caps["signal_cap"][w])
             slots = int(caps["act_live"][w]) * 12 + int(caps["timer_live"][w]) * 4  # CDR_ACT/TIM_PLANES
-            return (g, -int(math.log2(lens[w] + 1.0) * 16.0), -int(caps["act_cap"][w]) if counts else 0,
-                    -int(caps["timer_cap"][w]) if counts else 0, -ext if counts else 0, -slots, -int(lens[w]))
+            return (g, -int(math.log2(lens[w] + 1.0) * 16.0), -int(okey[w]) if counts else 0, -slots, -int(lens[w]))
         order = sorted(range(b.n_wfs), key=key)  # Python's sort is stable
         expect = []
         for i, w in enumerate(order):

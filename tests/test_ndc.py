@@ -108,7 +108,8 @@ def test_in_memory_carry_keeps_the_rebuilt_current_version():
 def test_apply_working_slots_bounded_by_live_rows():
     """cdr_plan_ndc_apply sizes an apply entry's live sets (the general kernel's working
     slots) by the loaded state's peak live rows — the sum of the parts' simulated peaks —
-    not by its table capacities (every row any part ever added)."""
+    and its pending tables by the same bound (the table capacities are peak live sets,
+    cdr_wf_caps), never by every row any part ever added."""
     import ctypes as C
     base, rebuild, forks = ndc.synth_forked(5, 200, 0x5EED0C05)
     caps_tab = ndc.state_caps_for(base, rebuild, forks).caps
@@ -120,15 +121,16 @@ def test_apply_working_slots_bounded_by_live_rows():
     caps = (abi.CdrWfCaps * fb.n_wfs)()
     tot = abi.CdrTotals()
     assert L.cdr_plan_ndc_apply(C.byref(fb.cstruct()), bound, caps, C.byref(tot)) == 0
-    tighter = 0
+    scheduled = 0
     for w in range(fb.n_wfs):
         peak = sum(p.caps[w].act_live for p in parts)
         assert bound[w].act_live == peak
-        assert bound[w].act_cap == caps_tab[w].act_cap  # the tables keep their capacities
+        assert bound[w].act_cap == caps_tab[w].act_cap == peak  # pending rows: the peak live sets
         assert caps[w].act_live == own[w].act_live + peak
         assert caps[w].act_cap == own[w].act_cap + caps_tab[w].act_cap
-        tighter += caps[w].act_live < own[w].act_live + caps_tab[w].act_cap
-    assert tighter > 0
+        scheduled += sum(1 for p in (base, rebuild, fb) for k in range(p.wfs[w].ev_len)
+                         if p.events[p.wfs[w].ev_off + k].type == abi.EV["ActivityTaskScheduled"])
+    assert sum(caps[w].act_cap for w in range(fb.n_wfs)) < scheduled
 
 
 def test_vh_item_capacity_is_reported():
