@@ -178,9 +178,9 @@ __device__ __forceinline__ T gget(const GAS T* p) {
 #define LD_CAPTURED 4u
 __device__ __forceinline__ bool ld_pending(uint32_t ld) { return (ld & 3u) != 0u && !(ld & LD_CAPTURED); }
 __device__ __forceinline__ uint32_t ld_make(uint32_t src, uint32_t k) { return src | (k << 3); }
-__device__ __forceinline__ void ld_write(GAS cdr_last_decision* o, uint32_t ld, int64_t dv, int64_t dsched,
-                                         int64_t dstart, uint32_t dreq, int32_t dto, int64_t datt, int64_t dsc_ts,
-                                         int64_t dst_ts, int64_t dorig_ts) {
+__device__ __forceinline__ cdr_last_decision ld_rec(uint32_t ld, int64_t dv, int64_t dsched, int64_t dstart,
+                                                    uint32_t dreq, int32_t dto, int64_t datt, int64_t dsc_ts,
+                                                    int64_t dst_ts, int64_t dorig_ts) {
   cdr_last_decision r;
   const bool any = (ld & 3u) != 0u;
   r.source = ld & 3u;
@@ -195,7 +195,12 @@ __device__ __forceinline__ void ld_write(GAS cdr_last_decision* o, uint32_t ld, 
   r.original_scheduled_ts = any ? dorig_ts : 0;
   r.decision_timeout = any ? dto : 0;
   r._pad = 0;
-  gput(o, r);
+  return r;
+}
+__device__ __forceinline__ void ld_write(GAS cdr_last_decision* o, uint32_t ld, int64_t dv, int64_t dsched,
+                                         int64_t dstart, uint32_t dreq, int32_t dto, int64_t datt, int64_t dsc_ts,
+                                         int64_t dst_ts, int64_t dorig_ts) {
+  gput(o, ld_rec(ld, dv, dsched, dstart, dreq, dto, datt, dsc_ts, dst_ts, dorig_ts));
 }
 
 // Opaque copy of a wave-uniform base pointer: loads through it cannot be hoisted out
@@ -337,6 +342,52 @@ struct LdsSlots {
     cdr_lds[l + (j * P + p) * CDR_SLICE_WIDTH] = (uint64_t)v;
   }
 };
+// One record per active lane (`on` lanes only), written by the whole wave together through an
+// LDS transpose at cdr_lds[lw ..] (8-B words; (CW + 1) * 65 of them): in each pass of up to CW
+// words, work item i is word i % cw of the record of the lane ranked i / cw, so that
+// consecutive lanes store consecutive words of one record in one instruction — whole segments
+// instead of one write request per field store from lanes whose records lie apart
+// (tools/calib.hip k_cal_wrec: 8 B per store from lanes 256 B apart cost a 64-B request each).
+// Every active lane of the wave calls it (wave-uniform control flow); the LDS words are free
+// for the caller again when it returns.
+template <uint32_t CW, class T>
+__device__ __forceinline__ void coop_put(GAS T* dst, const T& v, bool on, uint32_t lw) {
+  static_assert(sizeof(T) % 8 == 0, "record size");
+  constexpr uint32_t NW = sizeof(T) / 8, RS = 65;
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(&v);
+  const uint64_t em = __builtin_amdgcn_read_exec();
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+  const uint32_t na = (uint32_t)__builtin_popcountll(em);
+  uint64_t* const L = cdr_lds + lw;
+#pragma unroll
+  for (uint32_t w0 = 0; w0 < NW; w0 += CW) {
+    constexpr uint32_t one = 1;
+    const uint32_t cw = NW - w0 < CW ? NW - w0 : CW;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): earlier LDS traffic has landed
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t j = 0; j < CW; j++)
+      if (j < cw) L[j * RS + rank] = src[w0 + j];
+    L[CW * RS + rank] = on ? (uint64_t)(uintptr_t)((GAS uint64_t*)dst + w0) : 0ull;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = rank; i < cw * na; i += na) {
+      const uint32_t rr = i / cw, j = i - rr * cw;
+      const uint64_t p = L[CW * RS + rr];
+      if (p) ((GAS uint64_t*)(uintptr_t)p)[j] = L[j * RS + rr];
+    }
+    (void)one;
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// one 128-B half of a cdr_exec_info record (schema.h: the Started half, then the replay half)
+struct exec_half {
+  uint64_t w[16];
+};
+static_assert(sizeof(cdr_exec_info) == 2 * sizeof(exec_half), "ExecutionInfo halves");
+
 // global tier: the slice's lane-interleaved scratch (same plane layout)
 template <uint32_t P>
 struct GlbSlots {
