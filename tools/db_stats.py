@@ -1,15 +1,19 @@
-"""The kernel-stats summary of a rocprofv3 results database (its top_kernels view) as the
-CSV rocprofv3 --stats writes: Name, Calls, TotalDurationNs, AverageNs, Percentage.
+"""The kernel-stats summary of a rocprofv3 results database as the CSV rocprofv3 --stats writes
+(Name, Calls, TotalDurationNs, AverageNs, Percentage), one row per kernel AND grid size: a run
+that launches one kernel over two batches (bench.py's timed 1M-workflow launches, then a smaller
+host-path batch) gets a row for each, so the timed launches' average is the one to compare with
+the bench line's live kernel_ms.
 usage: tools/db_stats.py <run_results.db> <out.csv>"""
 import csv
 import sqlite3
 import sys
 
 c = sqlite3.connect(sys.argv[1])
-cur = c.execute("select * from top_kernels")
-cols = [d[0] for d in cur.description]
+rows = c.execute("select name, grid_x, count(*), sum(end - start), avg(end - start) from kernels "
+                 "group by name, grid_x order by sum(end - start) desc").fetchall()
+total = sum(r[3] for r in rows) or 1
 with open(sys.argv[2], "w", newline="") as f:
     w = csv.writer(f)
-    w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "source_columns:" + "|".join(cols)])
-    for name, calls, tot, avg, pct in cur:
-        w.writerow([name, calls, int(round(tot * 1e3)), round(avg * 1e3, 1), round(pct, 3)])
+    w.writerow(["Name", "Grid", "Calls", "TotalDurationNs", "AverageNs", "Percentage"])
+    for name, grid, calls, tot, avg in rows:
+        w.writerow([name, grid, calls, int(tot), round(avg, 1), round(100.0 * tot / total, 3)])
