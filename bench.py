@@ -953,16 +953,19 @@ def main():
     # the register-table slices' class-sorted blocks: emitted by the host packer beside the
     # slab (default; host packing time cls_pack_s), built on the device in every step
     # (--cls-in-step), or none (--no-cls)
-    # (with task lists: no class blocks — the register-table kernels emit no tasks — and no
-    # wave / PAR slices, cdr_replay_sliced_async's contract for task emission)
-    cls_src = None if args.no_cls or args.tasks else "device" if args.cls_in_step else "host"
+    # (with task lists: no wave / PAR slices, cdr_replay_sliced_async's contract for task
+    # emission; the class kernels' TASKS instantiations stage the register-table slices' tasks
+    # and k_tasks_merge orders them)
+    cls_src = None if args.no_cls else "device" if args.cls_in_step else "host"
     db = DeviceBatch(torch, args.config, mine, args.seed,
-                     plan_mode=0 if args.no_wave or args.tasks else abi.PLAN_WAVE
+                     plan_mode=0 if args.no_wave else abi.PLAN_WAVE
                      | (abi.PLAN_WAVE_ALL if args.wave_all else 0) | (0 if args.no_par else abi.PLAN_PAR),
                      ctx_for_cls=ctx, cls=cls_src, long_stride=args.long_stride, tasks=args.tasks)
     if args.no_cls:
         L.cdr_set_cls_path(ctx, abi.CLS_OFF)
     log(f"[rank {rank}] {db.n_fast} of {db.info.n_slices} slices on the fast-path kernel, {db.n_wave} wave slices")
+    if args.tasks and db.n_wave:
+        raise SystemExit("--tasks: the plan has wave slices (no task emission there); use --no-wave")
     log(f"[rank {rank}] packed {db.n_events:,} events in {db.pack_s:.2f}s (host SoA) + {db.cls_pack_s:.2f}s "
         f"(class blocks, {db.cls_where}), H2D {db.h2d_s:.2f}s "
         f"({db.in_bytes / 1e9:.2f} GB in, {db.out_bytes / 1e9:.2f} GB out buffers)")
@@ -1003,8 +1006,9 @@ def main():
     res = db.results()
     alg_bytes, n_ok, ev_b, wf_b, row_b = db.algorithmic_bytes(res)
     n_xfer, n_ttask = db.task_counts()
-    task_b = (n_xfer + n_ttask) * C.sizeof(abi.CdrTask)  # the task rows written (cdr_task)
-    alg_bytes += task_b
+    # the task rows written (cdr_task): listed apart, not in `achieved` / `frac` — SURVEY §8(d)
+    # prices no task bytes (a17: counts only); `frac_with_task_bytes` counts them as written
+    task_b = (n_xfer + n_ttask) * C.sizeof(abi.CdrTask)
     csum = torch.zeros(1, dtype=torch.int64, device="cuda")
     L.cdr_checksum_async(ctx, C.byref(db.db), C.byref(db.out), C.c_void_p(csum.data_ptr()), C.c_void_p(stream))
     stats = torch.tensor([db.n_events, db.info.n_entries, n_ok, 0], dtype=torch.int64, device="cuda")
@@ -1068,7 +1072,9 @@ def main():
                      + ("<TASKS>" if args.tasks else ""),
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": alg_bytes,
                      "bytes_breakdown": {"events": ev_b, "per_workflow": wf_b, "pending_rows": row_b,
-                                         "tasks": task_b},
+                                         "tasks_not_priced": task_b},
+                     "frac_with_task_bytes": ((alg_bytes + task_b) / (kern_ms / 1e3) / 1e9 / PEAK_HBM_GBS
+                                              if args.tasks else None),
                      "stream_copy_peak_gbs": peak_meas},
         "cpu_baseline": cpu,
         "refresh": refresh,

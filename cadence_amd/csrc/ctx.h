@@ -37,6 +37,7 @@ enum cdr_ws_slot {
   // cdr_ndc_replicate_async (ndc.hip)
   WS_NDC_SKIP_RB, WS_NDC_SKIP_AP, WS_NDC_INMEM, WS_NDC_SRC, WS_NDC_CARRY,
   WS_RETRY,  // the class kernels' retry lists: 8 counters, then a list of n_slices per class
+  WS_TSTAGE, WS_THEAD,  // k_replay_cls<TASKS>: staged task records, per-entry headers (k_tasks_merge)
   WS_NUM
 };
 
@@ -95,6 +96,11 @@ struct cdr_ctx {
   void* hs[HS_NUM] = {};
   uint64_t hs_bytes[HS_NUM] = {};
   cdr_one_host one;
+  // k_replay_cls<TASKS>: the task slices' total rows of the last batch seen (its caps array
+  // and entry count), read back once per batch to size the staging lists
+  const void* tasks_caps = nullptr;
+  uint32_t tasks_nwfs = 0;
+  uint64_t tasks_rows = 0;
 };
 
 // pinned host staging `slot` of at least `bytes` (grow-only; contents undefined); nullptr

@@ -555,6 +555,10 @@ struct cdr_launch {
   // PAR k_replay_cls: workgroups started (the other classes' streams wait until every PAR
   // workgroup holds its CU, so that the bulk classes' small workgroups cannot starve them)
   uint32_t* pstart;
+  // k_replay_cls<TASKS>: the per-class staging lists of the task records and the per-entry
+  // headers k_tasks_merge reads (replay_cls.inc)
+  uint64_t* tstage;
+  uint32_t* thead;
 };
 // result code k_replay_cls (or a carry-in k_replay_reg below the 12-activity variant) leaves
 // on an entry it hands to k_replay_reg (never returned)
@@ -1788,6 +1792,142 @@ __global__ __launch_bounds__(256) void k_tables(cdr_dev_batch B, cdr_out O) {
   }
 }
 
+// The class kernels' staged tasks into the entries' task slices (k_replay_cls<TASKS>): one
+// workgroup per class slice (launched on the class's stream after its kernel, so that it
+// overlaps the other classes' replay), one lane per entry, merging its four class lists (W,
+// activity, timer, external — each in history order) by history index, which is the order
+// stateBuilder appends them in (getTransferTasks / getTimerTasks, stateBuilder.go:38-52,
+// 613-804).  It fills what the class loops left to it (DomainID and TaskList of decision /
+// activity tasks, the external initiations' targets from their attributes, the
+// DeleteHistoryEvent retention) and writes the records by the wave together (coop_put: 8 whole
+// records per store instruction).  Each list keeps its head and the two records after it in
+// registers, so a step waits for a load only when one list is taken three times running.  Entries
+// without a complete header (handed on to k_replay_reg) are left alone.
+struct task_words {
+  uint64_t w[8];
+};
+static_assert(sizeof(cdr_task) == sizeof(task_words), "cdr_task words");
+template <uint32_t SFLAG>
+__global__ __launch_bounds__(CDR_SLICE_WIDTH) void k_tasks_merge(cdr_launch L) {
+  (void)L;  // read through KA()
+  const uint32_t s = blockIdx.x + KA()->s0;
+  const uint32_t lane = threadIdx.x;
+  if (s >= KA()->B.ev.n_slices) return;
+  if (!(__builtin_amdgcn_readfirstlane(KA()->B.ev.slice_flags[s]) & SFLAG)) return;
+  const int32_t w = KA()->B.ev.lane_wf[(uint64_t)s * CDR_SLICE_WIDTH + lane];
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 h = {0u, 0u, 0u, 0u};
+  if (w >= 0) h = *(const u32x4*)(KA()->thead + 8ull * (uint64_t)w);
+  const bool valid = (h.x >> 31) != 0;
+  if (__builtin_amdgcn_ballot_w64(valid) == 0) return;  // wave-uniform: coop_put needs the wave
+  const uint32_t n[4] = {h.x & 0x7FFFFFFFu, h.y, h.z, h.w};
+  cdr_wf_caps cp{};
+  uint32_t dom = 0, tl = 0;
+  int64_t ret = 0;
+  if (valid) {
+    cp = KA()->B.caps[w];
+    dom = KA()->B.wfs[w].domain_id;
+    ret = (int64_t)KA()->B.wfs[w].retention_days * 86400ll * NS_PER_S;
+    tl = KA()->thead[8ull * (uint64_t)w + 4];
+  }
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  const GAS u64x2* const st = (const GAS u64x2*)KA()->tstage;
+  const uint64_t sb = 4ull * (cp.xfer_off + cp.ttask_off), sc = (uint64_t)cp.xfer_cap + cp.ttask_cap;
+  // record i of list c (w0 with the history index in its high word, event id, value); past
+  // the list: key ~0
+  struct Rec {
+    uint64_t w0;
+    int64_t eid, v;
+  };
+  auto ld = [&](uint32_t c, uint32_t i) -> Rec {
+    Rec r{~0ull, 0, 0};
+    if (i < n[c]) {
+      const uint64_t q = 2ull * (sb + c * sc + i);
+      const u64x2 a = st[q], b = st[q + 1];
+      r.w0 = a.x;
+      r.eid = (int64_t)a.y;
+      r.v = (int64_t)b.x;
+    }
+    return r;
+  };
+  Rec hd[4], nx[4], n2[4];  // each list's head and the two records after it
+  uint32_t cur[4];
+#pragma unroll
+  for (uint32_t c = 0; c < 4; c++) {
+    hd[c] = ld(c, 0);
+    nx[c] = ld(c, 1);
+    n2[c] = ld(c, 2);
+    cur[c] = 0;
+  }
+  uint32_t n_xt = 0, n_tt = 0;
+  auto key = [](const Rec& r) { return (uint32_t)(r.w0 >> 32); };
+  while (__builtin_amdgcn_ballot_w64(valid && (key(hd[0]) & key(hd[1]) & key(hd[2]) & key(hd[3])) != 0xFFFFFFFFu)) {
+    // the head with the lowest history index (two lists never tie: an event is in one class)
+    uint32_t c = 0, km = key(hd[0]);
+#pragma unroll
+    for (uint32_t j = 1; j < 4; j++) {
+      const bool lt = key(hd[j]) < km;
+      c = lt ? j : c;
+      km = lt ? key(hd[j]) : km;
+    }
+    const bool on = valid && km != 0xFFFFFFFFu;
+    // the taken head by selects (an indexed pick would put the heads in scratch)
+    Rec r;
+    r.w0 = c == 0 ? hd[0].w0 : c == 1 ? hd[1].w0 : c == 2 ? hd[2].w0 : hd[3].w0;
+    r.eid = c == 0 ? hd[0].eid : c == 1 ? hd[1].eid : c == 2 ? hd[2].eid : hd[3].eid;
+    r.v = c == 0 ? hd[0].v : c == 1 ? hd[1].v : c == 2 ? hd[2].v : hd[3].v;
+    const uint32_t type = (uint32_t)r.w0 & 0xFFu;
+    const bool tim = (r.w0 >> 12) & 1u;
+    // the cdr_task record as its eight 8-B words (schema.h layout), kept in registers
+    uint32_t t_dom = 0, t_tl = 0, t_wf = 0, t_run = 0, t_fl = 0;
+    if (!tim && (type == CDR_TT_DECISION || type == CDR_TT_ACTIVITY)) {  // stateBuilder.go:196-197,265-266
+      t_dom = dom;
+      t_tl = tl;
+    }
+    const bool ext = on && !tim &&
+                     (type == CDR_TT_START_CHILD || type == CDR_TT_CANCEL_EXECUTION || type == CDR_TT_SIGNAL_EXECUTION);
+    if (ext) {  // :370-371, :421-427, :452-458
+      const GAS cdr_attr_external* xa = gp((const cdr_attr_external*)(KA()->B.ev.arena + (uint64_t)r.v));
+      t_dom = xa->target_domain_id;
+      t_wf = xa->workflow_id;
+      if (type != CDR_TT_START_CHILD) {
+        t_run = xa->run_id;
+        t_fl = (xa->flags & CDR_XF_CHILD_ONLY) ? CDR_TF_CHILD_ONLY : 0u;
+      }
+    }
+    task_words t;
+    t.w[0] = type | (((r.w0 >> 8) & 0xFull) << 32);                       // type, timeout_type
+    t.w[1] = (uint64_t)r.eid;                                               // event_id
+    t.w[2] = tim ? (uint64_t)(r.v + (type == CDR_TT_DELETE_HISTORY ? ret : 0)) : 0ull;  // visibility_ts
+    t.w[3] = 0;                                                             // attempt
+    t.w[4] = t_dom | ((uint64_t)t_tl << 32);                                // domain_id, task_list
+    t.w[5] = t_wf | ((uint64_t)t_run << 32);                                // target workflow / run
+    t.w[6] = t_fl;                                                          // flags, _pad
+    t.w[7] = 0;                                                             // version
+    const bool fits = tim ? n_tt < cp.ttask_cap : n_xt < cp.xfer_cap;
+    GAS task_words* dst = (GAS task_words*)(tim ? gp(KA()->O.timer_tasks) + cp.ttask_off + n_tt
+                                                : gp(KA()->O.transfer) + cp.xfer_off + n_xt);
+    // the taken list advances: its next record becomes the head, the one after is loaded
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const bool tk = on && c == j;
+      if (tk) {
+        hd[j] = nx[j];
+        nx[j] = n2[j];
+        cur[j]++;
+        n2[j] = ld(j, cur[j] + 2);
+      }
+    }
+    coop_put<8>(dst, t, on && fits, 0);
+    n_tt += (on && fits && tim) ? 1u : 0u;
+    n_xt += (on && fits && !tim) ? 1u : 0u;
+  }
+  if (valid) {
+    KA()->O.n_tasks[2ull * (uint64_t)w] = n_xt;
+    KA()->O.n_tasks[2ull * (uint64_t)w + 1] = n_tt;
+  }
+}
+
 // continue-as-new stitching (stateBuilder.go:557-574): a parent that applied its new
 // run inherits the new run's error; a new run its parent never reached is NOT_APPLIED.
 __global__ void k_finalize(cdr_dev_batch B, cdr_out O) {
@@ -2066,7 +2206,9 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   // instantiations of k_replay_reg, each class followed by its hand-on chain (below)
   const bool carry = in->carry != nullptr;
   // class-decomposed replay of the register-table slices (their class-sorted blocks)
-  const bool cls = reg && !carry && !tasks && c->cls && in->cls_slab && in->cls_row0 && in->cls_rows;
+  // (with tasks: k_replay_cls<TASKS> on the lane slices, k_tasks_merge after; the PAR slices'
+  // tasks from k_replay_reg<TASKS>)
+  const bool cls = reg && !carry && c->cls && in->cls_slab && in->cls_row0 && in->cls_rows;
   const bool cls_fb = c->cls != 2;  // 2 (tests): no k_replay_reg pass for the CLS_RETRY entries
   auto retry_of = [](cdr_launch x) {
     x.retry = 1u;
@@ -2082,7 +2224,24 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
                        in->ev.n_slices;
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
-  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u, 0u, 0u, nullptr, nullptr, nullptr, nullptr, nullptr};
+  cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u, 0u, 0u, nullptr, nullptr, nullptr, nullptr, nullptr,
+               nullptr, nullptr};
+  // k_replay_cls<TASKS>: per-class staging lists (4 x the entry's task rows, 32 B per record) and
+  // per-entry headers (zeroed: no header = not a class-kernel entry)
+  const bool cls_tasks = cls && tasks && in->n_wfs > 0;
+  if (cls_tasks) {
+    if (c->tasks_caps != (const void*)in->caps || c->tasks_nwfs != in->n_wfs) {  // once per batch
+      cdr_wf_caps last;
+      HIPCHK(hipMemcpy(&last, in->caps + (in->n_wfs - 1), sizeof(last), hipMemcpyDeviceToHost));
+      c->tasks_caps = in->caps;
+      c->tasks_nwfs = in->n_wfs;
+      c->tasks_rows = last.xfer_off + last.xfer_cap + last.ttask_off + last.ttask_cap;
+    }
+    L.tstage = (uint64_t*)cdr_ws_get(c, WS_TSTAGE, 4ull * c->tasks_rows * 32ull + 32ull);
+    L.thead = (uint32_t*)cdr_ws_get(c, WS_THEAD, 32ull * in->n_wfs);
+    if (!L.tstage || !L.thead) return CDR_API_ENOMEM;
+    HIPCHK(hipMemsetAsync(L.thead, 0, 32ull * in->n_wfs, st));
+  }
   // retry lists (k_replay_cls -> k_replay_reg): counters zeroed on the launch stream
   // (carry-in: a second level of lists, k_replay_reg<12-activity> -> the general kernel,
   // counters 8 + class)
@@ -2216,7 +2375,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
                        order[0] == '6' && std::strchr(order, '1') < std::strchr(order, '2') &&
                        std::strchr(order, '1') < std::strchr(order, '3') && std::strchr(order, '1') < std::strchr(order, '4') &&
                        std::strchr(order, '1') < std::strchr(order, '5');
-  const bool gate = gate_ok && par && fk[6];
+  const bool gate = gate_ok && par && fk[6] && !tasks;  // (with tasks the PAR slices run k_replay_reg: nothing counts in)
   // (the 12-activity class only in a batch without PAR slices: with them, holding the other
   // classes back for it too cost C4 / C5 0.2-0.4 ms; without, it is C3's longest class and
   // gains 5%: 5.07 -> 4.84 ms)
@@ -2240,7 +2399,7 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       cdr_launch Lp = L;
       Lp.s0 = 0;
       typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
-      if (cls) {
+      if (cls && !tasks) {
         typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, true> LC;
         cdr_launch Lpg = with_list(Lp, 6);
         if (rws && gate) Lpg.pstart = rws + 15;
@@ -2250,10 +2409,9 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       if (tasks)
         hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR, CDR_WPE_REG, false, true>),
                            dim3(npar), dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6), Lp);
-      else if (!cls || cls_fb)
-        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR>),
-                           cls ? retry_grid(dim3(npar)) : dim3(npar), dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6),
-                           cls ? retry_of(with_list(Lp, 6)) : Lp);
+      else if (!cls)  // (with class blocks: its retry pass after the join, launch_retry)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR>), dim3(npar),
+                           dim3(CDR_SLICE_WIDTH), LY::bytes, sx(6), Lp);
     }
         break;
       case 0:
@@ -2270,15 +2428,22 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
         typedef ClsLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LC;
         cdr_launch Lg2 = with_list(Lr2, 1);
         if (rws && gate2) Lg2.pstart = rws + 15;
-        hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_CLS2>), gr2,
-                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(1), Lg2);
+        if (tasks)
+          hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_CLS2, false, true>),
+                             gr2, dim3(CDR_SLICE_WIDTH), LC::bytes + CLS_TQ_BYTES, sx(1), Lg2);
+        else
+          hipLaunchKernelGGL((k_replay_cls<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_CLS2>), gr2,
+                             dim3(CDR_SLICE_WIDTH), LC::bytes, sx(1), Lg2);
       }
-      if (tasks)
+      if (cls && tasks)  // the class kernel's staged tasks into the task slices (the handed-on
+                         // entries have no header: their tasks come from the retry pass)
+        hipLaunchKernelGGL(k_tasks_merge<CDR_SLICE_REG2>, gr2, dim3(CDR_SLICE_WIDTH), 9 * 65 * 8, sx(1), Lr2);
+      if (tasks && !cls)
         hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_REG, false, true>), gr2,
                            dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), Lr2);
-      else if (!cls || cls_fb)
-        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), cls ? retry_grid(gr2) : gr2,
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1), cls ? retry_of(with_list(Lr2, 1)) : Lr2);
+      else if (!cls)  // (with class blocks: its retry pass after the join, launch_retry)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), gr2, dim3(CDR_SLICE_WIDTH), LY::bytes, sx(1),
+                           Lr2);
     }
         break;
       case 2:
@@ -2303,15 +2468,22 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
       if (cls) {
         typedef ClsLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LC;
-        hipLaunchKernelGGL((k_replay_cls<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_CLS0>), gr0,
-                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(3), with_list(Lr0, 3));
+        if (tasks)
+          hipLaunchKernelGGL((k_replay_cls<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_CLS_T, false, true>),
+                             gr0, dim3(CDR_SLICE_WIDTH), LC::bytes + CLS_TQ_BYTES, sx(3), with_list(Lr0, 3));
+        else
+          hipLaunchKernelGGL((k_replay_cls<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_CLS0>), gr0,
+                             dim3(CDR_SLICE_WIDTH), LC::bytes, sx(3), with_list(Lr0, 3));
       }
-      if (tasks)
+      if (cls && tasks)  // the class kernel's staged tasks into the task slices (the handed-on
+                         // entries have no header: their tasks come from the retry pass)
+        hipLaunchKernelGGL(k_tasks_merge<CDR_SLICE_REG0>, gr0, dim3(CDR_SLICE_WIDTH), 9 * 65 * 8, sx(3), Lr0);
+      if (tasks && !cls)
         hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_REG, false, true>), gr0,
                            dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), Lr0);
-      else if (!cls || cls_fb)
-        hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), cls ? retry_grid(gr0) : gr0,
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3), cls ? retry_of(with_list(Lr0, 3)) : Lr0);
+      else if (!cls)  // (with class blocks: its retry pass after the join, launch_retry)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), gr0, dim3(CDR_SLICE_WIDTH), LY::bytes, sx(3),
+                           Lr0);
     }
         break;
       case 4:
@@ -2326,16 +2498,75 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
       if (cls) {
         typedef ClsLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LC;
-        hipLaunchKernelGGL((k_replay_cls<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_CLS>), gr1,
-                           dim3(CDR_SLICE_WIDTH), LC::bytes, sx(5), with_list(Lr1, 5));
+        if (tasks)
+          hipLaunchKernelGGL((k_replay_cls<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_CLS_T, false, true>),
+                             gr1, dim3(CDR_SLICE_WIDTH), LC::bytes + CLS_TQ_BYTES, sx(5), with_list(Lr1, 5));
+        else
+          hipLaunchKernelGGL((k_replay_cls<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_CLS>), gr1,
+                             dim3(CDR_SLICE_WIDTH), LC::bytes, sx(5), with_list(Lr1, 5));
       }
-      if (tasks)
+      if (cls && tasks)  // the class kernel's staged tasks into the task slices (the handed-on
+                         // entries have no header: their tasks come from the retry pass)
+        hipLaunchKernelGGL(k_tasks_merge<CDR_SLICE_REG>, gr1, dim3(CDR_SLICE_WIDTH), 9 * 65 * 8, sx(5), Lr1);
+      if (tasks && !cls)
         hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_REG, false, true>), gr1,
                            dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), Lr1);
-      else if (!cls || cls_fb)
-        hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), cls ? retry_grid(gr1) : gr1,
-                         dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5), cls ? retry_of(with_list(Lr1, 5)) : Lr1);
+      else if (!cls)  // (with class blocks: its retry pass after the join, launch_retry)
+        hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), gr1, dim3(CDR_SLICE_WIDTH), LY::bytes, sx(5),
+                           Lr1);
     }
+        break;
+    }
+  };
+  // the class kernels' retry passes (k_replay_reg over the slices where k_replay_cls handed an
+  // entry on), on the caller's stream after the join: a pass has nothing to do in a clean batch,
+  // yet its 256-VGPR workgroups, dispatched beside the class kernels, each wait for a whole
+  // SIMD's registers to free and hold back the other kernels' dispatch meanwhile (measured:
+  // the empty 12-activity pass "ran" 2.7-7 ms and slowed the small-table class kernel)
+  auto launch_retry = [&](int i) {
+    if (!cls || !cls_fb || carry) return;
+    switch (i) {
+      case 6:
+        if (par && !tasks) {
+          typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
+          cdr_launch Lp = L;
+          Lp.s0 = 0;
+          hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_PAR>), retry_grid(dim3(npar)),
+                             dim3(CDR_SLICE_WIDTH), LY::bytes, st, retry_of(with_list(Lp, 6)));
+        }
+        break;
+      case 1:
+        if (reg2) {
+          typedef RegLds<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX> LY;
+          if (tasks)
+            hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2, CDR_WPE_REG, false, true>),
+                               retry_grid(gr2), dim3(CDR_SLICE_WIDTH), LY::bytes, st, retry_of(with_list(Lr2, 1)));
+          else
+            hipLaunchKernelGGL((k_replay_reg<CDR_REG2_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG2>), retry_grid(gr2),
+                               dim3(CDR_SLICE_WIDTH), LY::bytes, st, retry_of(with_list(Lr2, 1)));
+        }
+        break;
+      case 3:
+        if (reg0) {
+          typedef RegLds<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX> LY;
+          if (tasks)
+            hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, CDR_WPE_REG, false, true>),
+                               retry_grid(gr0), dim3(CDR_SLICE_WIDTH), LY::bytes, st, retry_of(with_list(Lr0, 3)));
+          else
+            hipLaunchKernelGGL((k_replay_reg<CDR_REG0_NA, CDR_REG0_NT, CDR_REG0_NX, CDR_SLICE_REG0, 3>), retry_grid(gr0),
+                               dim3(CDR_SLICE_WIDTH), LY::bytes, st, retry_of(with_list(Lr0, 3)));
+        }
+        break;
+      case 5:
+        if (reg1) {
+          typedef RegLds<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX> LY;
+          if (tasks)
+            hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG, CDR_WPE_REG, false, true>),
+                               retry_grid(gr1), dim3(CDR_SLICE_WIDTH), LY::bytes, st, retry_of(with_list(Lr1, 5)));
+          else
+            hipLaunchKernelGGL((k_replay_reg<CDR_REG_NA, CDR_REG_NT, CDR_REG_NX, CDR_SLICE_REG>), retry_grid(gr1),
+                               dim3(CDR_SLICE_WIDTH), LY::bytes, st, retry_of(with_list(Lr1, 5)));
+        }
         break;
     }
   };
@@ -2377,6 +2608,8 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
       HIPCHK(hipEventRecord(c->join[j], c->side[j]));
       HIPCHK(hipStreamWaitEvent(st, c->join[j], 0));
     }
+  for (int i : {6, 1, 3, 5}) launch_retry(i);
+  HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used + 1] : c->ev[1], st));
   if (ring) {
     // keep ev[0..1] meaningful for cdr_last_kernel_ms as well

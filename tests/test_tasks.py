@@ -236,14 +236,16 @@ def test_gpu_tasks_fast_kernel(engine_gpu, cfg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,reg", [(2, True), (3, True), (3, False)])
-def test_gpu_tasks_device_batch(engine_gpu, cfg, reg):
+@pytest.mark.parametrize("cfg,reg,cls", [(2, True, None), (3, True, None), (3, False, None), (3, True, "host"),
+                                         (4, True, "host"), (5, True, "host")])
+def test_gpu_tasks_device_batch(engine_gpu, cfg, reg, cls):
     """The `bench.py --tasks` path: a synthetic sliced batch carrying task capacities
-    (DeviceBatch(tasks=True), a plan without wave / PAR slices, no class blocks) replayed by
-    cdr_replay_sliced_async — C2 on k_replay_fast<TASKS>, C3's register-table slices on
-    k_replay_reg<..., TASKS> (and, with the register-table path off, every C3 slice on the
-    general kernel's TASKS instantiation) — equals the oracle's task lists for the same
-    workflows, entry by entry and byte for byte."""
+    (DeviceBatch(tasks=True), a plan without wave / PAR slices) replayed by
+    cdr_replay_sliced_async — C2 on k_replay_fast<TASKS>; C3's register-table slices on
+    k_replay_reg<..., TASKS> without class blocks (and, with the register-table path off, every
+    C3 slice on the general kernel's TASKS instantiation); with class blocks (cls="host", C3-C5)
+    on k_replay_cls<..., TASKS> + k_tasks_merge, the entries they hand on on k_replay_reg<TASKS>
+    — equals the oracle's task lists for the same workflows, entry by entry and byte for byte."""
     import ctypes as C
 
     import numpy as np
@@ -252,7 +254,7 @@ def test_gpu_tasks_device_batch(engine_gpu, cfg, reg):
     import oracle
     from cadence_amd.synth import DeviceBatch
     n, seed = 1500, 0x5EED0410 + cfg
-    db = DeviceBatch(torch, cfg, np.arange(n, dtype=np.uint32), seed, plan_mode=0, cls=None, tasks=True)
+    db = DeviceBatch(torch, cfg, np.arange(n, dtype=np.uint32), seed, plan_mode=0, cls=cls, tasks=True)
     L = abi.lib()
     ctx = L.cdr_create(torch.cuda.current_device(), None)
     try:
