@@ -461,7 +461,13 @@ int cdr_set_plan_mode(cdr_ctx* ctx, uint32_t mode);
  * instantiations (their slices) or the general kernel; an entry whose loaded state
  * outgrows its variant is handed on, on the device, to the 12-activity variant and then to
  * the general kernel (replay_reg.inc).  Never plan a loaded entry onto a fast or wave slice
- * (cdr_plan_caps / cdr_plan_ndc_apply never do: CDR_CAP_LOADED). */
+ * (cdr_plan_caps / cdr_plan_ndc_apply never do: CDR_CAP_LOADED).
+ * Task lists (out->transfer set) with class-sorted blocks (in->cls_slab): the class kernels
+ * stage each entry's tasks per class in the context's workspace and merge them on the device
+ * (replay_cls.inc, k_tasks_merge); the workspace is sized from the batch's task-slice total,
+ * which the first launch over a batch (a new in->caps pointer or entry count) reads back with
+ * one blocking 40-byte copy of in->caps[n_wfs - 1] — later launches over the same batch stay
+ * fully asynchronous.  A plan with task lists must have no wave slices (CDR_API_EINVAL). */
 int cdr_replay_sliced_async(cdr_ctx* ctx, const cdr_dev_batch* in, const cdr_out* out, void* stream);
 
 /* Whole pipeline for host-resident data: plan + pack + H2D + replay + D2H on `stream`

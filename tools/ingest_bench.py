@@ -23,10 +23,16 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--wfs", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cls", action="store_true",
+                    help="the plan also builds the class-sorted blocks on the device (CDR_CLS_BUILD): class kernels replay")
+    ap.add_argument("--par", action="store_true", help="plan with CDR_PLAN_PAR (long histories on PAR slices)")
     args = ap.parse_args()
     L = abi.lib()
     hip = engine._hip()
     eng = engine.Engine(0)
+    if args.cls:
+        L.cdr_set_cls_path(eng.ctx, abi.CLS_BUILD)
+    pmode = abi.PLAN_WAVE | (abi.PLAN_PAR if args.par else 0)
     b = engine.synth_batch(args.config, args.wfs, seed=0x5EED0000 + args.config)
     n_ev = len(b.events)
     enc = ingest.encode_batch(b, threads=16)
@@ -71,7 +77,7 @@ def main():
         tot = abi.CdrTotals()
         db = abi.CdrDevBatch()
         t2 = time.perf_counter()
-        assert L.cdr_ingest_plan(eng.ctx, C.byref(out), C.byref(meta[0]), abi.PLAN_WAVE, C.byref(db), caps,
+        assert L.cdr_ingest_plan(eng.ctx, C.byref(out), C.byref(meta[0]), pmode, C.byref(db), caps,
                                  C.byref(tot), None) == 0
         t3 = time.perf_counter()
         if rep:  # the first round grows the workspace
@@ -121,6 +127,7 @@ def main():
     dec_s, plan_s, rep_s = float(np.median(dec_t)), float(np.median(plan_t)), float(np.median(rep_t))
     print(json.dumps({
         "config": args.config, "workflows": args.wfs, "events": n_ev, "blobs": int(inp.n_blobs),
+        "class_blocks": bool(args.cls), "plan_par": bool(args.par),
         "blob_bytes": int(enc.blob_bytes.nbytes), "blob_h2d_s": h2d_s,
         "device_decode_s": dec_s, "device_plan_pack_s": plan_s,
         "device_events_per_s": n_ev / (dec_s + plan_s), "decode_gbs": enc.blob_bytes.nbytes / dec_s / 1e9,
