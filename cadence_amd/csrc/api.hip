@@ -378,8 +378,8 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   // class-sorted blocks of the register-table slices (k_replay_cls), packed on the host
   // beside the slab when the context asks for them (CDR_CLS_BUILD / CDR_CLS_ALONE): by
   // default a batch replayed once goes to k_replay_reg, since the block's packing and
-  // H2D cost more than the class kernel saves
-  if (ctx->cls >= CDR_CLS_ALONE && ctx->reg && ctx->fast && !tasks &&
+  // H2D cost more than the class kernel saves (with task lists: k_replay_cls<TASKS>)
+  if (ctx->cls >= CDR_CLS_ALONE && ctx->reg && ctx->fast &&
       db.n_reg_slices + db.n_reg2_slices + db.n_reg0_slices + db.n_par_slices > 0 &&
       b->cluster.n_clusters <= (int)CDR_REG_NCL) {
     // the uploads above read host memory this call owns: pack the blocks meanwhile

@@ -687,6 +687,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
   int64_t call_first_id = 0, prev_id = 0, prev_ver = 0;
   uint32_t call_first_k = 0, call_idx = 0;
   bool newrun_applied = false, stop_at_call_end = false;
+  uint32_t nr_call = 0xFFFFFFFFu;  // the call that applied the new run (a cluster panic there: never attempted)
   int32_t err = len == 0 ? CDR_E_HISTORY_EMPTY : CDR_OK;
   int64_t err_id = 0;
   uint32_t err_k = 0;
@@ -924,6 +925,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
         err = CDR_P_UNKNOWN_CLUSTER;
         err_id = call_first_id;
         err_k = call_first_k;
+        newrun_applied = newrun_applied && nr_call != call_idx;
       } else if (src != B_.cluster.current_cluster) {
         RS->lri_version[src] = prev_ver;
         RS->lri_last_event_id[src] = prev_id;
@@ -1546,6 +1548,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
           PFAIL(f, CDR_E_NEWRUN_HISTORY_EMPTY);
           const bool ap = mine && !f;
           newrun_applied |= ap;  // the new run replays in its own lane; k_finalize joins
+          nr_call = ap ? call_idx : nr_call;
           const bool f2 = ap && !transition_ok(x_state, x_close, CDR_STATE_COMPLETED, CDR_CLOSE_CONTINUED_AS_NEW);
           PFAIL(f2, CDR_E_INVALID_STATE_TRANSITION);
           const bool ok = ap && !f2;
@@ -1572,6 +1575,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) __attribute__((amdgpu_waves_per_eu
         err = CDR_P_UNKNOWN_CLUSTER;
         err_id = call_first_id;
         err_k = call_first_k;
+        newrun_applied = newrun_applied && nr_call != call_idx;
       } else if (src != B_.cluster.current_cluster && err == CDR_OK) {
         RS->lri_version[src] = prev_ver;
         RS->lri_last_event_id[src] = prev_id;

@@ -187,6 +187,34 @@ def test_gpu_tasks_configs(engine_gpu, cfg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [3, 4, 5])
+@pytest.mark.parametrize("err", [0.0, 0.2])
+def test_gpu_tasks_class_path(engine_gpu, cfg, err):
+    """Task lists from the class kernels (k_replay_cls<TASKS> staging + k_tasks_merge) through
+    the host-buffer call: with the k_replay_reg<TASKS> pass behind them (CLS_BUILD) every
+    entry's state and lists equal the oracle's — injected faults included, whose entries the
+    class kernel hands on; alone (CLS_ALONE) every entry it kept has the oracle's lists, and on
+    a clean batch it keeps every entry."""
+    import oracle
+    b = engine.synth_batch(cfg, 600, seed=0x5EED0500 + cfg + int(err * 10), error_rate=err)
+    ref = oracle.replay(b, tasks=True)
+    old = engine_gpu.set_cls(abi.CLS_BUILD)
+    try:
+        got = engine_gpu.replay(b, tasks=True)
+        bad = engine.compare(b, got, ref) + engine.compare_tasks(b, got, ref)
+        assert not bad, "\n".join(bad[:10])
+        engine_gpu.set_cls(abi.CLS_ALONE)
+        alone = engine_gpu.replay(b, tasks=True)
+    finally:
+        engine_gpu.set_cls(old)
+    kept = [w for w in range(b.n_wfs) if alone.result[w].code == abi.OK]
+    assert not engine.compare_tasks(b, alone, ref)  # (entries OK in both)
+    assert sum(alone.task_rows(w, "xfer").__len__() for w in kept) > 0
+    if err == 0.0:
+        assert len(kept) == b.n_wfs
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("builder", [abi.BUILDER_LOCAL, abi.BUILDER_2DC, abi.BUILDER_NDC])
 def test_gpu_tasks_builders(engine_gpu, builder):
     _check_tasks(engine_gpu, engine.synth_batch(0, 300, seed=51 + builder, builder=builder, error_rate=0.2))
