@@ -20,4 +20,5 @@ done
 timeout -k 10 400 python -u bench.py --config 4 --long-stride 125000 --no-cpu-baseline --no-stream-peak --no-refresh > $out/bench_c4_long.json 2> $out/bench_c4_long.log || exit 1
 timeout -k 10 400 python -u bench.py --tasks --steps 10 --warmup 2 --no-refresh --no-stream-peak > $out/bench_c2_tasks.json 2> $out/bench_c2_tasks.log || exit 1
 timeout -k 10 400 python -u bench.py --tasks --config 3 --steps 10 --warmup 2 --no-refresh --no-stream-peak > $out/bench_c3_tasks.json 2> $out/bench_c3_tasks.log || exit 1
+timeout -k 10 400 python -u bench.py --tasks --config 5 --steps 10 --warmup 2 --no-refresh --no-stream-peak > $out/bench_c5_tasks.json 2> $out/bench_c5_tasks.log || exit 1
 echo "bench set done"
