@@ -3,5 +3,5 @@
 # run through the carry tests and the class/newrun tests.
 set -o pipefail
 out=gpurun_out/${1:-r5za}; mkdir -p $out
-CDR_LIB=variants/libcdr_epiint.so timeout -k 10 300 python -u -m pytest tests/test_carry.py tests/test_cls_gpu.py -m gpu -q --timeout 120 --timeout-method thread > $out/epiint.log 2>&1; echo "rc=$?" >> $out/epiint.log
+CDR_LIB=variants/libcdr_${V:-epiint}.so timeout -k 10 300 python -u -m pytest tests/test_carry.py tests/test_cls_gpu.py -m gpu -q --timeout 120 --timeout-method thread > $out/${V:-epiint}.log 2>&1; echo "rc=$?" >> $out/${V:-epiint}.log
 echo done
