@@ -287,7 +287,8 @@ CdrDevBatch = _S("cdr_dev_batch", [
     ("n_fast_slices", u32), ("n_wave_slices", u32), ("n_reg_slices", u32), ("n_reg2_slices", u32),
     ("n_reg0_slices", u32), ("n_par_slices", u32), ("class_lo", u32 * 6), ("class_hi", u32 * 6),
     ("cluster", CdrClusterMeta), ("now_ns", i64), ("uuid_seed", u64), ("carry", C.c_void_p),
-    ("cls_slab", C.c_void_p), ("cls_row0", C.c_void_p), ("cls_rows", C.c_void_p), ("skip", C.c_void_p)])
+    ("cls_slab", C.c_void_p), ("cls_row0", C.c_void_p), ("cls_rows", C.c_void_p), ("skip", C.c_void_p),
+    ("task_rows", u64)])
 CdrNdcRound = _S("cdr_ndc_round", [("tasks", C.c_void_p), ("task_items", C.c_void_p), ("rebuild", CdrDevBatch),
                                    ("rebuild_out", CdrOut), ("apply", CdrDevBatch), ("apply_out", CdrOut),
                                    ("dec", C.c_void_p), ("refresh_now", i64), ("refresh_flags", u32), ("_pad", u32)])

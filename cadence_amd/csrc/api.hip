@@ -370,6 +370,7 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
     dout.transfer = (cdr_task*)dz(WS_O_XFER, tot->xfer * sizeof(cdr_task));
     dout.timer_tasks = (cdr_task*)dz(WS_O_TTASK, tot->ttask * sizeof(cdr_task));
     dout.n_tasks = (uint32_t*)dz(WS_O_NTASKS, (uint64_t)b->n_wfs * 2 * sizeof(uint32_t));
+    db.task_rows = tot->xfer + tot->ttask;
   }
   if (oom || dev_err) {
     (void)hipStreamSynchronize(st);  // no copy may still read the host vectors

@@ -98,9 +98,6 @@ struct cdr_ctx {
   cdr_one_host one;
   // k_replay_cls<TASKS>: the task slices' total rows of the last batch seen (its caps array
   // and entry count), read back once per batch to size the staging lists
-  const void* tasks_caps = nullptr;
-  uint32_t tasks_nwfs = 0;
-  uint64_t tasks_rows = 0;
 };
 
 // pinned host staging `slot` of at least `bytes` (grow-only; contents undefined); nullptr

@@ -559,6 +559,7 @@ struct cdr_launch {
   // headers k_tasks_merge reads (replay_cls.inc)
   uint64_t* tstage;
   uint32_t* thead;
+  uint64_t trows;  // records tstage holds (a staging index at or past it: the entry is handed on)
 };
 // result code k_replay_cls (or a carry-in k_replay_reg below the 12-activity variant) leaves
 // on an entry it hands to k_replay_reg (never returned)
@@ -1864,6 +1865,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) void k_tasks_merge(cdr_launch L) {
     cur[c] = 0;
   }
   uint32_t n_xt = 0, n_tt = 0;
+  bool lost = false;  // a record past the entry's task slice (capacities too small)
   auto key = [](const Rec& r) { return (uint32_t)(r.w0 >> 32); };
   while (__builtin_amdgcn_ballot_w64(valid && (key(hd[0]) & key(hd[1]) & key(hd[2]) & key(hd[3])) != 0xFFFFFFFFu)) {
     // the head with the lowest history index (two lists never tie: an event is in one class)
@@ -1923,12 +1925,14 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) void k_tasks_merge(cdr_launch L) {
       }
     }
     coop_put<8>(dst, t, on && fits, 0);
+    lost |= on && !fits;
     n_tt += (on && fits && tim) ? 1u : 0u;
     n_xt += (on && fits && !tim) ? 1u : 0u;
   }
-  if (valid) {
-    KA()->O.n_tasks[2ull * (uint64_t)w] = n_xt;
-    KA()->O.n_tasks[2ull * (uint64_t)w + 1] = n_tt;
+  if (valid) {  // (a truncated list is not returned: the entry reports the bad capacities)
+    KA()->O.n_tasks[2ull * (uint64_t)w] = lost ? 0u : n_xt;
+    KA()->O.n_tasks[2ull * (uint64_t)w + 1] = lost ? 0u : n_tt;
+    if (lost) KA()->O.result[w].code = CDR_E_BAD_INPUT;
   }
 }
 
@@ -2229,19 +2233,23 @@ int cdr_replay_sliced_async(cdr_ctx* c, const cdr_dev_batch* in, const cdr_out* 
   const bool ring = c->ring_used + 2 <= c->ring.size();
   HIPCHK(hipEventRecord(ring ? c->ring[c->ring_used] : c->ev[0], st));
   cdr_launch L{*in, *out, la, lt, fast ? 1u : 0u, reg ? 1u : 0u, 0u, 0u, nullptr, nullptr, nullptr, nullptr, nullptr,
-               nullptr, nullptr};
+               nullptr, nullptr, 0ull};
   // k_replay_cls<TASKS>: per-class staging lists (4 x the entry's task rows, 32 B per record) and
   // per-entry headers (zeroed: no header = not a class-kernel entry)
   const bool cls_tasks = cls && tasks && in->n_wfs > 0;
   if (cls_tasks) {
-    if (c->tasks_caps != (const void*)in->caps || c->tasks_nwfs != in->n_wfs) {  // once per batch
+    // the task-slice rows: the caller's (cdr_dev_batch.task_rows), else the last entry's
+    // offsets + capacities read on the launch stream (every launch: the same caps buffer may
+    // hold another batch's capacities next time)
+    uint64_t rows = in->task_rows;
+    if (rows == 0) {
       cdr_wf_caps last;
-      HIPCHK(hipMemcpy(&last, in->caps + (in->n_wfs - 1), sizeof(last), hipMemcpyDeviceToHost));
-      c->tasks_caps = in->caps;
-      c->tasks_nwfs = in->n_wfs;
-      c->tasks_rows = last.xfer_off + last.xfer_cap + last.ttask_off + last.ttask_cap;
+      HIPCHK(hipMemcpyAsync(&last, in->caps + (in->n_wfs - 1), sizeof(last), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      rows = (uint64_t)last.xfer_off + last.xfer_cap + last.ttask_off + last.ttask_cap;
     }
-    L.tstage = (uint64_t*)cdr_ws_get(c, WS_TSTAGE, 4ull * c->tasks_rows * 32ull + 32ull);
+    L.tstage = (uint64_t*)cdr_ws_get(c, WS_TSTAGE, 4ull * rows * 32ull + 32ull);
+    L.trows = 4ull * rows;
     L.thead = (uint32_t*)cdr_ws_get(c, WS_THEAD, 32ull * in->n_wfs);
     if (!L.tstage || !L.thead) return CDR_API_ENOMEM;
     HIPCHK(hipMemsetAsync(L.thead, 0, 32ull * in->n_wfs, st));

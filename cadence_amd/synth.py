@@ -179,6 +179,7 @@ class DeviceBatch:
         if tasks:
             sizes.update({"transfer": tot.xfer * C.sizeof(abi.CdrTask), "timer_tasks": tot.ttask * C.sizeof(abi.CdrTask),
                           "n_tasks": 2 * info.n_entries * 4})
+            db.task_rows = tot.xfer + tot.ttask
         self.out_bytes = sum(sizes.values())
         self.out_t = {}
         for k, nb in sizes.items():

@@ -248,6 +248,10 @@ typedef struct cdr_dev_batch {
    * their lanes stay idle and their output records untouched (the caller marks them,
    * e.g. result.code = CDR_NOT_RUN).  A masked launch replays without class-sorted blocks. */
   const uint8_t* skip;
+  /* task-slice rows of the batch (cdr_totals.xfer + cdr_totals.ttask), used to size the class
+   * kernels' task staging when the output asks for task lists; 0 = unknown: the launcher
+   * reads the last entry's capacities from caps (a copy and a stream synchronisation) */
+  uint64_t task_rows;
 } cdr_dev_batch;
 
 /* Class-sorted blocks (replay_cls.inc).  Every register-table slice (CDR_SLICE_REG /

@@ -176,10 +176,8 @@ def test_newrun_cluster_panic_all_kernels(engine_gpu):
     """A 2DC entry whose continue-as-new call ends on a version of no known cluster: the
     reference's ClusterNameForFailoverVersion panic fires at that call's first event
     (mutableStateBuilder.go:561-581, before the events), so the new run is never attempted —
-    result code CDR_P_UNKNOWN_CLUSTER without CDR_RF_NEWRUN_APPLIED — on the general and wave
-    kernels, which check a call's cluster when the call ends.  (The register-table kernel
-    still reports the flag in this case: its fix exposed a carry-in LastReplicationInfo
-    difference on unrelated entries, DESIGN.md §3 "Round 5" — open.)"""
+    result code CDR_P_UNKNOWN_CLUSTER without CDR_RF_NEWRUN_APPLIED — on every kernel that
+    checks the call ends lazily (register-table, general, wave) and through the class path."""
     import oracle
     b = engine.synth_batch(4, 600, seed=0x5EED0506, error_rate=0.2)
     ref = oracle.replay(b)
@@ -187,13 +185,20 @@ def test_newrun_cluster_panic_all_kernels(engine_gpu):
     assert case and all(ref.result[w].flags & abi.RF_NEWRUN_APPLIED == 0 for w in case)
     L = abi.lib()
     runs = {}
-    old_mode = engine_gpu.set_plan_mode(0)
+    old_mode = engine_gpu.set_plan_mode(0)  # lane slices: register-table / general kernels
     try:
+        runs["reg"] = engine_gpu.replay(b)
         L.cdr_set_reg_path(engine_gpu.ctx, 0)
         runs["general"] = engine_gpu.replay(b)
         L.cdr_set_reg_path(engine_gpu.ctx, 1)
         engine_gpu.set_plan_mode(abi.PLAN_WAVE | abi.PLAN_WAVE_ALL)
         runs["wave"] = engine_gpu.replay(b)
+        engine_gpu.set_plan_mode(abi.PLAN_WAVE | abi.PLAN_PAR)
+        old_cls = engine_gpu.set_cls(abi.CLS_BUILD)
+        try:
+            runs["class"] = engine_gpu.replay(b)
+        finally:
+            engine_gpu.set_cls(old_cls)
     finally:
         L.cdr_set_reg_path(engine_gpu.ctx, 1)
         engine_gpu.set_plan_mode(old_mode)
