@@ -385,6 +385,7 @@ EXPORTS = {
     "cdr_build_flags": (u32, []),
     "cdr_timing_begin": (i32, [C.c_void_p, u32]),
     "cdr_timing_read": (i32, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(u32)]),
+    "cdr_stream_copy_async": (i32, [C.c_void_p, C.c_void_p, u64, C.c_void_p]),
     "cdr_synth_shards": (i32, [u64, i32, C.c_void_p]),
     "cdr_synth_weights": (i32, [C.POINTER(CdrSynthParams), u64, C.c_void_p]),
     "cdr_synth_ndc_tasks": (i32, [C.POINTER(CdrSynthParams), i32, C.c_void_p, C.c_void_p, u32]),

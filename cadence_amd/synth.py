@@ -25,6 +25,25 @@ for _name, _b in (("WorkflowExecutionStarted", 96), ("ActivityTaskScheduled", 48
                   ("ActivityTaskStarted", 4), ("DecisionTaskTimedOut", 4), ("ChildWorkflowExecutionStarted", 4),
                   ("WorkflowExecutionContinuedAsNew", 4), ("UpsertWorkflowSearchAttributes", 8)):
     A_TYPE[abi.EV[_name]] = _b
+def encoded_event_bytes(tf) -> int:
+    """Bytes of the packed input the fast kernel must read for these events (type_flags
+    column `tf`, padding cells excluded): the 4-B type word, event_id / version unless the
+    packer's delta bits imply them (CDR_SEF_ID_NEXT / VER_SAME), the operand columns the
+    type's need bits name, and the arena record of WorkflowExecutionStarted /
+    ActivityTaskScheduled.  The canonical SURVEY §8(d) price (48 + A[type]) assumes every
+    core column is read; this is what the encoding leaves to read."""
+    tf = np.asarray(tf)
+    ty = tf & 0xFF
+    real = ty < abi.EV["UpsertWorkflowSearchAttributes"] + 1
+    b = np.full(tf.shape, 4, np.int64)
+    b += np.where(tf & abi.SEF_ID_NEXT, 0, 8) + np.where(tf & abi.SEF_VER_SAME, 0, 8)
+    for bit, w in ((1 << 16, 8), (1 << 17, 8), (1 << 18, 8), (1 << 19, 4), (1 << 20, 4)):  # CDR_SEF_NEED_*
+        b += np.where(tf & bit, w, 0)
+    b += np.where(ty == abi.EV["WorkflowExecutionStarted"], C.sizeof(abi.AttrStarted), 0)
+    b += np.where(ty == abi.EV["ActivityTaskScheduled"], C.sizeof(abi.AttrATSched), 0)
+    return int(b[real].sum())
+
+
 ROW_BYTES = {"n_activity": 128, "n_timer": 32, "n_child": 48, "n_cancel": 24, "n_signal": 40}
 RESULT_DTYPE = np.dtype([("code", "<i4"), ("flags", "<u4"), ("fid", "<i8"), ("fix", "<i8"),
                          ("n_activity", "<u4"), ("n_timer", "<u4"), ("n_child", "<u4"), ("n_cancel", "<u4"),
@@ -190,8 +209,11 @@ class DeviceBatch:
         torch.cuda.synchronize()
         self.h2d_s = time.perf_counter() - t0
         self.in_bytes = self.h_slab.nbytes + self.h_arena.nbytes + self.cls_bytes  # uploaded
-        types = abi.slab_columns(self.h_slab, self.h_row0, self.h_slen, ("type_flags",))["type_flags"] & 0xFF
+        tf = abi.slab_columns(self.h_slab, self.h_row0, self.h_slen, ("type_flags",))["type_flags"]
+        types = tf & 0xFF
         self.type_counts = np.bincount(types, minlength=256)
+        self.encoded_event_bytes = encoded_event_bytes(tf)
+        del tf
         self.n_events = int(self.type_counts[:abi.EV["UpsertWorkflowSearchAttributes"] + 1].sum())
 
     def build_cls(self, ctx):
@@ -267,3 +289,9 @@ class DeviceBatch:
         repl = int(((bld == abi.BUILDER_2DC) & ok).sum()) * 32
         wf_bytes = len(arr) * (256 + 8) + 16 * vh + repl
         return ev_bytes + wf_bytes + rows, n_ok, ev_bytes, wf_bytes, rows
+
+    def encoded_bytes(self, res):
+        """encoded_event_bytes + the same per-workflow and pending-row output bytes as
+        algorithmic_bytes: the bytes one fast-kernel launch cannot avoid moving."""
+        _, _, _, wf_bytes, rows = self.algorithmic_bytes(res)
+        return self.encoded_event_bytes + wf_bytes + rows
