@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise tools/gpu_calib.sh (gpurun_out/calib/) into profiles/<name>.json + .txt:
+"""Summarise `tools/gpu.sh calib` (gpurun_out/calib/) into profiles/<name>.json + .txt:
 per calibration kernel, the known bytes it moves (tools/calib.hip, printed by the plain run)
 against FETCH_SIZE / WRITE_SIZE (KiB) and the EA request counters of the rocprofv3 --pmc
 passes, averaged over the kernel's dispatches.  The ratio counter_bytes / known_bytes is the
@@ -63,7 +63,7 @@ def main():
                               for c in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_WRREQ_sum",
                                         "TCC_EA0_WRREQ_64B_sum") if c in e))
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    json.dump({"source": "tools/calib.hip under rocprofv3 --pmc (tools/gpu_calib.sh)", "kernels": out},
+    json.dump({"source": "tools/calib.hip under rocprofv3 --pmc (tools/gpu.sh calib)", "kernels": out},
               open(os.path.join(ROOT, "profiles", name + ".json"), "w"), indent=1)
     open(os.path.join(ROOT, "profiles", name + ".txt"), "w").write("\n".join(rows) + "\n")
     print("\n".join(rows))
