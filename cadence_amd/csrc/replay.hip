@@ -2645,7 +2645,7 @@ uint32_t cdr_build_flags(void) {
   f |= 1u;
 #endif
   if (CDR_PAR_PRIO != 0 || CDR_FDEPTH != 2 || CDR_DEPTH != 1 || CDR_TYPED != 1 || CDR_FAST_DELTA != 1 ||
-      CDR_VHBF != 1 || CDR_CLS_DEPTH != 1 || CDR_CLS_PDEPTH != 4 || CDR_CLS_DEPTH_PAR != 4 ||
+      CDR_VHBF != 1 || CDR_VHQUICK != 1 || CDR_CLS_DEPTH != 1 || CDR_CLS_PDEPTH != 4 || CDR_CLS_DEPTH_PAR != 4 ||
       CDR_CLS_PDEPTH_PAR != 16 || CDR_WPE_FAST != 3 || CDR_WPE != 3 || CDR_WPE_CLS != 4 || CDR_WPE_CLS0 != 4 ||
       CDR_WPE_CLS2 != 2 || FAST_CK != 8u || CDR_FAST_TBUF != 5 || CDR_WPE_FAST_TBUF != 2)
     f |= 2u;
