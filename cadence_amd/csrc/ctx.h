@@ -38,6 +38,7 @@ enum cdr_ws_slot {
   WS_NDC_SKIP_RB, WS_NDC_SKIP_AP, WS_NDC_INMEM, WS_NDC_SRC, WS_NDC_CARRY,
   WS_RETRY,  // the class kernels' retry lists: 8 counters, then a list of n_slices per class
   WS_TSTAGE, WS_THEAD,  // k_replay_cls<TASKS>: staged task records, per-entry headers (k_tasks_merge)
+  WS_CLS_MAP,  // the device class sort's per-event (class, position), type word and annotation (k_cls_count -> k_cls_gather)
   WS_NUM
 };
 
@@ -88,6 +89,9 @@ struct cdr_ctx {
   int wait_value = -1;  // hipStreamWaitValue32 usable on the device (-1: not asked yet)
   // grow-only device workspace of the host-buffer calls
   void* ws[WS_NUM] = {};
+  // the batch whose class-sort map WS_CLS_MAP holds (cdr_cls_plan_async), checked by cdr_cls_pack_async
+  const void* cls_map_slab = nullptr;
+  uint64_t cls_map_rows = 0;
   uint64_t ws_bytes[WS_NUM] = {};
   // grow-only pinned host staging of the host-buffer calls (the packed slab and arena):
   // no page faults or zero-fill after the first call, and the H2D copy reads page-locked

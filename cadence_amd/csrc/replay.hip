@@ -2137,7 +2137,12 @@ int cdr_cls_plan_async(cdr_ctx* c, const cdr_dev_batch* in, uint32_t* cls_rows, 
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipSetDevice(c->device));
   const uint32_t ns = in->ev.n_slices;
-  if (ns) hipLaunchKernelGGL(k_cls_count, dim3(ns), dim3(CDR_SLICE_WIDTH), 0, st, *in, cls_rows, cls_row0);
+  // the per-event map k_cls_gather transposes with (16 B per slab element); without the room for
+  // it, cdr_cls_pack_async scatters lane by lane (k_cls_fill)
+  void* map = ns ? cdr_ws_get(c, WS_CLS_MAP, in->ev.n_rows * CDR_SLICE_WIDTH * 16ull) : nullptr;
+  c->cls_map_slab = map ? (const void*)in->ev.slab : nullptr;
+  c->cls_map_rows = map ? in->ev.n_rows : 0;
+  if (ns) hipLaunchKernelGGL(k_cls_count, dim3(ns), dim3(CDR_SLICE_WIDTH), 0, st, *in, cls_rows, cls_row0, map);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_cls_scan, dim3(1), dim3(1024), 0, st, cls_row0, ns);
   HIPCHK(hipGetLastError());
@@ -2148,8 +2153,18 @@ int cdr_cls_pack_async(cdr_ctx* c, const cdr_dev_batch* in, void* stream) {
   if (!c || !in || !in->cls_slab || !in->cls_row0 || !in->cls_rows) return CDR_API_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipSetDevice(c->device));
+  const bool map = c->ws[WS_CLS_MAP] && c->cls_map_slab == (const void*)in->ev.slab &&
+                   c->cls_map_rows == in->ev.n_rows && in->ev.n_rows;
+  if (map && in->ev.n_slices) {  // the LDS transposition, then the slices too long for it
+    static const bool attr = hipFuncSetAttribute((const void*)k_cls_gather, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)CLS_G_LDS) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL(k_cls_gather, dim3(in->ev.n_slices), dim3(CLS_G_THREADS), CLS_G_LDS, st, *in,
+                       (const void*)c->ws[WS_CLS_MAP]);
+    HIPCHK(hipGetLastError());
+  }
   if (in->ev.n_slices)
-    hipLaunchKernelGGL(k_cls_fill, dim3(in->ev.n_slices), dim3(CDR_SLICE_WIDTH), 0, st, *in);
+    hipLaunchKernelGGL(k_cls_fill, dim3(in->ev.n_slices), dim3(CDR_SLICE_WIDTH), 0, st, *in, map ? 0 : 1);
   HIPCHK(hipGetLastError());
   return CDR_API_OK;
 }

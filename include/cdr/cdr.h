@@ -443,11 +443,16 @@ int cdr_pack_cls(const cdr_slices* s, const cdr_wf_desc* wfs, const uint32_t* cl
  * (device, n_slices * 4) = the rows of each class region of every register-table slice
  * (0 for the others) and cls_row0[0..n_slices] (device, n_slices + 1) their exclusive
  * scan; the caller reads the total, cls_row0[n_slices], and allocates cls_slab at
- * total * CDR_ROW_BYTES bytes.  Asynchronous. */
+ * total * CDR_ROW_BYTES bytes.  It also keeps, in the context's workspace (16 B per slab
+ * element), each event's class position, block type word and annotation for the write pass.
+ * Asynchronous. */
 int cdr_cls_plan_async(cdr_ctx* ctx, const cdr_dev_batch* in, uint32_t* cls_rows, uint64_t* cls_row0,
                        void* stream);
 /* Write pass: the class-sorted blocks into in->cls_slab at in->cls_row0 / cls_rows (from
- * cdr_cls_plan_async on the same batch).  Asynchronous. */
+ * cdr_cls_plan_async on the same batch, the last plan on this context): a transposition
+ * through LDS, column by column, one workgroup per slice (slices longer than its LDS budget,
+ * and every slice when the plan's map is not this batch's: a per-lane scatter).
+ * Asynchronous. */
 int cdr_cls_pack_async(cdr_ctx* ctx, const cdr_dev_batch* in, void* stream);
 
 /* Slicing mode of cdr_replay_batch's planning (CDR_PLAN_*; default CDR_PLAN_WAVE).
@@ -733,7 +738,7 @@ int cdr_timing_read(cdr_ctx* ctx, float* ms, uint32_t* n);
 const char* cdr_version(void);
 
 /* The measurement's bandwidth ceiling: copy `bytes` (a multiple of 64) from src to dst on
- * `stream` with 16-B vector loads and stores, four in flight per lane (the MI355X guide's
+ * `stream` with 16-B vector loads and stores, one per lane, one-shot grid (the MI355X guide's
  * float4 copy, ~6.3 TB/s of read + write).  bench.py times it beside the replay kernel. */
 int cdr_stream_copy_async(void* dst, const void* src, uint64_t bytes, void* stream);
 
