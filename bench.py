@@ -971,7 +971,9 @@ def main():
     cls_src = None if args.no_cls else "device" if args.cls_in_step else "host"
     db = DeviceBatch(torch, args.config, mine, args.seed,
                      plan_mode=0 if args.no_wave else abi.PLAN_WAVE
-                     | (abi.PLAN_WAVE_ALL if args.wave_all else 0) | (0 if args.no_par else abi.PLAN_PAR),
+                     | (abi.PLAN_WAVE_ALL if args.wave_all else 0) | (0 if args.no_par else abi.PLAN_PAR)
+                     # task batches: the PAR histories one per slice (their slices replay on k_replay_reg<TASKS>)
+                     | (abi.PLAN_PAR_SOLO if args.tasks and not args.no_par else 0),
                      ctx_for_cls=ctx, cls=cls_src, long_stride=args.long_stride, tasks=args.tasks)
     if args.no_cls:
         L.cdr_set_cls_path(ctx, abi.CLS_OFF)

@@ -243,6 +243,7 @@ CAP_WAVE = 0x2
 PLAN_WAVE = 0x1
 PLAN_WAVE_ALL = 0x2  # with PLAN_WAVE: lane-friendly (CAP_LANE) entries on the wave kernel too
 PLAN_PAR = 0x8  # with PLAN_WAVE: long register-table histories to CDR_SLICE_PAR lane slices (CDR_PLAN_PAR)
+PLAN_PAR_SOLO = 0x10  # with PLAN_PAR: every PAR history alone in its slice, the 512 longest at most (task batches)
 PLAN_NO_LONG = 0x4  # with PLAN_WAVE: keep long lane-capable histories in lane slices (CDR_PLAN_NO_LONG)
 CAP_LANE = 0x4
 CAP_REG = 0x8

@@ -547,9 +547,10 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
       const char* e = std::getenv("CDR_PAR_MAX");  // tuning override (slices)
       return (uint64_t)(e ? std::strtoul(e, nullptr, 0) : CDR_PAR_MAX_SLICES) * CDR_PAR_LANES;
     }();
-    if (pars.size() > par_max) {
-      lanes.insert(lanes.end(), pars.begin() + par_max, pars.end());
-      pars.resize(par_max);
+    const uint64_t pmax = (mode & CDR_PLAN_PAR_SOLO) ? (uint64_t)CDR_PAR_SOLO_MAX : par_max;
+    if (pars.size() > pmax) {
+      lanes.insert(lanes.end(), pars.begin() + pmax, pars.end());
+      pars.resize(pmax);
     }
   }
   {  // lane order: kernel group, length class (descending), then (register-table groups)
@@ -606,7 +607,9 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   }();
   uint32_t n_solo_len = 0;
   while (n_solo_len < pars.size() && wfs[pars[n_solo_len]].ev_len >= solo_len) n_solo_len++;
-  const uint32_t solo = std::min<uint32_t>(std::max(solo_max, n_solo_len), (uint32_t)pars.size());
+  // (CDR_PLAN_PAR_SOLO: every PAR history alone in its slice)
+  const uint32_t solo = (mode & CDR_PLAN_PAR_SOLO) ? (uint32_t)pars.size()
+                                                   : std::min<uint32_t>(std::max(solo_max, n_solo_len), (uint32_t)pars.size());
   // balanced PAR slices: a PAR slice's roles each walk its histories one at a time, so the
   // slice's time follows the summed lengths of its histories, and the kernel ends with its
   // heaviest slice (longest-first runs of 16 put the 16 longest histories in slice 0).

@@ -342,6 +342,12 @@ int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, ui
  * a slice, the first slices of the plan), where the class-decomposed kernel runs their
  * loops on four waves at once */
 #define CDR_PLAN_PAR 0x8u
+/* with CDR_PLAN_PAR: every PAR history alone in its slice, the CDR_PAR_SOLO_MAX longest at most —
+ * the plan of batches with task lists, whose PAR slices replay on k_replay_reg<TASKS>: a row there
+ * costs the union of the handler groups its lanes hit, so one history per slice steps one group
+ * (C5 --tasks 23.6 -> 16.0 ms; the PAR class kernel emits no tasks) */
+#define CDR_PLAN_PAR_SOLO 0x10u
+#define CDR_PAR_SOLO_MAX 512u
 #define CDR_PAR_LANES 16u /* histories per CDR_SLICE_PAR slice (lanes 0 .. 15; the rest empty) */
 #define CDR_PAR_SOLO 0u   /* ... except the longest CDR_PAR_SOLO, one per slice */
 #define CDR_PAR_SOLO_LEN 16384u /* ... and every PAR history at least this long, one per slice

@@ -323,6 +323,26 @@ def test_par_slices_plan():
     assert min(lo[c] for c in range(6) if hi[c]) >= len(par)
 
 
+def test_par_solo_plan():
+    """CDR_PLAN_PAR_SOLO (task batches): the same long register-table histories as CDR_PLAN_PAR,
+    each alone in lane 0 of its own PAR slice (the first slices, longest first), the 512 longest
+    at most; every entry still planned once."""
+    b = engine.synth_batch(4, 3000, seed=13)
+    pl = engine.plan(b)
+    lp, slen, _, fp = _plan(b, pl, abi.PLAN_WAVE | abi.PLAN_PAR)
+    ls, slen1, _, fs = _plan(b, pl, abi.PLAN_WAVE | abi.PLAN_PAR | abi.PLAN_PAR_SOLO)
+    par, par1 = np.nonzero(fp & abi.SLICE_PAR)[0], np.nonzero(fs & abi.SLICE_PAR)[0]
+    ws = sorted(int(x) for s in par for x in lp[s] if x >= 0)
+    assert (par1 == np.arange(len(par1))).all() and len(par1) == min(len(ws), 512)
+    assert all(ls[s][0] >= 0 and (ls[s][1:] == -1).all() for s in par1)
+    ws1 = [int(ls[s][0]) for s in par1]
+    assert len(ws) > 0 and (sorted(ws1) == ws if len(ws) <= 512 else len(ws1) == 512)
+    lens = [int(b.wfs[w].ev_len) for w in ws1]
+    assert lens == sorted(lens, reverse=True)
+    assert all(int(slen1[s]) == int(b.wfs[int(ls[s][0])].ev_len) for s in par1)
+    assert sorted(int(x) for x in ls.ravel() if x >= 0) == list(range(b.n_wfs))
+
+
 def test_par_slices_capped():
     """At most CDR_PAR_MAX_SLICES PAR slices (env CDR_PAR_MAX here, read once per process, so
     in a child process): the longest histories keep them, the rest return to the register-table
