@@ -240,12 +240,25 @@ __device__ __forceinline__ int alloc_initiated(const GAS Row* rows, uint32_t& hw
 // voffset: past the block, the load returns 0 without touching memory.
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #define OOB_BIT 0x80000000u
+// cache policy of a slab load (the buffer instruction's aux bits; gfx950: 2 = nt, a streaming
+// load whose lines the L2 may drop first).  The fast kernel reads each slab line once: its
+// loads stream (C2 -1.7%); the class kernels re-read rows of the original block at emission,
+// so theirs stay cached (nt on the class-block loads: C3 -3.2%, C4 +6.7%, C5 +7.2%; the fast
+// kernel's: C2 -1.5%, interleaved A/B in one process, profiles/r6_nt)
+#ifndef CDR_NT_FAST
+#define CDR_NT_FAST 2
+#endif
+#ifndef CDR_NT_CLS
+#define CDR_NT_CLS 0
+#endif
+template <int AUX = 0>
 __device__ __forceinline__ int64_t bld64(rsrc_t r, uint32_t voff, uint32_t soff) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, AUX);
   return (int64_t)(((uint64_t)v[1] << 32) | (uint64_t)v[0]);
 }
+template <int AUX = 0>
 __device__ __forceinline__ uint32_t bld32(rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX);
 }
 struct Slice {
   rsrc_t r;
@@ -266,8 +279,9 @@ struct Ev {
   int32_t n;
   int64_t id, ver, ts, key, aux;
 };
+template <int AUX = 0>
 __device__ __forceinline__ uint32_t load_tf(const Slice& S, uint32_t o8) {
-  return bld32(S.r, o8 - S.l4, S.col(CDR_COL_TYPE_FLAGS));
+  return bld32<AUX>(S.r, o8 - S.l4, S.col(CDR_COL_TYPE_FLAGS));
 }
 // need bit b of tf (CDR_SEF_NEED_*) clear -> OOB_BIT
 __device__ __forceinline__ uint32_t gate(uint32_t off, uint32_t tf, uint32_t bit) {
@@ -275,25 +289,25 @@ __device__ __forceinline__ uint32_t gate(uint32_t off, uint32_t tf, uint32_t bit
 }
 // DELTA: skip the event_id / version loads the packer's CDR_SEF_ID_NEXT / VER_SAME bits
 // make redundant (the consumer rebuilds them, ev_delta)
-template <bool DELTA = false>
+template <bool DELTA = false, int AUX = 0>
 __device__ __forceinline__ Ev load_ops(const Slice& S, uint32_t o8, uint32_t tf) {
   const uint32_t o4 = o8 - S.l4;
   Ev e;
   e.tf = tf;
-  e.id = bld64(S.r, DELTA ? o8 | ((tf & CDR_SEF_ID_NEXT) ? OOB_BIT : 0u) : o8, S.col(CDR_COL_EVENT_ID));
-  e.ver = bld64(S.r, DELTA ? o8 | ((tf & CDR_SEF_VER_SAME) ? OOB_BIT : 0u) : o8, S.col(CDR_COL_VERSION));
+  e.id = bld64<AUX>(S.r, DELTA ? o8 | ((tf & CDR_SEF_ID_NEXT) ? OOB_BIT : 0u) : o8, S.col(CDR_COL_EVENT_ID));
+  e.ver = bld64<AUX>(S.r, DELTA ? o8 | ((tf & CDR_SEF_VER_SAME) ? OOB_BIT : 0u) : o8, S.col(CDR_COL_VERSION));
 #if CDR_TYPED
-  e.ts = bld64(S.r, gate(o8, tf, CDR_SEF_NEED_TS), S.col(CDR_COL_TIMESTAMP));
-  e.key = bld64(S.r, gate(o8, tf, CDR_SEF_NEED_KEY), S.col(CDR_COL_KEY));
-  e.aux = bld64(S.r, gate(o8, tf, CDR_SEF_NEED_AUX), S.col(CDR_COL_AUX));
-  e.h = bld32(S.r, gate(o4, tf, CDR_SEF_NEED_H), S.col(CDR_COL_H));
-  e.n = (int32_t)bld32(S.r, gate(o4, tf, CDR_SEF_NEED_N), S.col(CDR_COL_N));
+  e.ts = bld64<AUX>(S.r, gate(o8, tf, CDR_SEF_NEED_TS), S.col(CDR_COL_TIMESTAMP));
+  e.key = bld64<AUX>(S.r, gate(o8, tf, CDR_SEF_NEED_KEY), S.col(CDR_COL_KEY));
+  e.aux = bld64<AUX>(S.r, gate(o8, tf, CDR_SEF_NEED_AUX), S.col(CDR_COL_AUX));
+  e.h = bld32<AUX>(S.r, gate(o4, tf, CDR_SEF_NEED_H), S.col(CDR_COL_H));
+  e.n = (int32_t)bld32<AUX>(S.r, gate(o4, tf, CDR_SEF_NEED_N), S.col(CDR_COL_N));
 #else
-  e.ts = bld64(S.r, o8, S.col(CDR_COL_TIMESTAMP));
-  e.key = bld64(S.r, o8, S.col(CDR_COL_KEY));
-  e.aux = bld64(S.r, o8, S.col(CDR_COL_AUX));
-  e.h = bld32(S.r, o4, S.col(CDR_COL_H));
-  e.n = (int32_t)bld32(S.r, o4, S.col(CDR_COL_N));
+  e.ts = bld64<AUX>(S.r, o8, S.col(CDR_COL_TIMESTAMP));
+  e.key = bld64<AUX>(S.r, o8, S.col(CDR_COL_KEY));
+  e.aux = bld64<AUX>(S.r, o8, S.col(CDR_COL_AUX));
+  e.h = bld32<AUX>(S.r, o4, S.col(CDR_COL_H));
+  e.n = (int32_t)bld32<AUX>(S.r, o4, S.col(CDR_COL_N));
 #endif
   return e;
 }

@@ -12,6 +12,8 @@
 #   tools/gpu.sh kstats   <tag> <configs...>      rocprofv3 kernel stats of C<n> steps
 #   tools/gpu.sh ab       <tag> <B> <configs...>  A/B step times: libcdr.so vs B (variant name or
 #                                                 env:VAR=value), A B A B per config
+#   tools/gpu.sh perfab   <tag> "<cfgs>" <libs>  interleaved in-process A/B of libcdr.so vs variant libs
+#                                                 (tools/perf.py; PERF_ARGS adds its flags)
 #   tools/gpu.sh multirank <tag>                  bench.py's multi-rank path, ranks sharing the GPU
 #   tools/gpu.sh ingest   <tag>                   on-device thriftrw decode -> replay (tools/ingest_bench.py)
 #   tools/gpu.sh calib    calib                   PMC calibration kernels (tools/calib.hip built into
@@ -82,6 +84,13 @@ for f in sorted(glob.glob(sys.argv[1] + "/c*_[AB]*.json")):
     print(f.rsplit("/", 1)[1], f"{d['ms_per_step']:.3f} ms/step kernel {d['roofline']['kernel_ms']:.3f} ms")
 EOF
     ;;
+  perfab)  # interleaved in-process A/B (tools/perf.py) per config: perfab <tag> "<configs>" <libs...>
+    cfgs=$1; shift
+    for c in $cfgs; do
+      $B 400 python -u tools/perf.py --config $c --rounds 4 $PERF_ARGS cadence_amd/libcdr.so "$@" > "$out/c$c.log" 2>&1 \
+        || { tail "$out/c$c.log"; exit 1; }
+      echo "C$c"; grep '"lib"' "$out/c$c.log"
+    done ;;
   multirank)
     export CDR_BENCH_BACKEND=gloo
     $B 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 \
