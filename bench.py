@@ -493,6 +493,39 @@ def canonical_event_bytes(batch) -> np.ndarray:
     return cum[off + ln] - cum[off]
 
 
+def carry_cpu_baseline(cfg, n_sample, seed, min_seconds=10.0):
+    """The carry line's CPU leg: oracle.replay of the second halves onto the first halves'
+    loaded states (the restated mutableStateBuilder.Load + applyEvents, mutableStateBuilder.go:
+    272-295, stateBuilder.go:112-611) on the box's host cores, over a sample split the way the
+    GPU line splits its population (engine.split_half); events counted as the GPU line counts
+    them (the suffixes')."""
+    import oracle
+    from cadence_amd import engine
+    b = engine.synth_batch(cfg, n_sample, seed)
+    cut = engine.split_half(b)
+    pre, _ = engine.cut_batches(b, cut)
+    th, how = host_cores()
+    pre_out = oracle.replay(pre, engine.plan(pre), threads=th)
+    suf = engine.suffix_batch(b, cut, pre, pre_out)
+    spl = engine.plan(suf)
+    n_ev = int(sum(int(suf.wfs[w].ev_len) for w in range(suf.n_wfs)))
+    res = {}
+    for t in (th, 1):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            oracle.replay(suf, spl, threads=t)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= (min_seconds if t == th else min_seconds / 4) or reps >= 200:
+                break
+        res[t] = n_ev * reps / el
+    return {"value": res[th], "unit": "events/s", "cores": th, "cores_source": how, "kind": "port",
+            "single_thread_events_per_s": res[1],
+            "sample": f"config {cfg}: {n_sample} workflows split at the call nearest their middle; the "
+                      f"second halves ({n_ev} events) replayed onto the first halves' oracle states, "
+                      f"repeatedly for >= {min_seconds:.0f} s"}
+
+
 def ndc_cpu_baseline(n_sample, seed, min_seconds=10.0):
     """configs[4]'s CPU leg: oracle.ndc_replicate (the restated stateRebuilder /
     conflict-resolution rounds, nDCConflictResolver.go:117-184, nDCStateRebuilder.go:92-160)
@@ -883,6 +916,7 @@ def carry_line(args):
                               zip(*np.unique(out_codes, return_counts=True))},
                    "parallelism": f"shard{world}"},
         "workflows_per_s": tot_wfs * args.steps / elapsed,
+        "cpu_baseline": None if (args.no_cpu_baseline or world > 1) else carry_cpu_baseline(cfg, 20000, seed),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS,
                      "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_note": tnote or traffic.get("source"),

@@ -32,7 +32,7 @@ def main():
                     help="replay only the histories of the full batch's first N PAR slices (PAR kernel alone)")
     ap.add_argument("--tasks", action="store_true", help="with the stateBuilder task lists (bench.py --tasks's batch)")
     ap.add_argument("--tasks-no-cls", action="store_true", help="--tasks without class blocks (k_replay_reg<TASKS>)")
-    ap.add_argument("--tasks-par", action="store_true", help="--tasks with the PAR plan (long histories on PAR slices)")
+    ap.add_argument("--tasks-par", action="store_true", help="--tasks with bench.py's task plan (long histories on PAR slices, one each)")
     ap.add_argument("--ab-cls", action="store_true",
                     help="each lib twice: class-decomposed register slices (k_replay_cls) on, then off")
     args = ap.parse_args()
@@ -53,7 +53,7 @@ def main():
                      | (abi.PLAN_NO_LONG if args.no_long else 0) | (0 if args.no_par else abi.PLAN_PAR),
                      ctx_for_cls=bctx) if not args.tasks else \
         DeviceBatch(torch, args.config, idx, 0x5EED0000 + args.config,
-                    plan_mode=abi.PLAN_WAVE | abi.PLAN_PAR if args.tasks_par else 0,
+                    plan_mode=abi.PLAN_WAVE | abi.PLAN_PAR | abi.PLAN_PAR_SOLO if args.tasks_par else 0,
                     cls=None if args.tasks_no_cls else "host", tasks=True)
     print(json.dumps({"cls_pack_s": round(db.cls_pack_s, 4), "cls_rows": db.cls_rows, "rows": db.info.n_rows}),
           flush=True)

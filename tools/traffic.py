@@ -15,8 +15,12 @@ of records) — real write traffic, not a miscount.  Counters are averaged over 
 an anchor kernel (a multi-kernel step: C3-C5 run several replay kernels per step), summed
 over every matching dispatch and divided by the anchor's dispatch count (one per step).
 Writes profiles/traffic_<workload>.json (and traffic_latest.json).
-usage: tools/traffic.py <tag> <workload> <profile-name> [kernel-substring] [anchor-kernel] [anchors per step]"""
+usage: tools/traffic.py <tag> <workload> <profile-name> [kernel-substring] [anchor-kernel] [anchors per step]
+env TRAFFIC_AFTER=<regex>: count only the dispatches from the first one whose kernel name matches
+(a bench line whose setup replays first: the carry line's prefix); TRAFFIC_EXCLUDE=<substring>:
+leave out matching kernels (the NDC line's closing k_digest)."""
 import collections
+import re
 import csv
 import glob
 import json
@@ -35,8 +39,17 @@ def main():
     nd = collections.defaultdict(set)
     steps = collections.defaultdict(set)  # per counter pass: the anchor's dispatches
     kernels = collections.defaultdict(set)
+    after = re.compile(os.environ["TRAFFIC_AFTER"]) if os.environ.get("TRAFFIC_AFTER") else None
+    excl = os.environ.get("TRAFFIC_EXCLUDE")
     for f in glob.glob(os.path.join(ROOT, "gpurun_out", f"{tag}_pmc", "*", "*counter_collection.csv")):
-        for r in csv.DictReader(open(f)):
+        rows = list(csv.DictReader(open(f)))
+        if after:  # this pass's first dispatch of the timed kernels (dispatch ids are per process)
+            ids = [int(r["Dispatch_Id"]) for r in rows if after.search(r["Kernel_Name"])]
+            first = min(ids) if ids else 1 << 62
+            rows = [r for r in rows if int(r["Dispatch_Id"]) >= first]
+        if excl:
+            rows = [r for r in rows if excl not in r["Kernel_Name"]]
+        for r in rows:
             if anchor and anchor in r["Kernel_Name"]:
                 steps[r["Counter_Name"]].add(r["Dispatch_Id"])
             if kern not in r["Kernel_Name"]:
