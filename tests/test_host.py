@@ -475,3 +475,23 @@ def test_lane_order_restated():
         exp_len = [max([int(lens[w]) for w in expect[s:s + 64] if w >= 0], default=0)
                    for s in range(0, len(expect), 64)]
         assert slen.tolist() == exp_len
+
+
+def test_bench_traffic_only_for_its_build(tmp_path, monkeypatch):
+    """bench.load_traffic uses a PMC summary only when it was collected on this very build of
+    libcdr.so (same SHA-1); another build's summary is reported stale, a missing one absent."""
+    import json
+    import bench
+    (tmp_path / "profiles").mkdir()
+    monkeypatch.setattr(bench, "HERE", str(tmp_path))
+    monkeypatch.setattr(bench, "lib_sha1", lambda: "a" * 40)
+    t, note = bench.load_traffic("C9-1wf-sliced")
+    assert t is None and "no PMC summary" in note
+    rec = {"workload": "C9-1wf-sliced", "lib_sha1": "b" * 40, "bytes_per_launch": 1.0e9}
+    (tmp_path / "profiles" / "traffic_C9-1wf-sliced.json").write_text(json.dumps(rec))
+    t, note = bench.load_traffic("C9-1wf-sliced")
+    assert t is None and "stale" in note
+    rec["lib_sha1"] = "a" * 40
+    (tmp_path / "profiles" / "traffic_C9-1wf-sliced.json").write_text(json.dumps(rec))
+    t, note = bench.load_traffic("C9-1wf-sliced")
+    assert t["bytes_per_launch"] == 1.0e9 and not note
