@@ -11,6 +11,7 @@
 
 #include "cdr/cdr.h"
 #include "ctx.h"
+#include "internal.h"
 
 extern "C" uint32_t cdr_get_plan_mode(const cdr_ctx* ctx);  // replay.hip
 
@@ -255,14 +256,13 @@ static int replay_host(cdr_ctx* ctx, const cdr_batch* b, const cdr_wf_caps* caps
   // the refresher's come from their own kernel after any replay
   const bool tasks = out->transfer != nullptr && !refresh;
   const uint32_t mode = tasks ? 0u : cdr_get_plan_mode(ctx);
-  int rc = cdr_plan_slices_ex(b->wfs, caps, b->n_wfs, mode, nullptr, nullptr, nullptr, nullptr, &ns, &rows, &n_wave);
+  cdr_internal::plan_vecs pv;  // one planning pass (the C ABI's size query + fill would plan twice)
+  int rc = cdr_internal::plan_slices_vec(b->wfs, caps, b->n_wfs, mode, pv, &ns, &rows, &n_wave);
   if (rc) return rc;
-  std::vector<int32_t> lane(ns * (size_t)CDR_SLICE_WIDTH);
-  std::vector<uint32_t> slen(ns), sflags(ns);
-  std::vector<uint64_t> row0(ns);
-  rc = cdr_plan_slices_ex(b->wfs, caps, b->n_wfs, mode, lane.data(), slen.data(), row0.data(), sflags.data(), &ns,
-                          &rows, &n_wave);
-  if (rc) return rc;
+  std::vector<int32_t>& lane = pv.lane_wf;
+  std::vector<uint32_t>& slen = pv.slice_len;
+  std::vector<uint32_t>& sflags = pv.slice_flags;
+  std::vector<uint64_t>& row0 = pv.slice_row0;
   const uint64_t ne = rows * CDR_SLICE_WIDTH;
   const uint64_t aw = cdr_plan_arena_words(b);
   // the packer writes every cell (padding included) and every arena word it names: staging

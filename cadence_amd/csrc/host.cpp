@@ -58,6 +58,43 @@ void parallel_for(uint64_t n, int threads, F&& f, uint64_t grain = 256, uint64_t
   for (auto& th : pool) th.join();
 }
 
+// std::stable_sort over `threads` host threads: contiguous chunks sorted in parallel, then
+// merged pairwise (std::merge takes the earlier chunk's element first on a tie), so the result
+// is the serial stable sort's, element for element
+template <class T, class Cmp>
+void par_stable_sort(std::vector<T>& v, Cmp cmp, int threads) {
+  const size_t n = v.size();
+  size_t t = (size_t)std::max(1, threads);
+  while (t > 1 && n / t < 32768) t >>= 1;
+  if (t <= 1) {
+    std::stable_sort(v.begin(), v.end(), cmp);
+    return;
+  }
+  std::vector<size_t> cut(t + 1);
+  for (size_t i = 0; i <= t; i++) cut[i] = n * i / t;
+  {
+    std::vector<std::thread> pool;
+    for (size_t i = 0; i < t; i++)
+      pool.emplace_back([&, i] { std::stable_sort(v.begin() + cut[i], v.begin() + cut[i + 1], cmp); });
+    for (auto& th : pool) th.join();
+  }
+  std::vector<T> buf(n);
+  std::vector<T>* src = &v;
+  std::vector<T>* dst = &buf;
+  for (size_t w = 1; w < t; w *= 2) {  // runs of w chunks -> runs of 2w chunks
+    std::vector<std::thread> pool;
+    for (size_t i = 0; i < t; i += 2 * w) {
+      const size_t a = cut[i], m = cut[std::min(t, i + w)], e = cut[std::min(t, i + 2 * w)];
+      pool.emplace_back([=] {
+        std::merge(src->begin() + a, src->begin() + m, src->begin() + m, src->begin() + e, dst->begin() + a, cmp);
+      });
+    }
+    for (auto& th : pool) th.join();
+    std::swap(src, dst);
+  }
+  if (src != &v) v.swap(*src);
+}
+
 }  // namespace
 
 
@@ -464,11 +501,11 @@ static int plan_caps_impl(const cdr_batch* b, cdr_wf_caps* caps, cdr_totals* tot
   return CDR_API_OK;
 }
 
-extern "C" {
-
-int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
-                       int32_t* lane_wf, uint32_t* slice_len, uint64_t* slice_row0, uint32_t* slice_flags,
-                       uint32_t* n_slices, uint64_t* n_rows, uint32_t* n_wave) {
+// cdr_plan_slices_ex's body; with `pv` set, the outputs go to its vectors (sized here: one
+// call plans and fills, where the C ABI takes a size query and a second call)
+static int plan_slices_impl(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
+                            cdr_internal::plan_vecs* pv, int32_t* lane_wf, uint32_t* slice_len, uint64_t* slice_row0,
+                            uint32_t* slice_flags, uint32_t* n_slices, uint64_t* n_rows, uint32_t* n_wave) {
   if (!wfs && n_wfs) return CDR_API_EINVAL;
   if ((mode & CDR_PLAN_WAVE) && !caps && n_wfs) return CDR_API_EINVAL;
   std::vector<uint32_t> lanes, waves, pars;
@@ -553,6 +590,7 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
       pars.resize(pmax);
     }
   }
+  std::vector<uint32_t> lane_len;  // ev_len of lanes[i] (0: padding)
   {  // lane order: kernel group, length class (descending), then (register-table groups)
      // entity counts, footprint and length, all descending; the keys are computed once per
      // entry (a log2 and the caps reads per comparison dominated the planner: C3 100k 145 ms)
@@ -568,28 +606,34 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
       const bool counts = caps && by_counts && g >= 1 && g <= 3;
       keys[i] = LaneKey{g, lclass(a), counts ? caps[a].order_key : 0u, slots(a), (uint64_t)wfs[a].ev_len, a};
     }
-    std::stable_sort(keys.begin(), keys.end(), [](const LaneKey& x, const LaneKey& y) {
+    // (on the host's threads: the serial sort was most of a 1M-entry plan)
+    par_stable_sort(keys, [](const LaneKey& x, const LaneKey& y) {
       if (x.group != y.group) return x.group < y.group;
       if (x.lclass != y.lclass) return x.lclass > y.lclass;
       if (x.counts != y.counts) return x.counts > y.counts;
       if (x.slots != y.slots) return x.slots > y.slots;
       return x.len > y.len;
-    });
+    }, std::min(hw_threads(0), 16));
     for (size_t i = 0; i < lanes.size(); i++) lanes[i] = keys[i].w;
-  }
-  std::stable_sort(waves.begin(), waves.end(), longer);
-  // each kernel group starts a slice of its own (a mixed slice would replay on the
-  // general kernel at the length of the next group's longest histories)
-  {
+    // each kernel group starts a slice of its own (a mixed slice would replay on the
+    // general kernel at the length of the next group's longest histories); the lanes' lengths
+    // ride along from the keys (the slice loop below would otherwise read every entry's
+    // descriptor again, in sorted — random — order)
     std::vector<uint32_t> padded;
     padded.reserve(lanes.size() + 3 * CDR_SLICE_WIDTH);
+    lane_len.reserve(lanes.size() + 3 * CDR_SLICE_WIDTH);
     for (size_t i = 0; i < lanes.size(); i++) {
-      if (i > 0 && group(lanes[i]) != group(lanes[i - 1]))
-        while (padded.size() % CDR_SLICE_WIDTH) padded.push_back(UINT32_MAX);
+      if (i > 0 && keys[i].group != keys[i - 1].group)
+        while (padded.size() % CDR_SLICE_WIDTH) {
+          padded.push_back(UINT32_MAX);
+          lane_len.push_back(0);
+        }
       padded.push_back(lanes[i]);
+      lane_len.push_back((uint32_t)keys[i].len);
     }
     lanes.swap(padded);
   }
+  std::stable_sort(waves.begin(), waves.end(), longer);
   // PAR slices first (slices 0 .. np - 1, CDR_PAR_LANES histories each: their P loop runs
   // one history at a time), then the lane slices, then the wave slices
   // (the CDR_PAR_SOLO longest get a slice each: a W step over one lane runs one handler group)
@@ -643,6 +687,16 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   const uint32_t np = solo + (uint32_t)((pars.size() - solo + CDR_PAR_LANES - 1) / CDR_PAR_LANES);
   const uint32_t nl = np + (uint32_t)((lanes.size() + CDR_SLICE_WIDTH - 1) / CDR_SLICE_WIDTH);
   const uint32_t nw = (uint32_t)waves.size();
+  if (pv) {
+    pv->lane_wf.resize((size_t)(nl + nw) * CDR_SLICE_WIDTH);
+    pv->slice_len.resize(nl + nw);
+    pv->slice_row0.resize(nl + nw);
+    pv->slice_flags.resize(nl + nw);
+    lane_wf = pv->lane_wf.data();
+    slice_len = pv->slice_len.data();
+    slice_row0 = pv->slice_row0.data();
+    slice_flags = pv->slice_flags.data();
+  }
   uint64_t rows = 0;
   for (uint32_t s = 0; s < nl; s++) {
     const std::vector<uint32_t>& src = s < np ? pars : lanes;
@@ -655,7 +709,7 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
     uint32_t len = 0;  // the slice's longest lane
     for (uint32_t l = 0; l < CDR_SLICE_WIDTH; l++) {
       const uint32_t w = at(l);
-      if (w != UINT32_MAX) len = std::max(len, (uint32_t)wfs[w].ev_len);
+      if (w != UINT32_MAX) len = std::max(len, s < np ? (uint32_t)wfs[w].ev_len : lane_len[first + l]);
     }
     if (slice_len) slice_len[s] = len;
     if (slice_row0) slice_row0[s] = rows;
@@ -682,6 +736,20 @@ int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t
   if (n_rows) *n_rows = rows;
   if (n_wave) *n_wave = nw;
   return CDR_API_OK;
+}
+
+int cdr_internal::plan_slices_vec(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
+                                  plan_vecs& out, uint32_t* n_slices, uint64_t* n_rows, uint32_t* n_wave) {
+  return plan_slices_impl(wfs, caps, n_wfs, mode, &out, nullptr, nullptr, nullptr, nullptr, n_slices, n_rows, n_wave);
+}
+
+extern "C" {
+
+int cdr_plan_slices_ex(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode,
+                       int32_t* lane_wf, uint32_t* slice_len, uint64_t* slice_row0, uint32_t* slice_flags,
+                       uint32_t* n_slices, uint64_t* n_rows, uint32_t* n_wave) {
+  return plan_slices_impl(wfs, caps, n_wfs, mode, nullptr, lane_wf, slice_len, slice_row0, slice_flags, n_slices,
+                          n_rows, n_wave);
 }
 
 int cdr_plan_slices(const cdr_wf_desc* wfs, uint32_t n_wfs, int32_t* lane_wf, uint32_t* slice_len,

@@ -28,6 +28,7 @@
 #include "cdr/cdr.h"
 #include "cdr/ingest.h"
 #include "ctx.h"
+#include "internal.h"
 
 #define HIPCHK(x)                                                                                     \
   do {                                                                                                \
@@ -1421,15 +1422,14 @@ extern "C" int cdr_ingest_plan(cdr_ctx* ctx, const cdr_ingest_out* dec, const cd
   // ---- the slice plan (host, per-entry records only)
   uint32_t ns = 0, n_wave = 0;
   uint64_t rows = 0;
-  if ((rc = cdr_plan_slices_ex(wfs.data(), caps, n, plan_mode, nullptr, nullptr, nullptr, nullptr, &ns, &rows,
-                               &n_wave)))
-    return rc;
-  std::vector<int32_t> lane(ns * (size_t)CDR_SLICE_WIDTH);
-  std::vector<uint32_t> slen(ns), sflags(ns), sc_act(ns), sc_tim(ns);
-  std::vector<uint64_t> row0(ns), sc_off(ns);
-  if ((rc = cdr_plan_slices_ex(wfs.data(), caps, n, plan_mode, lane.data(), slen.data(), row0.data(), sflags.data(),
-                               &ns, &rows, &n_wave)))
-    return rc;
+  cdr_internal::plan_vecs pv;  // one planning pass (the C ABI's size query + fill would plan twice)
+  if ((rc = cdr_internal::plan_slices_vec(wfs.data(), caps, n, plan_mode, pv, &ns, &rows, &n_wave))) return rc;
+  std::vector<int32_t>& lane = pv.lane_wf;
+  std::vector<uint32_t>& slen = pv.slice_len;
+  std::vector<uint32_t>& sflags = pv.slice_flags;
+  std::vector<uint64_t>& row0 = pv.slice_row0;
+  std::vector<uint32_t> sc_act(ns), sc_tim(ns);
+  std::vector<uint64_t> sc_off(ns);
   uint64_t sc_words = 0;
   uint32_t n_fast = 0;
   if ((rc = cdr_plan_scratch(caps, lane.data(), ns, sc_off.data(), sc_act.data(), sc_tim.data(), sflags.data(),

@@ -1,6 +1,7 @@
 // internal.h — helpers shared by the host-side translation units of libcdr.
 #pragma once
 #include <cstdint>
+#include <vector>
 
 #include "cdr/cdr.h"
 
@@ -39,5 +40,16 @@ void pack_chunked(const cdr_event* ev, uint64_t n_ev, uint64_t row0, uint32_t ro
                   const cdr_slices* o);
 void pack_lane(const cdr_event* ev, uint64_t n, uint64_t row0, uint32_t len, uint32_t lane, uint64_t apos,
                const cdr_slices* o);
+
+// cdr_plan_slices_ex in one call, its outputs in vectors sized by the plan (the host-buffer
+// pipeline and the device ingest plan once per batch instead of a size query and a fill)
+struct plan_vecs {
+  std::vector<int32_t> lane_wf;
+  std::vector<uint32_t> slice_len;
+  std::vector<uint64_t> slice_row0;
+  std::vector<uint32_t> slice_flags;
+};
+int plan_slices_vec(const cdr_wf_desc* wfs, const cdr_wf_caps* caps, uint32_t n_wfs, uint32_t mode, plan_vecs& out,
+                    uint32_t* n_slices, uint64_t* n_rows, uint32_t* n_wave);
 
 }  // namespace cdr_internal
