@@ -16,6 +16,14 @@ passes() {  # name limit bench-args...
       python3 bench.py "$@" $F > $out/${p%%:*}.log 2>&1 || { echo "pass ${p%%:*} of $name failed"; tail -5 $out/${p%%:*}.log; return 1; }
   done
 }
+if [ "$2" = extra ]; then  # the remaining lines: configs[3] at the count limit, C3 carry
+  passes ${tag}lg4 300 --config 4 --long-stride 125000 --steps 2 --warmup 0 &&
+  python3 tools/traffic.py ${tag}lg4 C4-1000000wf-sliced-long125000 ${tag}_c4_long k_replay k_tables > gpurun_out/${tag}_t_lg4.log &&
+  passes ${tag}cy3 300 --carry --config 3 --wfs 1000000 --steps 2 --warmup 0 &&
+  TRAFFIC_AFTER='k_replay_reg<.*, true, false>' python3 tools/traffic.py ${tag}cy3 C3-1000000wf-carry-half ${tag}_carry_c3 k_replay k_finalize > gpurun_out/${tag}_t_cy3.log &&
+  cp profiles/traffic_C4-1000000wf-sliced-long125000.json profiles/traffic_C3-1000000wf-carry-half.json gpurun_out/ && echo "pmc extra done"
+  exit $?
+fi
 passes ${tag}cy5 300 --carry --config 5 --wfs 1000000 --steps 2 --warmup 0 &&
 TRAFFIC_AFTER='k_replay_reg<.*, true, false>' python3 tools/traffic.py ${tag}cy5 C5-1000000wf-carry-half ${tag}_carry_c5 k_replay k_finalize > gpurun_out/${tag}_t_cy5.log &&
 passes ${tag}ct3 300 --carry --tasks --config 3 --wfs 1000000 --steps 2 --warmup 0 &&
