@@ -15,6 +15,14 @@
 
 #include "cdr/cdr.h"
 
+// k_tasks_merge's occupancy attribute (A/B builds: tools/build_variant.sh -DCDR_MERGE_ATTR=...)
+#ifndef CDR_MERGE_ATTR
+#define CDR_MERGE_ATTR
+#endif
+#ifndef CDR_MERGE_D2
+#define CDR_MERGE_D2 0 /* 1: each list keeps its head and one record after it (not two) */
+#endif
+
 // device workspace slots of the host-buffer pipeline (api.hip replay_host)
 enum cdr_ws_slot {
   WS_ROW0, WS_SLEN, WS_LANE, WS_SLAB, WS_ARENA, WS_SFLAGS, WS_SC_OFF, WS_SC_ACT, WS_SC_TIM, WS_SCRATCH,
@@ -100,8 +108,6 @@ struct cdr_ctx {
   void* hs[HS_NUM] = {};
   uint64_t hs_bytes[HS_NUM] = {};
   cdr_one_host one;
-  // k_replay_cls<TASKS>: the task slices' total rows of the last batch seen (its caps array
-  // and entry count), read back once per batch to size the staging lists
 };
 
 // pinned host staging `slot` of at least `bytes` (grow-only; contents undefined); nullptr

@@ -1827,7 +1827,7 @@ struct task_words {
 };
 static_assert(sizeof(cdr_task) == sizeof(task_words), "cdr_task words");
 template <uint32_t SFLAG>
-__global__ __launch_bounds__(CDR_SLICE_WIDTH) void k_tasks_merge(cdr_launch L) {
+__global__ __launch_bounds__(CDR_SLICE_WIDTH) CDR_MERGE_ATTR void k_tasks_merge(cdr_launch L) {
   (void)L;  // read through KA()
   const uint32_t s = blockIdx.x + KA()->s0;
   const uint32_t lane = threadIdx.x;
@@ -1875,7 +1875,7 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) void k_tasks_merge(cdr_launch L) {
   for (uint32_t c = 0; c < 4; c++) {
     hd[c] = ld(c, 0);
     nx[c] = ld(c, 1);
-    n2[c] = ld(c, 2);
+    if (!CDR_MERGE_D2) n2[c] = ld(c, 2);
     cur[c] = 0;
   }
   uint32_t n_xt = 0, n_tt = 0;
@@ -1933,9 +1933,9 @@ __global__ __launch_bounds__(CDR_SLICE_WIDTH) void k_tasks_merge(cdr_launch L) {
       const bool tk = on && c == j;
       if (tk) {
         hd[j] = nx[j];
-        nx[j] = n2[j];
+        nx[j] = CDR_MERGE_D2 ? ld(j, cur[j] + 2) : n2[j];
         cur[j]++;
-        n2[j] = ld(j, cur[j] + 2);
+        if (!CDR_MERGE_D2) n2[j] = ld(j, cur[j] + 2);
       }
     }
     coop_put<8>(dst, t, on && fits, 0);
